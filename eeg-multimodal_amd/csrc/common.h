@@ -1,0 +1,172 @@
+// common.h — shared device helpers for the EEG+action fusion path (gfx950 / CDNA4 only).
+//
+// Conventions used by every kernel in this directory:
+//   * element type T is either `float` (fp32 parity mode) or `bf16` (performance mode);
+//     accumulation is always fp32.
+//   * an MFMA "k32 fragment" is 8 consecutive contraction-axis elements held by one lane:
+//       lane l, group g = l >> 4, owns k = 8g .. 8g+7 of a 32-deep chunk,
+//       row/col index = l & 15 of a 16-wide tile.
+//     bf16 consumes it in one v_mfma_f32_16x16x32_bf16; fp32 consumes it as eight
+//     v_mfma_f32_16x16x4_f32 (lane group g feeds k = 8g+t to instruction t).  Both sum the
+//     same 32 products, so every kernel is written once for both precisions.
+//   * C/D layout of a 16x16 accumulator: col = l & 15, row = 4*(l >> 4) + reg.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(8))) float f32x8;
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+template <typename T> struct Frag8;
+template <> struct Frag8<bf16> { typedef bf16x8 type; };
+template <> struct Frag8<float> { typedef f32x8 type; };
+
+#define DEV __device__ __forceinline__
+
+DEV float to_f32(float x) { return x; }
+DEV float to_f32(bf16 x) { return (float)x; }
+template <typename T> DEV T from_f32(float x);
+template <> DEV float from_f32<float>(float x) { return x; }
+template <> DEV bf16 from_f32<bf16>(float x) { return (bf16)x; }
+
+DEV f32x4 mma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+DEV f32x4 mma16(f32x8 a, f32x8 b, f32x4 c) {
+#pragma unroll
+  for (int t = 0; t < 8; ++t) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t], b[t], c, 0, 0, 0);
+  return c;
+}
+
+// 8 contiguous elements (16-B aligned) from LDS or global.
+DEV bf16x8 ld_row8(const bf16* p) { return *(const bf16x8*)p; }
+DEV f32x8 ld_row8(const float* p) {
+  f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
+  f32x8 r;
+  r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
+  r[4] = b[0]; r[5] = b[1]; r[6] = b[2]; r[7] = b[3];
+  return r;
+}
+
+// 8 elements down a column of an LDS tile stored [k][col] with leading dimension ld:
+// returns tile[(k0 + j) * ld + c0 + (lane & 15)], j = 0..7.
+// bf16 uses two ds_read_b64_tr_b16 (lane 4q+p of a 16-group addresses row q, cols 4p..4p+3;
+// lane i receives column i of the 4 rows).  k0 may differ per 16-lane group.
+DEV bf16x8 ld_col8(const bf16* tile, int ld, int k0, int c0, int lane) {
+  const int i = lane & 15, q = i >> 2, p = i & 3;
+  const bf16* a0 = tile + (k0 + q) * ld + c0 + 4 * p;
+  const bf16* a1 = a0 + 4 * ld;
+  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)a0);
+  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)a1);
+  bf16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+DEV f32x8 ld_col8(const float* tile, int ld, int k0, int c0, int lane) {
+  f32x8 r;
+  const float* p = tile + k0 * ld + c0 + (lane & 15);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = p[j * ld];
+  return r;
+}
+
+// Same as ld_col8 but for a "split" k pattern: rows k0+0..3 and k1+0..3
+// (used when an accumulator tile is re-used as an operand; see attention kernels).
+DEV bf16x8 ld_col4x2(const bf16* tile, int ld, int k0, int k1, int c0, int lane) {
+  const int i = lane & 15, q = i >> 2, p = i & 3;
+  const bf16* a0 = tile + (k0 + q) * ld + c0 + 4 * p;
+  const bf16* a1 = tile + (k1 + q) * ld + c0 + 4 * p;
+  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)a0);
+  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)a1);
+  bf16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+DEV f32x8 ld_col4x2(const float* tile, int ld, int k0, int k1, int c0, int lane) {
+  f32x8 r;
+  const float* p0 = tile + k0 * ld + c0 + (lane & 15);
+  const float* p1 = tile + k1 * ld + c0 + (lane & 15);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { r[j] = p0[j * ld]; r[4 + j] = p1[j * ld]; }
+  return r;
+}
+
+// Pack two accumulator tiles (rows 4g+r of tile a and of tile b) into one k32 operand
+// fragment whose k order is {4g+0..3 of a, 4g+0..3 of b}.  The partner operand must use
+// the same permuted k order (ld_col4x2 with k0 = 4g, k1 = 16 + 4g).
+template <typename T> DEV typename Frag8<T>::type pack_acc(f32x4 a, f32x4 b);
+template <> DEV bf16x8 pack_acc<bf16>(f32x4 a, f32x4 b) {
+  bf16x8 r;
+  r[0] = (bf16)a[0]; r[1] = (bf16)a[1]; r[2] = (bf16)a[2]; r[3] = (bf16)a[3];
+  r[4] = (bf16)b[0]; r[5] = (bf16)b[1]; r[6] = (bf16)b[2]; r[7] = (bf16)b[3];
+  return r;
+}
+template <> DEV f32x8 pack_acc<float>(f32x4 a, f32x4 b) {
+  f32x8 r;
+  r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
+  r[4] = b[0]; r[5] = b[1]; r[6] = b[2]; r[7] = b[3];
+  return r;
+}
+
+// 16-byte vector load/store of raw bytes
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+DEV u32x4 ld16(const void* p) { return *(const u32x4*)p; }
+DEV void st16(void* p, u32x4 v) { *(u32x4*)p = v; }
+
+// wave reductions (64 lanes)
+DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+DEV float wave_min(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// XCD-aware bijective remap of a 1-D block id (blocks b and b+8 share an XCD under the
+// observed round-robin dispatch; this makes consecutive logical tiles share one XCD's L2).
+DEV int xcd_remap(int orig, int nwg) {
+  if (nwg < 16) return orig;
+  const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
+// ---------------------------------------------------------------------------------------
+// Counter-based RNG: Philox4x32-10 (Salmon et al., SC'11).  Every random draw in the path
+// (dropout masks, Laplace noise, Gumbel noise) is a pure function of (seed, stream, counter),
+// so forward and backward regenerate identical masks and the CPU oracle can replay them.
+// ---------------------------------------------------------------------------------------
+struct u32x4s { uint32_t x, y, z, w; };
+DEV uint32_t mulhilo(uint32_t a, uint32_t b, uint32_t* hi) {
+  uint64_t p = (uint64_t)a * (uint64_t)b;
+  *hi = (uint32_t)(p >> 32);
+  return (uint32_t)p;
+}
+DEV u32x4s philox4x32(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t hi0, hi1;
+    uint32_t lo0 = mulhilo(0xD2511F53u, c0, &hi0);
+    uint32_t lo1 = mulhilo(0xCD9E8D57u, c2, &hi1);
+    uint32_t n0 = hi1 ^ c1 ^ k0, n1 = lo1, n2 = hi0 ^ c3 ^ k1, n3 = lo0;
+    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  return {c0, c1, c2, c3};
+}
+// uniform in (0, 1]: (x + 1) * 2^-32 with x in [0, 2^32)  → never exactly 0
+DEV float u01_open0(uint32_t x) { return ((float)(x >> 8) + 1.0f) * (1.0f / 16777216.0f); }

@@ -1,0 +1,69 @@
+"""Build the HIP C-ABI library ``libeegfusion.so`` in-tree for gfx950.
+
+Each ``csrc/*.hip`` file is compiled separately (in parallel) with ``hipcc --offload-arch=gfx950``
+and linked into ``eegfusion/libeegfusion.so``.  Rebuilds are incremental on source/header mtimes.
+Run ``python -m eegfusion.build`` (with ``eeg-multimodal_amd`` on ``sys.path``) or call
+``build()``.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+PKG_DIR = Path(__file__).resolve().parent
+ROOT = PKG_DIR.parent                    # eeg-multimodal_amd/
+CSRC = ROOT / "csrc"
+INCLUDE = ROOT.parent / "include"
+OBJ_DIR = ROOT / "build"
+LIB_PATH = PKG_DIR / "libeegfusion.so"
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=fast",
+          "-Wno-unused-result", f"-I{INCLUDE}", f"-I{CSRC}"]
+
+
+def _headers() -> list[Path]:
+    return sorted(CSRC.glob("*.h")) + sorted(INCLUDE.glob("*.h"))
+
+
+def _needs(target: Path, deps: list[Path]) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(d.stat().st_mtime > t for d in deps)
+
+
+def _compile(src: Path, hdrs: list[Path], verbose: bool) -> Path:
+    obj = OBJ_DIR / (src.stem + ".o")
+    if _needs(obj, [src, *hdrs]):
+        cmd = [HIPCC, *CFLAGS, "-c", str(src), "-o", str(obj)]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stdout}\n{r.stderr}")
+    return obj
+
+
+def build(verbose: bool = False, jobs: int | None = None) -> Path:
+    OBJ_DIR.mkdir(exist_ok=True)
+    srcs = sorted(CSRC.glob("*.hip"))
+    hdrs = _headers()
+    jobs = jobs or min(8, len(srcs), os.cpu_count() or 4)
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        objs = list(ex.map(lambda s: _compile(s, hdrs, verbose), srcs))
+    if _needs(LIB_PATH, objs):
+        cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", str(LIB_PATH), *map(str, objs)]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+    return LIB_PATH
+
+
+if __name__ == "__main__":
+    print(build(verbose="-v" in sys.argv))

@@ -1,0 +1,131 @@
+"""GPU numerics of the MFMA GEMM (eegf_gemm) against a float64 torch reference of the same op.
+
+Tolerances: fp32 path ≤ 1e-4·(1+|ref|) per element (exact-f32 MFMA, k-permuted summation);
+bf16 path ≤ 2e-2·max|ref| (bf16 operands, fp32 accumulation).
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _k():
+    from eegfusion import kernels
+    return kernels
+
+
+def _ref_epi(v, epi, bias, aux, scale):
+    if epi in ("bias", "bias_gelu", "bias_relu", "bias_tanh"):
+        v = v + bias.double()
+    if epi == "bias_gelu":
+        return torch.nn.functional.gelu(v), v
+    if epi == "bias_relu":
+        return torch.relu(v), None
+    if epi == "bias_tanh":
+        return torch.tanh(v), None
+    if epi == "dgelu":
+        x = aux.double()
+        g = 0.5 * (1 + torch.erf(x / 2 ** 0.5)) + x * torch.exp(-0.5 * x * x) / (2 * torch.pi) ** 0.5
+        return v * g, None
+    if epi == "drelu":
+        return v * (aux.double() > 0) * scale, None
+    if epi == "dtanh":
+        return v * (1 - aux.double() ** 2), None
+    return v, None
+
+
+def _check(out, ref, dt):
+    out = out.double()
+    if dt == torch.float32:
+        err = ((out - ref).abs() / (1 + ref.abs())).max().item()
+        assert err <= 1e-4, err
+    else:
+        err = (out - ref).abs().max().item() / max(ref.abs().max().item(), 1e-6)
+        assert err <= 2e-2, err
+
+
+SHAPES = [(256, 768, 768), (300, 200, 96), (128, 2, 768), (64, 2304, 2304), (1000, 130, 72), (33, 17, 8)]
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,N,K", SHAPES)
+@pytest.mark.parametrize("layout", ["fwd", "dgrad", "wgrad", "tn"])
+def test_gemm_layouts(dt, M, N, K, layout):
+    k = _k()
+    torch.manual_seed(0)
+    dev = "cuda"
+    # logical A[M,K], B[K,N]
+    A = torch.randn(M, K, device=dev).to(dt)
+    B = torch.randn(K, N, device=dev).to(dt)
+    ref = A.double() @ B.double()
+    outdt = torch.float32 if (dt == torch.float32 or layout == "wgrad") else dt
+    C = torch.empty(M, N, device=dev, dtype=outdt)
+    if layout == "fwd":        # A [M,K] row-major, B stored [N,K]
+        Bs = B.t().contiguous()
+        k.gemm(A, Bs, C, M=M, N=N, K=K, a_kc=1, b_kc=1, lda=K, ldb=K, ldc=N)
+    elif layout == "dgrad":    # A [M,K], B stored [K,N]
+        k.gemm(A, B.contiguous(), C, M=M, N=N, K=K, a_kc=1, b_kc=0, lda=K, ldb=N, ldc=N)
+    elif layout == "wgrad":    # A stored [K,M], B stored [K,N]
+        k.gemm(A.t().contiguous(), B.contiguous(), C, M=M, N=N, K=K, a_kc=0, b_kc=0, lda=M, ldb=N, ldc=N)
+    else:                      # A stored [K,M], B stored [N,K]
+        k.gemm(A.t().contiguous(), B.t().contiguous(), C, M=M, N=N, K=K, a_kc=0, b_kc=1, lda=M, ldb=K, ldc=N)
+    torch.cuda.synchronize()
+    _check(C, ref, dt if outdt != torch.float32 or dt == torch.float32 else torch.bfloat16)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("epi", ["bias", "bias_gelu", "bias_relu", "bias_tanh"])
+def test_gemm_fwd_epilogues(dt, epi):
+    k = _k()
+    torch.manual_seed(1)
+    M, N, K = 260, 300, 192
+    x = (torch.randn(M, K, device="cuda") * 0.3).to(dt)
+    w = (torch.randn(N, K, device="cuda") * 0.3).to(dt)
+    b = torch.randn(N, device="cuda")
+    aux = torch.empty(M, N, device="cuda", dtype=dt) if epi == "bias_gelu" else None
+    out = k.linear(x, w, b, epi=epi, aux=aux)
+    torch.cuda.synchronize()
+    ref, pre = _ref_epi(x.double() @ w.double().t(), epi, b, None, 1.0)
+    _check(out, ref, dt)
+    if pre is not None:
+        _check(aux, pre, dt)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("epi", ["dgelu", "drelu", "dtanh"])
+def test_gemm_dgrad_epilogues(dt, epi):
+    k = _k()
+    torch.manual_seed(2)
+    M, N, K = 260, 300, 192
+    dy = torch.randn(M, N, device="cuda").to(dt)
+    w = (torch.randn(N, K, device="cuda") * 0.2).to(dt)
+    aux = torch.randn(M, K, device="cuda").to(dt)
+    if epi == "dtanh":
+        aux = torch.tanh(aux.float()).to(dt)
+    out = k.linear_dgrad(dy, w, epi=epi, aux=aux, epi_scale=1.25)
+    torch.cuda.synchronize()
+    ref, _ = _ref_epi(dy.double() @ w.double(), epi, None, aux, 1.25)
+    _check(out, ref, dt)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_gemm_wgrad_beta_and_batch(dt):
+    k = _k()
+    torch.manual_seed(3)
+    M, N, K = 515, 96, 136
+    dy = torch.randn(M, N, device="cuda").to(dt)
+    x = torch.randn(M, K, device="cuda").to(dt)
+    dw = torch.randn(N, K, device="cuda")
+    ref = dw.double() * 0.5 + dy.double().t() @ x.double()
+    k.linear_wgrad(dy, x, dw, beta=0.5)
+    torch.cuda.synchronize()
+    _check(dw, ref, dt)
+    # batched (z) strided: 3 independent products
+    Z = 3
+    A = torch.randn(Z, 70, 64, device="cuda").to(dt)
+    B = torch.randn(Z, 50, 64, device="cuda").to(dt)
+    C = torch.empty(Z, 70, 50, device="cuda", dtype=torch.float32 if dt == torch.float32 else dt)
+    k.gemm(A, B, C, M=70, N=50, K=64, a_kc=1, b_kc=1, lda=64, ldb=64, ldc=50, batch=Z,
+           sA=70 * 64, sB=50 * 64, sC=70 * 50)
+    torch.cuda.synchronize()
+    _check(C, A.double() @ B.double().transpose(1, 2), dt)
