@@ -1,0 +1,281 @@
+"""CPU oracle for the EEG+action fusion training path — TEST INFRASTRUCTURE ONLY.
+
+A plain torch-CPU fp32 restatement (no `transformers`, no HIP) of the reference computation,
+used by tests/, `__graft_entry__.smoke()` and the `cpu_baseline` leg of bench.py as the checker.
+The product path (eeg-multimodal_amd/eegfusion) never imports this module.
+
+Pinned against golden vectors produced by running the reference itself in the survey container
+(tests/golden/make_golden.py → tests/golden/*.npz; checked by tests/test_oracle_golden.py).
+
+Follows, line by line:
+  * BERT encoder: transformers 5.15.0 `modeling_bert.py` BertEmbeddings :53-106 (word/pos/type +
+    LayerNorm 1e-12), BertSelfAttention :139-199 (12 heads x 64, scale 1/8, additive key mask),
+    BertSelfOutput :282-293, BertIntermediate/BertOutput :325-351 (GELU-erf), BertPooler :451-462.
+  * decoder: torch 2.10 `nn/modules/transformer.py` TransformerDecoderLayer (post-norm, ReLU,
+    d_ff 2048, LN 1e-5) :1100-1200 and `F.multi_head_attention_forward` (literal q/k/v form).
+  * fusion + privacy: model.py:34-64, past_acc.py:108-139, main_0430.py:76-123,
+    python/src/custom_models/models.py:56-82.
+  * gumbel_softmax: torch/nn/functional.py gumbel_softmax (soft + straight-through hard).
+  * Laplace sampling: torch/distributions/laplace.py:83-86 (u ~ U[eps-1, 1); loc - scale*sign(u)*log1p(-|u|)).
+Dropout is p=0 in parity mode (the reference's dropout draws come from torch's RNG and cannot be
+replayed); the HIP path's own dropout is checked separately through its Philox stream.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+import torch.nn.functional as F
+
+HID, NHEAD, DHEAD, FFN, NLAYER = 768, 12, 64, 3072, 12
+DEC_FF, DEC_LAYERS = 2048, 3
+LN_BERT, LN_DEC = 1e-12, 1e-5
+FUSED = 3 * HID
+
+
+@dataclass
+class PathConfig:
+    contract: str = "W"          # "W": window (eeg [B,C,T] f32, act [B,32]); "T": token ids (L=512) + CLIP [B,1,512]
+    variant: str = "prigumbel"   # "concat" (model.py), "priconcat" (main_0430.py), "prigumbel" (past_acc.py)
+    eps: float = 1.0
+    eps_mode: str = "newfrac"    # "newfrac": 1/ln((e^eps-w)/(1-w)) (past_acc.py:132); "new": ln(...) (model.py:57)
+    hard: bool = False
+    honor_dp_mode: bool = False  # PriConcat: apply DP_guarantee('feature_all_lap') (main_0430.py:76-85)
+
+
+# ------------------------------------------------------------------------------ BERT (a4)
+def _ln(x, w, b, eps):
+    return F.layer_norm(x, (x.shape[-1],), w, b, eps)
+
+
+def _lin(x, p, name):
+    return F.linear(x, p[name + ".weight"], p.get(name + ".bias"))
+
+
+def bert_embeddings(p, *, input_ids=None, inputs_embeds=None):
+    """BertEmbeddings.forward (modeling_bert.py:68-106): word|embeds + type[0] + pos, LN 1e-12."""
+    pre = "bert.embeddings."
+    if inputs_embeds is None:
+        inputs_embeds = p[pre + "word_embeddings.weight"][input_ids]
+    L = inputs_embeds.shape[1]
+    x = inputs_embeds + p[pre + "token_type_embeddings.weight"][0] + p[pre + "position_embeddings.weight"][:L]
+    return _ln(x, p[pre + "LayerNorm.weight"], p[pre + "LayerNorm.bias"], LN_BERT)
+
+
+def bert_layer(p, i, h, key_bias):
+    """BertLayer (modeling_bert.py:354-417) with eager attention (:111-136) semantics."""
+    pre = f"bert.encoder.layer.{i}."
+    B, L, _ = h.shape
+
+    def heads(t):
+        return t.view(B, L, NHEAD, DHEAD).transpose(1, 2)
+
+    q = heads(_lin(h, p, pre + "attention.self.query"))
+    k = heads(_lin(h, p, pre + "attention.self.key"))
+    v = heads(_lin(h, p, pre + "attention.self.value"))
+    s = q @ k.transpose(-1, -2) * (DHEAD ** -0.5) + key_bias[:, None, None, :]
+    ctx = (s.softmax(-1) @ v).transpose(1, 2).reshape(B, L, HID)
+    a = _ln(_lin(ctx, p, pre + "attention.output.dense") + h,
+            p[pre + "attention.output.LayerNorm.weight"], p[pre + "attention.output.LayerNorm.bias"], LN_BERT)
+    f = F.gelu(_lin(a, p, pre + "intermediate.dense"))
+    return _ln(_lin(f, p, pre + "output.dense") + a,
+               p[pre + "output.LayerNorm.weight"], p[pre + "output.LayerNorm.bias"], LN_BERT)
+
+
+def bert(p, emb, attention_mask):
+    """BertModel.forward (modeling_bert.py:623-686) → (sequence_output, pooled_output)."""
+    key_bias = torch.zeros(attention_mask.shape, dtype=emb.dtype)
+    key_bias = key_bias.masked_fill(attention_mask == 0, torch.finfo(emb.dtype).min)
+    h = emb
+    for i in range(NLAYER):
+        h = bert_layer(p, i, h, key_bias)
+    pooled = torch.tanh(_lin(h[:, 0], p, "bert.pooler.dense"))
+    return h, pooled
+
+
+# -------------------------------------------------------------------------- decoder (a5)
+def mha_literal(x, mem, in_w, in_b, out_w, out_b, key_padding_mask):
+    """F.multi_head_attention_forward, batch-major: x [B,Lq,E], mem [B,S,E]; mask True = ignore."""
+    B, Lq, E = x.shape
+    S = mem.shape[1]
+    wq, wk, wv = in_w.chunk(3)
+    bq, bk, bv = in_b.chunk(3)
+    q = F.linear(x, wq, bq).view(B, Lq, NHEAD, DHEAD).transpose(1, 2)
+    k = F.linear(mem, wk, bk).view(B, S, NHEAD, DHEAD).transpose(1, 2)
+    v = F.linear(mem, wv, bv).view(B, S, NHEAD, DHEAD).transpose(1, 2)
+    s = (q * DHEAD ** -0.5) @ k.transpose(-1, -2)
+    if key_padding_mask is not None:
+        s = s.masked_fill(key_padding_mask[:, None, None, :], float("-inf"))
+    ctx = (s.softmax(-1) @ v).transpose(1, 2).reshape(B, Lq, E)
+    return F.linear(ctx, out_w, out_b)
+
+
+def decoder_layer(p, i, x, mem, mem_pad, tgt_pad):
+    """TransformerDecoderLayer.forward, norm_first=False (transformer.py:1158-1200)."""
+    pre = f"multi_head_decoder.layers.{i}."
+    sa = mha_literal(x, x, p[pre + "self_attn.in_proj_weight"], p[pre + "self_attn.in_proj_bias"],
+                     p[pre + "self_attn.out_proj.weight"], p[pre + "self_attn.out_proj.bias"], tgt_pad)
+    x = _ln(x + sa, p[pre + "norm1.weight"], p[pre + "norm1.bias"], LN_DEC)
+    ca = mha_literal(x, mem, p[pre + "multihead_attn.in_proj_weight"], p[pre + "multihead_attn.in_proj_bias"],
+                     p[pre + "multihead_attn.out_proj.weight"], p[pre + "multihead_attn.out_proj.bias"], mem_pad)
+    x = _ln(x + ca, p[pre + "norm2.weight"], p[pre + "norm2.bias"], LN_DEC)
+    ff = _lin(F.relu(_lin(x, p, pre + "linear1")), p, pre + "linear2")
+    return _ln(x + ff, p[pre + "norm3.weight"], p[pre + "norm3.bias"], LN_DEC)
+
+
+def decoder(p, tgt, mem, mem_mask, tgt_mask):
+    """multi_head_decoder(tgt, memory, tgt_key_padding_mask, memory_key_padding_mask)
+    followed by .permute(1,0,2).mean(dim=1) (model.py:40-44)."""
+    x = tgt
+    for i in range(DEC_LAYERS):
+        x = decoder_layer(p, i, x, mem, mem_mask == 0, tgt_mask == 0)
+    return x.mean(dim=1)
+
+
+# --------------------------------------------------------------------- fusion + privacy
+def minmax(f):
+    """Row-wise min-max normalisation, no epsilon (model.py:47-50; past_acc.py:121-123)."""
+    fmin = f.min(dim=-1, keepdim=True)[0]
+    fmax = f.max(dim=-1, keepdim=True)[0]
+    return (f - fmin) / (fmax - fmin)
+
+
+def eps_hat(w, eps, mode):
+    a = torch.tensor(math.exp(eps), dtype=torch.float32)
+    r = ((a - w) / (1 - w)).log()
+    return 1.0 / r if mode == "newfrac" else r
+
+
+def gumbel_softmax_injected(logits, gumbels, hard, tau=1.0, dim=0):
+    """torch.nn.functional.gumbel_softmax with the -log(Exp(1)) draws supplied."""
+    y_soft = ((logits + gumbels) / tau).softmax(dim)
+    if not hard:
+        return y_soft
+    index = y_soft.max(dim, keepdim=True)[1]
+    y_hard = torch.zeros_like(logits).scatter_(dim, index, 1.0)
+    return y_hard - y_soft.detach() + y_soft
+
+
+def prigumbel_gate(feature, DP, noise, gumbels, eps, mode, hard):
+    """past_acc.py:130-136 / models.py:73-79."""
+    w = torch.sigmoid(DP)
+    y = feature + noise * eps_hat(w, eps, mode)
+    logits = torch.stack((w, 1 - w)).repeat(1, feature.shape[0], 1)
+    mask = gumbel_softmax_injected(logits, gumbels, hard)
+    return (y * mask).sum(0)
+
+
+def dp_guarantee(feature, row_noise, honor):
+    """main_0430.py:76-85: identity for dp_mode=None (as ConcatModel.forward calls it, :118);
+    'feature_all_lap': min-max then one Laplace(0, 1/eps) scalar per row."""
+    if not honor:
+        return feature
+    return minmax(feature) + row_noise.view(-1, 1)
+
+
+def laplace_from_uniform(u, scale=1.0):
+    """torch Laplace.rsample (laplace.py:83-86) given u ~ U[finfo.eps - 1, 1)."""
+    return -scale * u.sign() * torch.log1p(-u.abs())
+
+
+def head(p, f):
+    """fc_layers + classifier (model.py:24-32,62-63)."""
+    h = torch.relu(_lin(f, p, "fc_layers.0"))
+    h = torch.tanh(_lin(h, p, "fc_layers.2"))
+    return _lin(h, p, "classifier")
+
+
+# ---------------------------------------------------------------------------- full path
+def encoders(p, batch, cfg: PathConfig):
+    """→ (pooled [B,768], img [B,768], cross [B,768])."""
+    if cfg.contract == "W":
+        eeg, act = batch["eeg"], batch["act"]                      # [B,C,T], [B,A]
+        tokens = eeg.transpose(1, 2)                               # time-major [B,T,C]
+        emb = bert_embeddings(p, inputs_embeds=_lin(tokens, p, "eeg_encoder"))
+        mask = batch.get("eeg_mask", torch.ones(eeg.shape[0], eeg.shape[2], dtype=torch.long))
+        vis = _lin(act.unsqueeze(1), p, "visual_encoder")          # [B,1,768]
+        vmask = torch.ones(eeg.shape[0], 1, dtype=torch.long)
+    else:
+        emb = bert_embeddings(p, input_ids=batch["title_input"])
+        mask = batch["text_mask"]
+        vis = _lin(batch["frame_input"], p, "visual_encoder")
+        vmask = batch["vedio_mask"]
+    seq, pooled = bert(p, emb, mask)
+    cross = decoder(p, vis, seq, mask, vmask)
+    return pooled, vis.squeeze(1), cross
+
+
+def forward(p, batch, cfg: PathConfig, noise=None, gumbels=None, row_noise=None, return_feature=False):
+    pooled, img, cross = encoders(p, batch, cfg)
+    f = torch.cat((pooled, img, cross), dim=1)                     # [B,2304]: EEG || action || cross
+    if cfg.variant == "priconcat":
+        g = dp_guarantee(f, row_noise, cfg.honor_dp_mode)
+    elif cfg.variant == "concat":
+        g = minmax(f)
+    else:
+        g = prigumbel_gate(minmax(f), p["DP"], noise, gumbels, cfg.eps, cfg.eps_mode, cfg.hard)
+    logits = head(p, g)
+    return (logits, f, g) if return_feature else logits
+
+
+def cal_loss(logits, labels):
+    """past_acc.py:71-77 (mean CE, argmax accuracy)."""
+    loss = F.cross_entropy(logits, labels)
+    acc = (logits.argmax(1) == labels).float().mean()
+    return loss, acc
+
+
+# -------------------------------------------------------------- parameter inventory
+def param_shapes(contract: str = "W", variant: str = "prigumbel", eeg_channels=64, act_dim=32) -> dict:
+    """state_dict names/shapes of the path (reference names, SURVEY Appendix A.6 / probe7)."""
+    s = {}
+    e = "bert.embeddings."
+    s[e + "word_embeddings.weight"] = (30522, HID)
+    s[e + "position_embeddings.weight"] = (512, HID)
+    s[e + "token_type_embeddings.weight"] = (2, HID)
+    s[e + "LayerNorm.weight"] = (HID,)
+    s[e + "LayerNorm.bias"] = (HID,)
+    for i in range(NLAYER):
+        pre = f"bert.encoder.layer.{i}."
+        for n in ("attention.self.query", "attention.self.key", "attention.self.value", "attention.output.dense"):
+            s[pre + n + ".weight"] = (HID, HID)
+            s[pre + n + ".bias"] = (HID,)
+        for n in ("attention.output.LayerNorm", "output.LayerNorm"):
+            s[pre + n + ".weight"] = (HID,)
+            s[pre + n + ".bias"] = (HID,)
+        s[pre + "intermediate.dense.weight"] = (FFN, HID)
+        s[pre + "intermediate.dense.bias"] = (FFN,)
+        s[pre + "output.dense.weight"] = (HID, FFN)
+        s[pre + "output.dense.bias"] = (HID,)
+    s["bert.pooler.dense.weight"] = (HID, HID)
+    s["bert.pooler.dense.bias"] = (HID,)
+    if contract == "W":
+        s["eeg_encoder.weight"] = (HID, eeg_channels)
+        s["eeg_encoder.bias"] = (HID,)
+        s["visual_encoder.weight"] = (HID, act_dim)
+    else:
+        s["visual_encoder.weight"] = (HID, 512)
+    s["visual_encoder.bias"] = (HID,)
+    for pre in ["multi_head_decoderlayer."] + [f"multi_head_decoder.layers.{i}." for i in range(DEC_LAYERS)]:
+        for a in ("self_attn", "multihead_attn"):
+            s[pre + a + ".in_proj_weight"] = (3 * HID, HID)
+            s[pre + a + ".in_proj_bias"] = (3 * HID,)
+            s[pre + a + ".out_proj.weight"] = (HID, HID)
+            s[pre + a + ".out_proj.bias"] = (HID,)
+        s[pre + "linear1.weight"] = (DEC_FF, HID)
+        s[pre + "linear1.bias"] = (DEC_FF,)
+        s[pre + "linear2.weight"] = (HID, DEC_FF)
+        s[pre + "linear2.bias"] = (HID,)
+        for n in ("norm1", "norm2", "norm3"):
+            s[pre + n + ".weight"] = (HID,)
+            s[pre + n + ".bias"] = (HID,)
+    s["fc_layers.0.weight"] = (FUSED, FUSED)
+    s["fc_layers.0.bias"] = (FUSED,)
+    s["fc_layers.2.weight"] = (HID, FUSED)
+    s["fc_layers.2.bias"] = (HID,)
+    s["classifier.weight"] = (2, HID)
+    s["classifier.bias"] = (2,)
+    if variant in ("prigumbel", "concat"):
+        s["DP"] = (1, FUSED)
+    return s

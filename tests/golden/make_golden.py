@@ -1,0 +1,341 @@
+"""Generate golden vectors by running the REFERENCE itself (survey container only).
+
+Imports the reference's own modules from /root/reference (read-only) — past_acc.py,
+main_0430.py, model.py — with the survey's shims:
+  * `opacus` stubbed (PrivacyEngine is not on the hot path), `transformers.AdamW` aliased;
+  * `BertModel.from_pretrained('bert-base-uncased')` replaced by a local `BertModel(BertConfig())`
+    constructor (bert-base geometry, sdpa attention) — no network fetch, weights then overwritten
+    with closed-form deterministic values (oracle/detweights.py);
+  * contract W: the reference's BERT call receives the EEG window in place of `title_input`; a
+    wrapper applies the per-time-step `eeg_encoder` Linear(64,768) and calls the reference BertModel
+    with `inputs_embeds=`; `visual_encoder` is Linear(32,768).  Everything downstream (decoder,
+    fusion, min-max, Laplace/Gumbel gate, fc head) is the reference's own forward code.
+  * dropout p=0 everywhere (the reference's dropout RNG cannot be replayed), Laplace noise
+    injected through `model.noiser.sample`, Gumbel draws recorded from the reference's own
+    `gumbel_softmax` call (by wrapping `Tensor.exponential_`).
+The reference's pickled feature files are NOT loaded (no code-free loader exists for them):
+contract-T fixtures use synthetic token ids / CLIP-like vectors of the same shapes.
+
+Outputs: tests/golden/*.npz (inputs, injected draws, outputs, gradient checksums and samples).
+Run:  python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import json
+import math
+import sys
+import types
+from pathlib import Path
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+HERE = Path(__file__).resolve().parent
+ROOT = HERE.parents[1]
+REF = Path("/root/reference")
+sys.path.insert(0, str(ROOT))
+from oracle.detweights import det_tensor, sample_positions  # noqa: E402
+
+SEED = 20240501
+B_W, C_W, T_W, A_W = 2, 64, 256, 32
+
+
+def import_reference():
+    sys.modules.setdefault("opacus", types.SimpleNamespace(PrivacyEngine=object))
+    import transformers
+    from transformers import BertConfig, BertModel
+    setattr(sys.modules["transformers"], "AdamW", torch.optim.AdamW)
+
+    def _local(cls, name, *a, **k):
+        return cls(BertConfig(attn_implementation="sdpa"))
+
+    BertModel.from_pretrained = classmethod(_local)
+    sys.path.insert(0, str(REF))
+    import main_0430
+    import model as ref_model
+    import past_acc
+    past_acc.device = torch.device("cpu")
+    return past_acc, main_0430, ref_model
+
+
+class WindowBert(nn.Module):
+    """Contract W front-end around the reference BertModel."""
+
+    def __init__(self, bert, eeg_encoder):
+        super().__init__()
+        self.bert = bert
+        self.eeg_encoder = eeg_encoder
+
+    def forward(self, input_ids=None, attention_mask=None, return_dict=False):
+        emb = self.eeg_encoder(input_ids.transpose(1, 2))
+        return self.bert(inputs_embeds=emb, attention_mask=attention_mask, return_dict=return_dict)
+
+
+def canon(name: str) -> str:
+    return name.replace("bert.bert.", "bert.").replace("bert.eeg_encoder.", "eeg_encoder.")
+
+
+def prepare(m: nn.Module, contract: str, dp=None):
+    if contract == "W":
+        m.bert = WindowBert(m.bert, nn.Linear(C_W, 768))
+        m.visual_encoder = nn.Linear(A_W, 768)
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            cn = canon(n)
+            if cn == "DP":
+                p.copy_(torch.as_tensor(dp if dp is not None else np.zeros((1, 2304), np.float32)))
+            else:
+                p.copy_(torch.from_numpy(det_tensor(SEED, cn, tuple(p.shape))))
+    for mod in m.modules():
+        if isinstance(mod, nn.Dropout):
+            mod.p = 0.0
+        if isinstance(mod, nn.MultiheadAttention):
+            mod.dropout = 0.0
+    m.train()
+    return m
+
+
+class InjectedNoise:
+    def __init__(self, noise):
+        self.noise = noise
+
+    def sample(self, shape):
+        return self.noise.clone().view(*shape)
+
+
+class RecordExp:
+    """Records the Exp(1) draws of the reference's own F.gumbel_softmax call."""
+
+    def __enter__(self):
+        self.orig = torch.Tensor.exponential_
+        self.draws = []
+        rec = self
+
+        def exp_(t, *a, **k):
+            r = rec.orig(t, *a, **k)
+            rec.draws.append(r.detach().clone())
+            return r
+
+        torch.Tensor.exponential_ = exp_
+        return self
+
+    def __exit__(self, *exc):
+        torch.Tensor.exponential_ = self.orig
+
+
+def grad_record(m):
+    out = {}
+    for n, p in m.named_parameters():
+        cn = canon(n)
+        g = p.grad
+        if g is None:
+            out[f"gnone:{cn}"] = np.array(1)
+            continue
+        g = g.detach().double().reshape(-1).numpy()
+        out[f"gsum:{cn}"] = np.array(g.sum())
+        out[f"gabs:{cn}"] = np.array(np.abs(g).sum())
+        if g.size <= 4096:
+            out[f"gfull:{cn}"] = g.astype(np.float32)
+        else:
+            pos = sample_positions(cn, g.size)
+            out[f"gpos:{cn}"] = pos
+            out[f"gval:{cn}"] = g[pos].astype(np.float32)
+    return out
+
+
+def laplace_noise(gen, shape):
+    return torch.distributions.laplace.Laplace(torch.tensor([0.0]), torch.tensor([1.0])).sample(shape).view(*shape)
+
+
+def window_inputs(gen):
+    eeg = torch.randn(B_W, C_W, T_W, generator=gen)
+    act = torch.randn(B_W, A_W, generator=gen) * 0.5
+    return eeg, act
+
+
+def save(name, cfg, arrays):
+    arrays = {k: (v.detach().numpy() if torch.is_tensor(v) else v) for k, v in arrays.items()}
+    np.savez_compressed(HERE / f"{name}.npz", config=np.array(json.dumps(cfg)), **arrays)
+    print("wrote", name, sum(a.nbytes for a in arrays.values() if hasattr(a, "nbytes")), "bytes")
+
+
+def w_values_dp():
+    w = np.loadtxt(REF / "w_values.txt", delimiter=",", dtype=np.float64).reshape(1, -1)
+    return np.log(w / (1 - w)).astype(np.float32)
+
+
+# --------------------------------------------------------------------------- fixtures
+def gen_prigumbel_full(past_acc, hard, tag, dp=None, eps=1.0):
+    torch.manual_seed(7)
+    gen = torch.Generator().manual_seed(11)
+    m = prepare(past_acc.ConcatModel(eps), "W", dp)
+    eeg, act = window_inputs(gen)
+    frame = act.unsqueeze(1)
+    vmask = torch.ones(B_W, 1, dtype=torch.long)
+    tmask = torch.ones(B_W, T_W, dtype=torch.long)
+    labels = torch.tensor([[1], [0]])
+    noise = laplace_noise(gen, (B_W, 2304))
+    m.noiser = InjectedNoise(noise)
+    feats = {}
+    m.fc_layers.register_forward_pre_hook(lambda mod, a: feats.__setitem__("gated", a[0].detach().clone()))
+    m.multi_head_decoder.register_forward_hook(lambda mod, a, o: feats.__setitem__("cross", o.detach().permute(1, 0, 2).mean(1)))
+    m.bert.register_forward_hook(lambda mod, a, o: feats.__setitem__("pooled", o[1].detach().clone()))
+    with RecordExp() as rec:
+        logits = m(frame, vmask, eeg, tmask, hard)
+    loss, acc, _, _ = past_acc.cal_loss(logits, labels)
+    loss.backward()
+    gumbels = -torch.log(rec.draws[0])          # [2,B,2304] (the draws the reference used)
+    cfg = dict(contract="W", variant="prigumbel", eps=eps, eps_mode="newfrac", hard=bool(hard), seed=SEED,
+               B=B_W, C=C_W, T=T_W, A=A_W, dp="w_values" if dp is not None else "zeros")
+    save(f"full_prigumbel_{tag}", cfg, dict(eeg=eeg, act=act, labels=labels.view(-1), noise=noise, gumbels=gumbels,
+                                             logits=logits.detach(), loss=loss.detach(), pooled=feats["pooled"],
+                                             cross=feats["cross"], gated=feats["gated"], **grad_record(m)))
+
+
+def gen_priconcat_full(main_0430):
+    torch.manual_seed(8)
+    gen = torch.Generator().manual_seed(12)
+    args = types.SimpleNamespace(EPSILON=1.0)
+    m = prepare(main_0430.ConcatModel(args, dp_mode="feature_all_lap"), "W")
+    eeg, act = window_inputs(gen)
+    labels = torch.tensor([0, 1])
+    logits = m(act.unsqueeze(1), torch.ones(B_W, 1, dtype=torch.long), eeg, torch.ones(B_W, T_W, dtype=torch.long))
+    loss = nn.functional.cross_entropy(logits, labels)
+    loss.backward()
+    cfg = dict(contract="W", variant="priconcat", eps=1.0, honor_dp_mode=False, seed=SEED, B=B_W, C=C_W, T=T_W, A=A_W)
+    save("full_priconcat", cfg, dict(eeg=eeg, act=act, labels=labels, logits=logits.detach(), loss=loss.detach(),
+                                     **grad_record(m)))
+
+
+def gen_concat_tokens(ref_model):
+    """model.py ConcatModel (contract T, L=512) — C1's model on synthetic token ids."""
+    torch.manual_seed(9)
+    gen = torch.Generator().manual_seed(13)
+    m = prepare(ref_model.ConcatModel(), "T")
+    B, L = 2, 512
+    lens = [51, 37]
+    ids = torch.zeros(B, L, dtype=torch.long)
+    mask = torch.zeros(B, L, dtype=torch.long)
+    for b, n in enumerate(lens):
+        body = torch.randint(1000, 1030, (n - 2,), generator=gen)
+        ids[b, :n] = torch.cat([torch.tensor([101]), body, torch.tensor([102])])
+        mask[b, :n] = 1
+    frame = torch.randn(B, 1, 512, generator=gen) * 0.5
+    vmask = torch.ones(B, 1, dtype=torch.long)
+    labels = torch.tensor([1, 0])
+    logits = m((frame, vmask, ids, mask), hard=True)
+    loss = nn.CrossEntropyLoss(reduction="none")(logits, labels).sum()     # train.py:69,110-111
+    loss.backward()
+    cfg = dict(contract="T", variant="concat", seed=SEED, B=B, L=L)
+    save("full_concat_tokens", cfg, dict(title_input=ids, text_mask=mask, frame_input=frame, vedio_mask=vmask,
+                                         labels=labels, logits=logits.detach(), loss=loss.detach(), **grad_record(m)))
+
+
+class Const(nn.Module):
+    def __init__(self, fn):
+        super().__init__()
+        self.fn = fn
+
+    def forward(self, *a, **k):
+        return self.fn(*a, **k)
+
+
+def gen_gate_head(past_acc, ref_model, main_0430):
+    """Fusion (concat + min-max) + privacy stage + fc head through the reference's own forward,
+    with the encoders replaced by leaves (B=4).  One case per (eps, hard, DP init)."""
+    gen = torch.Generator().manual_seed(21)
+    B = 4
+    cases = [("zeros", 1.0, False), ("zeros", 1.0, True), ("w_values", 0.1, False), ("w_values", 1.0, True),
+             ("w_values", 3.0, False), ("w_values", 5.0, True), ("w_values", 10.0, False), ("w_values", 10.0, True)]
+    out = {}
+    for ci, (dpname, eps, hard) in enumerate(cases):
+        pooled = (torch.randn(B, 768, generator=gen) * 0.5).requires_grad_()
+        img = (torch.randn(B, 1, 768, generator=gen) * 0.5).requires_grad_()
+        cross = (torch.randn(1, B, 768, generator=gen) * 0.5).requires_grad_()
+        m = past_acc.ConcatModel(eps)
+        prepare(m, "T", w_values_dp() if dpname == "w_values" else None)
+        m.bert = Const(lambda **k: (torch.zeros(B, 1, 768), pooled))
+        m.visual_encoder = Const(lambda x: img)
+        m.multi_head_decoder = Const(lambda **k: cross)
+        noise = laplace_noise(gen, (B, 2304))
+        m.noiser = InjectedNoise(noise)
+        labels = torch.randint(0, 2, (B,), generator=gen)
+        with RecordExp() as rec:
+            logits = m(None, torch.ones(B, 1), None, None, hard)
+        loss, _, _, _ = past_acc.cal_loss(logits, labels.view(-1, 1))
+        loss.backward()
+        pre = f"c{ci}:"
+        out.update({pre + "pooled": pooled.detach(), pre + "img": img.detach().squeeze(1),
+                    pre + "cross": cross.detach().squeeze(0), pre + "noise": noise,
+                    pre + "gumbels": -torch.log(rec.draws[0]), pre + "labels": labels,
+                    pre + "DP": m.DP.detach().clone(), pre + "logits": logits.detach(), pre + "loss": loss.detach(),
+                    pre + "d_pooled": pooled.grad, pre + "d_img": img.grad.squeeze(1), pre + "d_cross": cross.grad.squeeze(0),
+                    pre + "d_DP": m.DP.grad.clone()})
+        for n in ("fc_layers.0.weight", "fc_layers.2.weight"):
+            g = dict(m.named_parameters())[n].grad.reshape(-1).double().numpy()
+            out[pre + "gsum:" + n] = np.array(g.sum())
+            pos = sample_positions(n, g.size)
+            out[pre + "gpos:" + n] = pos
+            out[pre + "gval:" + n] = g[pos].astype(np.float32)
+        for n in ("fc_layers.0.bias", "fc_layers.2.bias", "classifier.weight", "classifier.bias"):
+            out[pre + "gfull:" + n] = dict(m.named_parameters())[n].grad.reshape(-1)
+    cfg = dict(cases=[dict(dp=d, eps=e, hard=h, eps_mode="newfrac") for d, e, h in cases], B=B, seed=SEED)
+    save("gate_head", cfg, out)
+
+    # PriConcat DP_guarantee('feature_all_lap') (main_0430.py:76-85), called directly.
+    f = torch.randn(B, 2304, generator=gen)
+    torch.manual_seed(31)
+    y = main_0430.DP_guarantee(f.clone(), 1.0, dp_mode="feature_all_lap")
+    torch.manual_seed(31)
+    row_noise = torch.distributions.laplace.Laplace(torch.tensor([0.0]), torch.tensor([1.0 / 1.0])).sample([B])
+    save("dp_guarantee", dict(eps=1.0, B=B), dict(feature=f, out=y, row_noise=row_noise.view(-1)))
+
+
+def gen_adam_two_optimizer(past_acc):
+    """One PriGumbel iteration of past_acc.main2's loop body (:194-212) with the reference's two
+    Adam optimizers (lr 1e-6): parameter deltas / lr recorded for DP and the head."""
+    torch.manual_seed(10)
+    gen = torch.Generator().manual_seed(14)
+    m = prepare(past_acc.ConcatModel(1.0), "W", w_values_dp())
+    eeg, act = window_inputs(gen)
+    frame, vmask, tmask = act.unsqueeze(1), torch.ones(B_W, 1, dtype=torch.long), torch.ones(B_W, T_W, dtype=torch.long)
+    labels = torch.tensor([[0], [1]])
+    n1, n2 = laplace_noise(gen, (B_W, 2304)), laplace_noise(gen, (B_W, 2304))
+    DP_params = [p for n, p in m.named_parameters() if "DP" in n]
+    model_params = [p for n, p in m.named_parameters() if "DP" not in n]
+    lr = 1e-6
+    model_opt, dp_opt = torch.optim.Adam(model_params, lr=lr), torch.optim.Adam(DP_params, lr=lr)
+    before = {canon(n): p.detach().clone() for n, p in m.named_parameters()}
+    dp_opt.zero_grad()
+    m.noiser = InjectedNoise(n1)
+    with RecordExp() as r1:
+        loss1, _, _, _ = past_acc.cal_loss(m(frame, vmask, eeg, tmask, hard=False), labels)
+    loss1.backward()
+    dp_opt.step()
+    model_opt.zero_grad()
+    m.noiser = InjectedNoise(n2)
+    with RecordExp() as r2:
+        loss2, _, _, _ = past_acc.cal_loss(m(frame, vmask, eeg, tmask, hard=True), labels)
+    loss2.backward()
+    model_opt.step()
+    out = dict(eeg=eeg, act=act, labels=labels.view(-1), noise1=n1, noise2=n2, gumbels1=-torch.log(r1.draws[0]),
+               gumbels2=-torch.log(r2.draws[0]), loss1=loss1.detach(), loss2=loss2.detach())
+    for n, p in m.named_parameters():
+        cn = canon(n)
+        if cn in ("DP", "classifier.weight", "classifier.bias", "fc_layers.2.bias", "bert.pooler.dense.bias",
+                  "multi_head_decoder.layers.2.norm3.weight"):
+            out["delta:" + cn] = ((p.detach() - before[cn]) / lr).reshape(-1)
+    save("two_optimizer_step", dict(lr=lr, eps=1.0, seed=SEED, B=B_W, C=C_W, T=T_W, A=A_W, dp="w_values"), out)
+
+
+if __name__ == "__main__":
+    torch.set_num_threads(8)
+    past_acc, main_0430, ref_model = import_reference()
+    np.savez_compressed(HERE / "w_values_dp.npz", DP=w_values_dp())
+    gen_gate_head(past_acc, ref_model, main_0430)
+    gen_prigumbel_full(past_acc, hard=False, tag="soft")
+    gen_prigumbel_full(past_acc, hard=True, tag="hard_wvalues", dp=w_values_dp())
+    gen_priconcat_full(main_0430)
+    gen_concat_tokens(ref_model)
+    gen_adam_two_optimizer(past_acc)
