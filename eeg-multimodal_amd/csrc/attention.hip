@@ -1,0 +1,314 @@
+// attention.hip — fused multi-head self-attention forward/backward (BERT, 12 heads x 64).
+//
+// Replaces BertSelfAttention's  softmax(Q K^T / 8 + key_mask) V   (modeling_bert.py:139-199,
+// sdpa/eager :111-136) and its autograd backward.  Q/K/V are read straight out of the fused
+// QKV projection output [B, L, 3*768]; the context is written as [B, L, 768].
+//
+// Forward: grid (L/128, H, B), 8 waves x 16 queries.  S^T = K Q^T is computed "swapped" so the
+// accumulator of S^T is directly the B operand of O^T = V^T P^T (k order permuted consistently,
+// V^T read with ds_read_b64_tr_b16).  K/V tiles of 64 keys staged through LDS; online softmax.
+// Stores LSE (natural log, scaled-score units) for the backward.
+// Backward: grid (L/256, H, B), 8 waves x 32 keys; per 32-query chunk: S, P (from LSE), dP,
+// dS = P (dP - rowsum(dO o O)); dV += P^T dO and dK += dS^T Q accumulate in registers; dS goes
+// through LDS once for dQ = dS K.  With L <= 256 every dQ element is produced by exactly one
+// workgroup (plain stores); for longer sequences dQ is accumulated with fp32 atomics.
+#include "common.h"
+#include "eegfusion_internal.h"
+
+namespace {
+
+constexpr int DH = 64;          // head dim
+constexpr float NEG = -1e30f;   // masked-key score (finfo.min semantics: never NaN)
+
+template <typename T> constexpr int pad16() { return 16 / (int)sizeof(T); }
+
+struct AttnArgs {
+  const void* qkv; void* out; float* lse; const float* kbias;
+  const void* o; const void* dout; void* dqkv; float* dq_acc;
+  int B, H, L; long ld_qkv, ld_out; float scale;
+};
+
+// Cooperative copy of `rows` x 64 elements (row stride `ld` in global) into LDS [rows][64+pad].
+template <typename T, int NTHR>
+DEV void stage_rows(T* lds, int ldl, const T* g, long ld, int rows, int tid) {
+  constexpr int VE = 16 / (int)sizeof(T);
+  constexpr int CPR = DH / VE;                 // 16-B chunks per row
+  for (int c = tid; c < rows * CPR; c += NTHR) {
+    const int r = c / CPR, cc = (c % CPR) * VE;
+    st16(lds + r * ldl + cc, ld16(g + (long)r * ld + cc));
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(512) attn_fwd_kernel(AttnArgs a) {
+  using F = typename Frag8<T>::type;
+  constexpr int KT = 64, LDK = DH + pad16<T>();
+  __shared__ __attribute__((aligned(16))) T lds[2 * KT * LDK];
+  T* Ks = lds;
+  T* Vs = lds + KT * LDK;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, li = lane & 15;
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int q = blockIdx.x * 128 + wave * 16 + li;                  // this lane's query (B/C column)
+  const T* base = (const T*)a.qkv + (long)b * a.L * a.ld_qkv;
+  const T* Qg = base + h * DH;
+  const T* Kg = base + 768 + h * DH;
+  const T* Vg = base + 1536 + h * DH;
+
+  F qf[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) qf[c] = ld_row8(Qg + (long)q * a.ld_qkv + 32 * c + 8 * g);
+
+  f32x4 o[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) o[e] = f32x4{0, 0, 0, 0};
+  float m = NEG, l = 0.f;
+  const float* kb = a.kbias ? a.kbias + (long)b * a.L : nullptr;
+
+  for (int k0 = 0; k0 < a.L; k0 += KT) {
+    __syncthreads();
+    stage_rows<T, 512>(Ks, LDK, Kg + (long)k0 * a.ld_qkv, a.ld_qkv, KT, tid);
+    stage_rows<T, 512>(Vs, LDK, Vg + (long)k0 * a.ld_qkv, a.ld_qkv, KT, tid);
+    __syncthreads();
+    f32x4 s[4];
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      s[f] = f32x4{0, 0, 0, 0};
+#pragma unroll
+      for (int c = 0; c < 2; ++c) s[f] = mma16(ld_row8(Ks + (16 * f + li) * LDK + 32 * c + 8 * g), qf[c], s[f]);
+    }
+    // s[f][r]: key = k0 + 16f + 4g + r, query = q
+    float tmax = NEG;
+#pragma unroll
+    for (int f = 0; f < 4; ++f)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = s[f][r] * a.scale;
+        if (kb) v += kb[k0 + 16 * f + 4 * g + r];
+        s[f][r] = v;
+        tmax = fmaxf(tmax, v);
+      }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float mn = fmaxf(m, tmax);
+    const float alpha = __expf(m - mn);
+    m = mn;
+    float ps = 0.f;
+#pragma unroll
+    for (int f = 0; f < 4; ++f)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { s[f][r] = __expf(s[f][r] - mn); ps += s[f][r]; }
+    l = l * alpha + ps;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] *= alpha;
+    // O^T[d, q] += sum_key V[key, d] P[q, key]   (k order: {4g..4g+3 of frag 2c, of frag 2c+1})
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const F pb = pack_acc<T>(s[2 * c], s[2 * c + 1]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        o[e] = mma16(ld_col4x2(Vs, LDK, 32 * c + 4 * g, 32 * c + 16 + 4 * g, 16 * e, lane), pb, o[e]);
+    }
+  }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  const float inv = 1.0f / l;
+  T* out = (T*)a.out + ((long)b * a.L + q) * a.ld_out + h * DH;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    // o[e][r]: d = 16e + 4g + r
+#pragma unroll
+    for (int r = 0; r < 4; ++r) out[16 * e + 4 * g + r] = from_f32<T>(o[e][r] * inv);
+  }
+  if (g == 0) a.lse[((long)b * a.H + h) * a.L + q] = m + __logf(l);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(512) attn_bwd_kernel(AttnArgs a) {
+  using F = typename Frag8<T>::type;
+  constexpr int KB = 256, QC = 32, LDK = DH + pad16<T>(), LDS_ = KB + pad16<T>();
+  constexpr int SZ_K = KB * LDK, SZ_Q = QC * LDK, SZ_S = QC * LDS_;
+  __shared__ __attribute__((aligned(16))) T lds[SZ_K + 3 * SZ_Q + SZ_S];
+  __shared__ float lse_s[QC], dd_s[QC];
+  T* Ks = lds;
+  T* Qs = Ks + SZ_K;
+  T* dOs = Qs + SZ_Q;
+  T* Os = dOs + SZ_Q;
+  T* dSs = Os + SZ_Q;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, li = lane & 15;
+  const int b = blockIdx.z, h = blockIdx.y, kb0 = blockIdx.x * KB;
+  const int kw0 = kb0 + wave * 32;                                    // this wave's 32 keys
+  const T* base = (const T*)a.qkv + (long)b * a.L * a.ld_qkv;
+  const T* Qg = base + h * DH;
+  const T* Kg = base + 768 + h * DH;
+  const T* Vg = base + 1536 + h * DH;
+  const T* Og = (const T*)a.o + (long)b * a.L * a.ld_out + h * DH;
+  const T* dOg = (const T*)a.dout + (long)b * a.L * a.ld_out + h * DH;
+  const float* lse = a.lse + ((long)b * a.H + h) * a.L;
+  const float* kbias = a.kbias ? a.kbias + (long)b * a.L : nullptr;
+  const int nkb = a.L / KB;
+
+  // this wave's K and V as B operands (key = column): lane holds [key kw0+16f+li][d 32c+8g..]
+  F kf[2][2], vf[2][2];
+#pragma unroll
+  for (int f = 0; f < 2; ++f)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      kf[f][c] = ld_row8(Kg + (long)(kw0 + 16 * f + li) * a.ld_qkv + 32 * c + 8 * g);
+      vf[f][c] = ld_row8(Vg + (long)(kw0 + 16 * f + li) * a.ld_qkv + 32 * c + 8 * g);
+    }
+  float kbv[2];
+#pragma unroll
+  for (int f = 0; f < 2; ++f) kbv[f] = kbias ? kbias[kw0 + 16 * f + li] : 0.f;
+
+  f32x4 dk[2][4], dv[2][4];
+#pragma unroll
+  for (int f = 0; f < 2; ++f)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { dk[f][e] = f32x4{0, 0, 0, 0}; dv[f][e] = f32x4{0, 0, 0, 0}; }
+
+  stage_rows<T, 512>(Ks, LDK, Kg + (long)kb0 * a.ld_qkv, a.ld_qkv, KB, tid);
+
+  for (int q0 = 0; q0 < a.L; q0 += QC) {
+    __syncthreads();
+    stage_rows<T, 512>(Qs, LDK, Qg + (long)q0 * a.ld_qkv, a.ld_qkv, QC, tid);
+    stage_rows<T, 512>(dOs, LDK, dOg + (long)q0 * a.ld_out, a.ld_out, QC, tid);
+    stage_rows<T, 512>(Os, LDK, Og + (long)q0 * a.ld_out, a.ld_out, QC, tid);
+    if (tid < QC) lse_s[tid] = lse[q0 + tid];
+    __syncthreads();
+    {  // D[q] = sum_d dO[q,d] O[q,d]: 16 lanes per query
+      const int qq = tid >> 4, part = tid & 15;
+      float acc = 0.f;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) acc += to_f32(dOs[qq * LDK + part * 4 + d]) * to_f32(Os[qq * LDK + part * 4 + d]);
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 16);
+      if (part == 0) dd_s[qq] = acc;
+    }
+    __syncthreads();
+    // S = Q K^T and dP = dO V^T : rows = queries (4g+r within q-frag), cols = keys (li)
+    f32x4 p[2][2], ds[2][2];
+#pragma unroll
+    for (int qf = 0; qf < 2; ++qf) {
+      F qa[2], da[2];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        qa[c] = ld_row8(Qs + (16 * qf + li) * LDK + 32 * c + 8 * g);
+        da[c] = ld_row8(dOs + (16 * qf + li) * LDK + 32 * c + 8 * g);
+      }
+#pragma unroll
+      for (int f = 0; f < 2; ++f) {
+        f32x4 s = f32x4{0, 0, 0, 0}, dp = f32x4{0, 0, 0, 0};
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          s = mma16(qa[c], kf[f][c], s);
+          dp = mma16(da[c], vf[f][c], dp);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int qi = 16 * qf + 4 * g + r;
+          const float pv = __expf(s[r] * a.scale + kbv[f] - lse_s[qi]);
+          s[r] = pv;
+          dp[r] = pv * (dp[r] - dd_s[qi]);
+        }
+        p[qf][f] = s;
+        ds[qf][f] = dp;
+      }
+    }
+    // dV[key, d] += sum_q P[q,key] dO[q,d];  dK[key, d] += sum_q dS[q,key] Q[q,d]
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      const F pa = pack_acc<T>(p[0][f], p[1][f]);
+      const F sa = pack_acc<T>(ds[0][f], ds[1][f]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        dv[f][e] = mma16(pa, ld_col4x2(dOs, LDK, 4 * g, 16 + 4 * g, 16 * e, lane), dv[f][e]);
+        dk[f][e] = mma16(sa, ld_col4x2(Qs, LDK, 4 * g, 16 + 4 * g, 16 * e, lane), dk[f][e]);
+      }
+    }
+    // dS -> LDS [q][key - kb0]
+#pragma unroll
+    for (int qf = 0; qf < 2; ++qf)
+#pragma unroll
+      for (int f = 0; f < 2; ++f)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          dSs[(16 * qf + 4 * g + r) * LDS_ + wave * 32 + 16 * f + li] = from_f32<T>(ds[qf][f][r]);
+    __syncthreads();
+    {  // dQ[q, d] = scale * sum_key dS[q,key] K[key,d]; wave -> (q-frag w>>2, d-frag w&3)
+      const int qf = wave >> 2, e = wave & 3;
+      f32x4 acc = f32x4{0, 0, 0, 0};
+#pragma unroll
+      for (int kc = 0; kc < KB / 32; ++kc)
+        acc = mma16(ld_row8(dSs + (16 * qf + li) * LDS_ + 32 * kc + 8 * g),
+                    ld_col8(Ks, LDK, 32 * kc + 8 * g, 16 * e, lane), acc);
+      // acc[r]: q = q0 + 16qf + 4g + r, d = 16e + li
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const long qrow = (long)b * a.L + q0 + 16 * qf + 4 * g + r;
+        const int d = 16 * e + li;
+        if (nkb == 1) ((T*)a.dqkv)[qrow * a.ld_qkv + h * DH + d] = from_f32<T>(acc[r] * a.scale);
+        else atomicAdd(a.dq_acc + qrow * 768 + h * DH + d, acc[r] * a.scale);
+      }
+    }
+  }
+  // write dK, dV: dk[f][e][r]: key = kw0 + 16f + 4g + r ... wait: rows of dK acc = keys? (see note)
+  T* dqkv = (T*)a.dqkv + (long)b * a.L * a.ld_qkv;
+#pragma unroll
+  for (int f = 0; f < 2; ++f)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const long key = kw0 + 16 * f + 4 * g + r;
+        const int d = 16 * e + li;
+        dqkv[key * a.ld_qkv + 768 + h * DH + d] = from_f32<T>(dk[f][e][r] * a.scale);
+        dqkv[key * a.ld_qkv + 1536 + h * DH + d] = from_f32<T>(dv[f][e][r]);
+      }
+}
+
+__global__ void dq_convert_kernel(const float* dq_acc, void* dqkv, int is_bf16, long rows, long ld) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows * 768) return;
+  const long r = i / 768, c = i % 768;
+  if (is_bf16) ((bf16*)dqkv)[r * ld + c] = (bf16)dq_acc[i];
+  else ((float*)dqkv)[r * ld + c] = dq_acc[i];
+}
+
+}  // namespace
+
+extern "C" int eegf_attn_fwd(int dtype, int B, int H, int L, const void* qkv, long ld_qkv, const float* key_bias,
+                             float scale, void* out, long ld_out, float* lse, hipStream_t stream) {
+  if (B <= 0 || H != 12 || L <= 0 || L % 128 != 0 || !qkv || !out || !lse || ld_qkv < 2304 || ld_out < 768)
+    return EEGF_ERR_ARG;
+  if (B > 65535) return EEGF_ERR_ARG;
+  AttnArgs a{qkv, out, lse, key_bias, nullptr, nullptr, nullptr, nullptr, B, H, L, ld_qkv, ld_out, scale};
+  const dim3 grid(L / 128, H, B);
+  if (dtype == EEGF_F32) hipLaunchKernelGGL(attn_fwd_kernel<float>, grid, dim3(512), 0, stream, a);
+  else if (dtype == EEGF_BF16) hipLaunchKernelGGL(attn_fwd_kernel<bf16>, grid, dim3(512), 0, stream, a);
+  else return EEGF_ERR_ARG;
+  return (int)hipGetLastError();
+}
+
+extern "C" long eegf_attn_bwd_workspace(int B, int L) { return L > 256 ? (long)B * L * 768 : 0; }
+
+extern "C" int eegf_attn_bwd(int dtype, int B, int H, int L, const void* qkv, long ld_qkv, const float* key_bias,
+                             float scale, const void* out, const void* dout, long ld_out, const float* lse,
+                             void* dqkv, float* dq_workspace, hipStream_t stream) {
+  if (B <= 0 || H != 12 || L <= 0 || L % 256 != 0 || !qkv || !out || !dout || !lse || !dqkv) return EEGF_ERR_ARG;
+  if (ld_qkv < 2304 || ld_out < 768 || B > 65535) return EEGF_ERR_ARG;
+  if (L > 256 && !dq_workspace) return EEGF_ERR_ARG;
+  if (L > 256) hipMemsetAsync(dq_workspace, 0, sizeof(float) * (size_t)B * L * 768, stream);
+  AttnArgs a{qkv, nullptr, const_cast<float*>(lse), key_bias, out, dout, dqkv, dq_workspace, B, H, L, ld_qkv, ld_out,
+             scale};
+  const dim3 grid(L / 256, H, B);
+  if (dtype == EEGF_F32) hipLaunchKernelGGL(attn_bwd_kernel<float>, grid, dim3(512), 0, stream, a);
+  else if (dtype == EEGF_BF16) hipLaunchKernelGGL(attn_bwd_kernel<bf16>, grid, dim3(512), 0, stream, a);
+  else return EEGF_ERR_ARG;
+  if (L > 256) {
+    const long n = (long)B * L * 768;
+    hipLaunchKernelGGL(dq_convert_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, dq_workspace, dqkv,
+                       dtype == EEGF_BF16, (long)B * L, ld_qkv);
+  }
+  return (int)hipGetLastError();
+}

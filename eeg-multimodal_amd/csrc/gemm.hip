@@ -21,7 +21,7 @@ constexpr int BM = 128, BN = 128, NT = 256;
 struct GemmArgs {
   const void* A; const void* B; void* C; const float* bias; void* aux;
   long lda, ldb, ldc, ldaux;
-  long sA, sB, sC, sAux;
+  long sA, sB, sC, sAux, sBias;
   int M, N, K;
   float alpha, beta, epi_scale;
 };
@@ -159,7 +159,7 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmArgs g) {
     const int n = n0 + wn * 64 + j * 16 + (lane & 15);
     if (n >= g.N) continue;
     float bias = 0.f;
-    if (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_TANH) bias = g.bias[n];
+    if (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_TANH) bias = g.bias[(long)z * g.sBias + n];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
 #pragma unroll
@@ -222,7 +222,7 @@ extern "C" int eegf_gemm(int dtype, int out_dtype, int a_kcontig, int b_kcontig,
                          const void* A, long lda, long strideA,
                          const void* B, long ldb, long strideB,
                          void* C, long ldc, long strideC,
-                         const float* bias, void* aux, long ldaux, long strideAux,
+                         const float* bias, long strideBias, void* aux, long ldaux, long strideAux,
                          float alpha, float beta, float epi_scale, hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0 || batch <= 0 || !A || !B || !C) return EEGF_ERR_ARG;
   if (batch > 65535) return EEGF_ERR_ARG;
@@ -234,7 +234,7 @@ extern "C" int eegf_gemm(int dtype, int out_dtype, int a_kcontig, int b_kcontig,
     if (fwd && !(a_kcontig && b_kcontig)) return EEGF_ERR_ARG;
     if (!fwd && !(a_kcontig && !b_kcontig)) return EEGF_ERR_ARG;
   }
-  GemmArgs a{A, B, C, bias, aux, lda, ldb, ldc, ldaux, strideA, strideB, strideC, strideAux, M, N, K, alpha, beta, epi_scale};
+  GemmArgs a{A, B, C, bias, aux, lda, ldb, ldc, ldaux, strideA, strideB, strideC, strideAux, strideBias, M, N, K, alpha, beta, epi_scale};
   if (dtype == EEGF_F32) {
     if (out_dtype != EEGF_F32) return EEGF_ERR_ARG;
     return dispatch_epi<float, float>(epi, a_kcontig, b_kcontig, a, batch, stream);

@@ -1,0 +1,287 @@
+// layernorm.hip — residual-add + dropout + LayerNorm forward/backward, and strided row reductions.
+//
+// Replaces (per row of `width` features):
+//   BertEmbeddings   LN(embeds + type[0] + pos[t]) then dropout          (modeling_bert.py:95-105)
+//   BertSelfOutput / BertOutput   LN(dropout(dense) + residual)          (modeling_bert.py:282-351)
+//   TransformerDecoderLayer norm1/2/3(x + dropout_k(block(x)))           (transformer.py:1158-1200)
+// One wave per row, 4 features per lane-chunk (8-B bf16 / 16-B fp32 loads), fp32 statistics.
+// The backward writes per-block partial sums of dgamma/dbeta (no atomics → bitwise reproducible);
+// eegf_colsum reduces them (and bias / position-embedding gradients) in a second pass.
+#include "common.h"
+#include "eegfusion_internal.h"
+
+namespace {
+
+template <typename T> struct V4;
+template <> struct V4<float> {
+  typedef f32x4 raw;
+  static DEV f32x4 load(const float* p) { return *(const f32x4*)p; }
+  static DEV void store(float* p, f32x4 v) { *(f32x4*)p = v; }
+};
+template <> struct V4<bf16> {
+  typedef bf16x4 raw;
+  static DEV f32x4 load(const bf16* p) {
+    bf16x4 v = *(const bf16x4*)p;
+    return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+  }
+  static DEV void store(bf16* p, f32x4 v) {
+    bf16x4 o;
+    o[0] = (bf16)v[0]; o[1] = (bf16)v[1]; o[2] = (bf16)v[2]; o[3] = (bf16)v[3];
+    *(bf16x4*)p = o;
+  }
+};
+
+// Dropout keep-mask for 4 consecutive elements starting at element index e4*4.
+DEV void drop_mask4(uint64_t seed, uint64_t offset, uint64_t e4, float p, float (&m)[4]) {
+  const u32x4s r = philox4x32((uint32_t)e4, (uint32_t)(e4 >> 32), (uint32_t)offset, (uint32_t)(offset >> 32),
+                              (uint32_t)seed, (uint32_t)(seed >> 32));
+  const float scale = 1.0f / (1.0f - p);
+  const uint32_t thr = (uint32_t)fminf(p * 4294967296.0f, 4294967295.0f);
+  m[0] = r.x >= thr ? scale : 0.f;
+  m[1] = r.y >= thr ? scale : 0.f;
+  m[2] = r.z >= thr ? scale : 0.f;
+  m[3] = r.w >= thr ? scale : 0.f;
+}
+
+struct LnFwdArgs {
+  const void* x; const void* r; const float* table; const float* table2;
+  const float* gamma; const float* beta;
+  void* y; void* s; float* mean; float* rstd;
+  long rows; int table_period; float eps; float p; int drop_mode; uint64_t seed, offset;
+};
+
+template <typename T, int NCH>
+__global__ void __launch_bounds__(256) ln_fwd_kernel(LnFwdArgs a) {
+  constexpr int W = NCH * 256;
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= a.rows) return;
+  const T* x = (const T*)a.x + row * W;
+  f32x4 v[NCH];
+  float sum = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = (lane + 64 * c) * 4;
+    v[c] = V4<T>::load(x + col);
+    if (a.drop_mode == 1 && a.p > 0.f) {
+      float m[4];
+      drop_mask4(a.seed, a.offset, (uint64_t)(row * W + col) >> 2, a.p, m);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[c][e] *= m[e];
+    }
+    if (a.r) v[c] += V4<T>::load((const T*)a.r + row * W + col);
+    if (a.table) v[c] += *(const f32x4*)(a.table + (row % a.table_period) * W + col);
+    if (a.table2) v[c] += *(const f32x4*)(a.table2 + col);
+    if (a.s) V4<T>::store((T*)a.s + row * W + col, v[c]);
+    sum += v[c][0] + v[c][1] + v[c][2] + v[c][3];
+  }
+  const float mean = wave_sum(sum) * (1.0f / W);
+  float sq = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { const float d = v[c][e] - mean; sq += d * d; }
+  const float rstd = rsqrtf(wave_sum(sq) * (1.0f / W) + a.eps);
+  T* y = (T*)a.y + row * W;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = (lane + 64 * c) * 4;
+    const f32x4 g = *(const f32x4*)(a.gamma + col), b = *(const f32x4*)(a.beta + col);
+    f32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (v[c][e] - mean) * rstd * g[e] + b[e];
+    if (a.drop_mode == 2 && a.p > 0.f) {
+      float m[4];
+      drop_mask4(a.seed, a.offset, (uint64_t)(row * W + col) >> 2, a.p, m);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] *= m[e];
+    }
+    V4<T>::store(y + col, o);
+  }
+  if (lane == 0) {
+    if (a.mean) a.mean[row] = mean;
+    if (a.rstd) a.rstd[row] = rstd;
+  }
+}
+
+struct LnBwdArgs {
+  const void* dy; const void* s; const float* mean; const float* rstd; const float* gamma;
+  void* dx; void* dr; float* dgamma_part; float* dbeta_part;
+  long rows; int rows_per_block; float p; int drop_mode; uint64_t seed, offset;
+};
+
+template <typename T, int NCH>
+__global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
+  constexpr int W = NCH * 256;
+  __shared__ float red[2][4][W];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  f32x4 dg[NCH], db[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) { dg[c] = f32x4{0, 0, 0, 0}; db[c] = f32x4{0, 0, 0, 0}; }
+  f32x4 gam[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) gam[c] = *(const f32x4*)(a.gamma + (lane + 64 * c) * 4);
+
+  const long r0 = (long)blockIdx.x * a.rows_per_block;
+  for (int i = wave; i < a.rows_per_block; i += 4) {
+    const long row = r0 + i;
+    if (row >= a.rows) break;
+    const float mean = a.mean[row], rstd = a.rstd[row];
+    f32x4 dy[NCH], xh[NCH];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = (lane + 64 * c) * 4;
+      dy[c] = V4<T>::load((const T*)a.dy + row * W + col);
+      if (a.drop_mode == 2 && a.p > 0.f) {
+        float m[4];
+        drop_mask4(a.seed, a.offset, (uint64_t)(row * W + col) >> 2, a.p, m);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dy[c][e] *= m[e];
+      }
+      const f32x4 sv = V4<T>::load((const T*)a.s + row * W + col);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        xh[c][e] = (sv[e] - mean) * rstd;
+        const float g = dy[c][e] * gam[c][e];
+        s1 += g;
+        s2 += g * xh[c][e];
+        dg[c][e] += dy[c][e] * xh[c][e];
+        db[c][e] += dy[c][e];
+      }
+    }
+    s1 = wave_sum(s1) * (1.0f / W);
+    s2 = wave_sum(s2) * (1.0f / W);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = (lane + 64 * c) * 4;
+      f32x4 ds;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ds[e] = rstd * (dy[c][e] * gam[c][e] - s1 - xh[c][e] * s2);
+      if (a.dr) V4<T>::store((T*)a.dr + row * W + col, ds);
+      if (a.drop_mode == 1 && a.p > 0.f) {
+        float m[4];
+        drop_mask4(a.seed, a.offset, (uint64_t)(row * W + col) >> 2, a.p, m);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ds[e] *= m[e];
+      }
+      if (a.dx) V4<T>::store((T*)a.dx + row * W + col, ds);
+    }
+  }
+  // per-block partial dgamma / dbeta (fixed order: bitwise reproducible)
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = (lane + 64 * c) * 4;
+    *(f32x4*)&red[0][wave][col] = dg[c];
+    *(f32x4*)&red[1][wave][col] = db[c];
+  }
+  __syncthreads();
+  for (int col = threadIdx.x; col < W; col += 256) {
+    const float g = red[0][0][col] + red[0][1][col] + red[0][2][col] + red[0][3][col];
+    const float b = red[1][0][col] + red[1][1][col] + red[1][2][col] + red[1][3][col];
+    if (a.dgamma_part) a.dgamma_part[(long)blockIdx.x * W + col] = g;
+    if (a.dbeta_part) a.dbeta_part[(long)blockIdx.x * W + col] = b;
+  }
+}
+
+// ---- strided column sums: out[p, c] = sum_{r = p (mod period)} in[r*ld + c]  (+ beta*out) ----
+template <typename T>
+__global__ void __launch_bounds__(256) colsum_stage1(const T* in, long ld, long rows, int width, int period,
+                                                      int splits, float* ws) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  const int p = blockIdx.y, s = blockIdx.z;
+  if (c >= width) return;
+  float acc = 0.f;
+  for (long r = p + (long)period * s; r < rows; r += (long)period * splits) acc += to_f32(in[r * ld + c]);
+  ws[((long)s * period + p) * width + c] = acc;
+}
+
+__global__ void __launch_bounds__(256) colsum_stage2(const float* ws, int splits, long n, float* out, float beta) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  float acc = 0.f;
+  for (int s = 0; s < splits; ++s) acc += ws[(long)s * n + i];
+  out[i] = beta != 0.f ? acc + beta * out[i] : acc;
+}
+
+template <typename T>
+int colsum_t(const void* in, long ld, long rows, int width, int period, float* ws, long ws_elems, float* out,
+             float beta, hipStream_t st) {
+  const long per = (rows + period - 1) / period;              // rows per output element
+  int splits = (int)((per + 63) / 64);
+  while ((long)splits * period * width > ws_elems && splits > 1) splits = (splits + 1) / 2;
+  if ((long)splits * period * width > ws_elems) return EEGF_ERR_ARG;
+  if (splits > 65535) splits = 65535;
+  hipLaunchKernelGGL(colsum_stage1<T>, dim3((width + 255) / 256, period, splits), dim3(256), 0, st,
+                     (const T*)in, ld, rows, width, period, splits, ws);
+  const long n = (long)period * width;
+  hipLaunchKernelGGL(colsum_stage2, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, ws, splits, n, out, beta);
+  return (int)hipGetLastError();
+}
+
+template <typename T>
+int ln_fwd_t(int nch, const LnFwdArgs& a, hipStream_t st) {
+  const dim3 grid((unsigned)((a.rows + 3) / 4));
+  switch (nch) {
+    case 1: hipLaunchKernelGGL((ln_fwd_kernel<T, 1>), grid, dim3(256), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((ln_fwd_kernel<T, 2>), grid, dim3(256), 0, st, a); break;
+    case 3: hipLaunchKernelGGL((ln_fwd_kernel<T, 3>), grid, dim3(256), 0, st, a); break;
+    case 4: hipLaunchKernelGGL((ln_fwd_kernel<T, 4>), grid, dim3(256), 0, st, a); break;
+    default: return EEGF_ERR_ARG;
+  }
+  return (int)hipGetLastError();
+}
+
+template <typename T>
+int ln_bwd_t(int nch, const LnBwdArgs& a, hipStream_t st) {
+  const dim3 grid((unsigned)((a.rows + a.rows_per_block - 1) / a.rows_per_block));
+  switch (nch) {
+    case 1: hipLaunchKernelGGL((ln_bwd_kernel<T, 1>), grid, dim3(256), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((ln_bwd_kernel<T, 2>), grid, dim3(256), 0, st, a); break;
+    case 3: hipLaunchKernelGGL((ln_bwd_kernel<T, 3>), grid, dim3(256), 0, st, a); break;
+    case 4: hipLaunchKernelGGL((ln_bwd_kernel<T, 4>), grid, dim3(256), 0, st, a); break;
+    default: return EEGF_ERR_ARG;
+  }
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" int eegf_ln_fwd(int dtype, long rows, int width, const void* x, const void* r, const float* table,
+                           int table_period, const float* table2, const float* gamma, const float* beta, float eps,
+                           float drop_p, int drop_mode, unsigned long long seed, unsigned long long offset,
+                           void* y, void* s_out, float* mean, float* rstd, hipStream_t stream) {
+  if (rows <= 0 || width % 256 != 0 || width > 1024 || !x || !gamma || !beta || !y) return EEGF_ERR_ARG;
+  if (table && table_period <= 0) return EEGF_ERR_ARG;
+  if (drop_p < 0.f || drop_p >= 1.f || drop_mode < 0 || drop_mode > 2) return EEGF_ERR_ARG;
+  LnFwdArgs a{x, r, table, table2, gamma, beta, y, s_out, mean, rstd, rows, table_period, eps, drop_p, drop_mode,
+              seed, offset};
+  if (dtype == EEGF_F32) return ln_fwd_t<float>(width / 256, a, stream);
+  if (dtype == EEGF_BF16) return ln_fwd_t<bf16>(width / 256, a, stream);
+  return EEGF_ERR_ARG;
+}
+
+extern "C" long eegf_ln_bwd_partial_rows(long rows) {
+  (void)rows;
+  return 64;  // rows per block of eegf_ln_bwd: partial buffers hold ceil(rows/64) x width floats
+}
+
+extern "C" int eegf_ln_bwd(int dtype, long rows, int width, const void* dy, const void* s, const float* mean,
+                           const float* rstd, const float* gamma, float drop_p, int drop_mode,
+                           unsigned long long seed, unsigned long long offset, void* dx, void* dr,
+                           float* dgamma_part, float* dbeta_part, hipStream_t stream) {
+  if (rows <= 0 || width % 256 != 0 || width > 1024 || !dy || !s || !mean || !rstd || !gamma) return EEGF_ERR_ARG;
+  if (drop_p < 0.f || drop_p >= 1.f || drop_mode < 0 || drop_mode > 2) return EEGF_ERR_ARG;
+  LnBwdArgs a{dy, s, mean, rstd, gamma, dx, dr, dgamma_part, dbeta_part, rows, 64, drop_p, drop_mode, seed, offset};
+  if (dtype == EEGF_F32) return ln_bwd_t<float>(width / 256, a, stream);
+  if (dtype == EEGF_BF16) return ln_bwd_t<bf16>(width / 256, a, stream);
+  return EEGF_ERR_ARG;
+}
+
+extern "C" int eegf_colsum(int dtype, const void* in, long ld, long rows, int width, int period, float* ws,
+                           long ws_elems, float* out, float beta, hipStream_t stream) {
+  if (!in || !ws || !out || rows <= 0 || width <= 0 || period <= 0 || period > 65535) return EEGF_ERR_ARG;
+  if (dtype == EEGF_F32) return colsum_t<float>(in, ld, rows, width, period, ws, ws_elems, out, beta, stream);
+  if (dtype == EEGF_BF16) return colsum_t<bf16>(in, ld, rows, width, period, ws, ws_elems, out, beta, stream);
+  return EEGF_ERR_ARG;
+}

@@ -16,6 +16,7 @@ F32, BF16 = 0, 1
 ERR_ARG = -1
 
 EPI_NONE, EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_RELU, EPI_BIAS_TANH, EPI_DGELU, EPI_DRELU, EPI_DTANH = range(8)
+FUSE_CONCAT, FUSE_PRICONCAT, FUSE_PRICONCAT_LAP, FUSE_PRIGUMBEL = range(4)
 
 i32, i64, f32, u64, vp = C.c_int, C.c_long, C.c_float, C.c_uint64, C.c_void_p
 
@@ -23,8 +24,31 @@ i32, i64, f32, u64, vp = C.c_int, C.c_long, C.c_float, C.c_uint64, C.c_void_p
 SIGNATURES: dict[str, list] = {
     "eegf_gemm": [i32, i32, i32, i32, i32, i32, i32, i32, i32,
                   vp, i64, i64, vp, i64, i64, vp, i64, i64,
-                  vp, vp, i64, i64, f32, f32, f32, vp],
+                  vp, i64, vp, i64, i64, f32, f32, f32, vp],
+    "eegf_ln_fwd": [i32, i64, i32, vp, vp, vp, i32, vp, vp, vp, f32, f32, i32, u64, u64, vp, vp, vp, vp, vp],
+    "eegf_ln_bwd_partial_rows": [i64],
+    "eegf_ln_bwd": [i32, i64, i32, vp, vp, vp, vp, vp, f32, i32, u64, u64, vp, vp, vp, vp, vp],
+    "eegf_colsum": [i32, vp, i64, i64, i32, i32, vp, i64, vp, f32, vp],
+    "eegf_attn_fwd": [i32, i32, i32, i32, vp, i64, vp, f32, vp, i64, vp, vp],
+    "eegf_attn_bwd_workspace": [i32, i32],
+    "eegf_attn_bwd": [i32, i32, i32, i32, vp, i64, vp, f32, vp, vp, i64, vp, vp, vp, vp],
+    "eegf_xattn_fwd": [i32, i32, i32, vp, vp, vp, vp, vp, vp],
+    "eegf_xattn_bwd": [i32, i32, i32, vp, vp, vp, vp, vp, f32, vp, vp],
+    "eegf_fusion_fwd": [i32, i32, i32, vp, i64, vp, i64, vp, i64, vp, vp, vp, vp, i32, i32, f32, f32, u64, u64,
+                        vp, vp, vp, vp, vp, vp],
+    "eegf_fusion_bwd": [i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, f32, u64, u64,
+                        vp, i64, vp, i64, vp, i64, vp, vp],
+    "eegf_cross_entropy": [i32, i32, i32, vp, vp, i32, f32, vp, vp, vp, vp],
+    "eegf_adam": [i64, vp, vp, vp, vp, vp, f32, f32, f32, f32, f32, i32, vp],
+    "eegf_cast_f32_bf16": [i64, vp, vp, vp],
+    "eegf_axpby": [i32, i64, f32, vp, f32, vp, vp],
+    "eegf_tanh_bwd": [i32, i64, vp, vp, vp, vp],
+    "eegf_key_bias": [i64, vp, vp, vp],
+    "eegf_window_tokens": [i32, i32, i32, i32, vp, vp, vp],
+    "eegf_embed_gather": [i32, i64, i32, vp, vp, vp, vp],
+    "eegf_embed_scatter_add": [i32, i64, i32, vp, vp, vp, vp],
 }
+RESTYPE_LONG = {"eegf_ln_bwd_partial_rows", "eegf_attn_bwd_workspace"}
 
 
 def register(name: str, argtypes: list) -> None:
@@ -42,7 +66,7 @@ def lib() -> C.CDLL:
         for name, argtypes in SIGNATURES.items():
             fn = getattr(_LIB, name)
             fn.argtypes = argtypes
-            fn.restype = C.c_int
+            fn.restype = C.c_long if name in RESTYPE_LONG else C.c_int
     return _LIB
 
 

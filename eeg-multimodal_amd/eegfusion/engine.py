@@ -1,0 +1,558 @@
+"""FusionEngine — the MI355X forward/backward of the whole fusion path over a ParamArena.
+
+Every FLOP is a libeegfusion.so launch on torch's current stream; this module only sequences the
+launches, owns activation buffers and routes gradients into the arena.  The op sequence restates
+ConcatModel.forward (model.py:34-64, past_acc.py:108-139, main_0430.py:108-123) with the BERT
+encoder (transformers modeling_bert.py) and the 3-layer post-norm TransformerDecoder
+(torch transformer.py) expanded into fused kernels:
+
+  EEG  : window->tokens | eeg_encoder GEMM | +pos+type, LN (+drop)           (contract W)
+         word gather     | +pos+type, LN (+drop)                               (contract T)
+         12 x [QKV GEMM | flash attention | out GEMM | drop+res+LN | FFN1 GEMM+GELU | FFN2 GEMM | drop+res+LN]
+         pooler GEMM+tanh (CLS row read in place, lda = L*768)
+  act  : visual_encoder GEMM
+  dec  : 3 x [v GEMM | out GEMM | drop+res+LN1 | q GEMM | q' = Wk^T q/8 (batched GEMM) |
+              memory softmax/context (eegf_xattn_fwd) | Wv c + bv (batched GEMM) | out GEMM |
+              drop+res+LN2 | linear1+ReLU | linear2 | drop+res+LN3]
+  fuse : concat + min-max + PriGumbel gate / PriConcat mechanism (one kernel)
+  head : fc0+ReLU | fc2+tanh | classifier
+Backward runs the same list in reverse with dgrad/wgrad GEMMs, fused epilogues for the activation
+derivatives, LN backward with deterministic partial sums and column reductions for biases.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import torch
+
+from . import _lib
+from ._lib import BF16, F32, call
+from .arena import ParamArena
+
+HID, NH, DH, FFN, NL = 768, 12, 64, 3072, 12
+DEC_FF, DEC_L = 2048, 3
+FUSED = 3 * HID
+VARIANTS = {"concat": _lib.FUSE_CONCAT, "priconcat": _lib.FUSE_PRICONCAT,
+            "priconcat_lap": _lib.FUSE_PRICONCAT_LAP, "prigumbel": _lib.FUSE_PRIGUMBEL}
+
+
+def P(t):
+    return None if t is None else t.data_ptr()
+
+
+@dataclass
+class EngineConfig:
+    contract: str = "W"            # "W" window / "T" token ids
+    variant: str = "prigumbel"     # concat | priconcat | priconcat_lap | prigumbel
+    dtype: torch.dtype = torch.bfloat16
+    eps: float = 1.0
+    eps_mode: str = "newfrac"
+    hidden_dropout: float = 0.1    # BertConfig.hidden_dropout_prob
+    attn_dropout: float = 0.1      # attention_probs_dropout_prob (not yet fused)
+    dec_dropout: float = 0.1       # TransformerDecoderLayer(dropout=0.1)
+    eeg_channels: int = 64
+    act_dim: int = 32
+    seed: int = 980616
+
+
+@dataclass
+class Saved:
+    B: int = 0
+    L: int = 0
+    hard: bool = False
+    training: bool = True
+    rng: int = 0
+    t: dict = field(default_factory=dict)
+
+
+class Workspace:
+    """Reusable scratch buffers keyed by name (grown on demand)."""
+
+    def __init__(self, device):
+        self.device = device
+        self.bufs: dict[str, torch.Tensor] = {}
+
+    def get(self, name, numel, dtype):
+        b = self.bufs.get(name)
+        if b is None or b.numel() < numel or b.dtype != dtype:
+            b = torch.empty(max(numel, 1), dtype=dtype, device=self.device)
+            self.bufs[name] = b
+        return b[:numel]
+
+
+class FusionEngine:
+    def __init__(self, arena: ParamArena, cfg: EngineConfig):
+        self.a = arena
+        self.cfg = cfg
+        self.dt = cfg.dtype
+        self.code = F32 if cfg.dtype == torch.float32 else BF16
+        self.variant = VARIANTS[cfg.variant]
+        self.ws = Workspace(arena.device)
+        self.rng_counter = 0
+        self.injected = None        # parity hook: dict(noise=..., gumbels=..., row_noise=...)
+        self.needs_grad: set[str] | None = None
+
+    # ------------------------------------------------------------------ parameter access
+    def _refresh_shadow(self):
+        a = self.a
+        if self.dt == torch.float32:
+            return
+        v = a.master._version
+        if a.shadow is None:
+            a.shadow = torch.empty(a.numel, dtype=torch.bfloat16, device=a.device)
+            a.shadow_version = -1
+        if a.shadow_version != v:
+            call("eegf_cast_f32_bf16", a.numel, P(a.master), P(a.shadow), _stream())
+            a.shadow_version = v
+
+    def W(self, name):
+        """weight in compute dtype"""
+        return self.a.view(name, self.a.shadow if self.dt != torch.float32 else None)
+
+    def Wspan(self, first, n):
+        return self.a.span(first, n, self.a.shadow if self.dt != torch.float32 else None)
+
+    def F(self, name):
+        """fp32 master (biases, LN params, tables, DP)"""
+        return self.a.view(name)
+
+    def G(self, name):
+        return self.a.gview(name)
+
+    def need(self, name):
+        return self.needs_grad is None or name in self.needs_grad
+
+    # --------------------------------------------------------------------- primitives
+    def empty(self, *shape, dtype=None):
+        return torch.empty(*shape, dtype=dtype or self.dt, device=self.a.device)
+
+    def gemm(self, A, B, C, M, N, K, a_kc, b_kc, lda, ldb, ldc, epi=_lib.EPI_NONE, bias=None, aux=None, ldaux=0,
+             alpha=1.0, beta=0.0, scale=1.0, batch=1, sA=0, sB=0, sC=0, sAux=0, sBias=0):
+        call("eegf_gemm", self.code, F32 if C.dtype == torch.float32 else BF16, a_kc, b_kc, epi, M, N, K, batch,
+             P(A), lda, sA, P(B), ldb, sB, P(C), ldc, sC, P(bias), sBias, P(aux), ldaux, sAux,
+             float(alpha), float(beta), float(scale), _stream())
+        return C
+
+    def linear(self, x, w, b, out, M, lda=None, epi=None, aux=None):
+        N, K = w.shape
+        if epi is None:
+            epi = _lib.EPI_BIAS if b is not None else _lib.EPI_NONE
+        return self.gemm(x, w, out, M, N, K, 1, 1, lda or K, K, out.shape[-1], epi=epi, bias=b, aux=aux,
+                         ldaux=(aux.shape[-1] if aux is not None else 0))
+
+    def dgrad(self, dy, w, out, M, ldd=None, ldo=None, epi=_lib.EPI_NONE, aux=None, scale=1.0, beta=0.0):
+        N, K = w.shape
+        return self.gemm(dy, w, out, M, K, N, 1, 0, ldd or N, K, ldo or K, epi=epi, aux=aux,
+                         ldaux=(aux.shape[-1] if aux is not None else 0), scale=scale, beta=beta)
+
+    def wgrad(self, dy, x, name, M, ldd=None, ldx=None):
+        if not self.need(name):
+            return
+        g = self.G(name)
+        N, K = g.shape
+        self.gemm(dy, x, g, N, K, M, 0, 0, ldd or N, ldx or K, K, beta=1.0)
+
+    def bgrad(self, dy, name, rows, width=None, ld=None, period=1, out=None):
+        if out is None and not self.need(name):
+            return
+        o = out if out is not None else self.G(name)
+        width = width or o.shape[-1]
+        ws = self.ws.get("colsum", 1 << 24, torch.float32)
+        call("eegf_colsum", _code(dy), P(dy), ld or width, rows, width, period, P(ws), ws.numel(), P(o), 1.0,
+             _stream())
+
+    def ln_fwd(self, x, r, pre, rows, out, s, mean, rstd, eps, p=0.0, mode=0, rng=0, table=None, period=1,
+               table2=None):
+        call("eegf_ln_fwd", self.code, rows, HID, P(x), P(r), P(table), period, P(table2), P(self.F(pre + ".weight")),
+             P(self.F(pre + ".bias")), float(eps), float(p), int(mode if p > 0 else 0), self.cfg.seed, rng, P(out),
+             P(s), P(mean), P(rstd), _stream())
+
+    def ln_bwd(self, dy, s, mean, rstd, pre, rows, dx, dr, p=0.0, mode=0, rng=0):
+        nb = (rows + 63) // 64
+        part = self.ws.get("ln_part", 2 * nb * HID, torch.float32)
+        call("eegf_ln_bwd", self.code, rows, HID, P(dy), P(s), P(mean), P(rstd), P(self.F(pre + ".weight")), float(p),
+             int(mode if p > 0 else 0), self.cfg.seed, rng, P(dx), P(dr), P(part), P(part[nb * HID:]), _stream())
+        self.bgrad(part[: nb * HID], pre + ".weight", nb, HID)
+        self.bgrad(part[nb * HID:], pre + ".bias", nb, HID)
+
+    # =================================================================== forward
+    def forward(self, batch: dict, hard: bool, training: bool, save: bool = True):
+        """batch (device tensors): contract W: eeg [B,C,T] f32, act [B,A] f32;
+        contract T: title_input [B,L] i64, text_mask [B,L] i64, frame_input [B,1,512] f32."""
+        cfg = self.cfg
+        self._refresh_shadow()
+        sv = Saved(hard=hard, training=training)
+        t = sv.t
+        sv.rng = self.rng_counter
+        self.rng_counter += 1 << 12
+        pdrop = cfg.hidden_dropout if training else 0.0
+        ddrop = cfg.dec_dropout if training else 0.0
+
+        # ---------------- EEG front-end + BERT embeddings
+        if cfg.contract == "W":
+            eeg = batch["eeg"]
+            B, C, L = eeg.shape
+            tok = self.empty(B * L, C)
+            call("eegf_window_tokens", self.code, B, C, L, P(eeg), P(tok), _stream())
+            x = self.empty(B * L, HID)
+            self.linear(tok, self.W("eeg_encoder.weight"), self.F("eeg_encoder.bias"), x, B * L)
+            kbias = None
+            t["tok"] = tok
+        else:
+            ids = batch["title_input"]
+            B, L = ids.shape
+            x = self.empty(B * L, HID)
+            call("eegf_embed_gather", self.code, B * L, HID, P(ids), P(self.F("bert.embeddings.word_embeddings.weight")),
+                 P(x), _stream())
+            mask = batch["text_mask"]
+            kbias = torch.empty(B, L, dtype=torch.float32, device=self.a.device)
+            call("eegf_key_bias", B * L, P(mask), P(kbias), _stream())
+            t["ids"] = ids
+        sv.B, sv.L = B, L
+        R = B * L
+        t["kbias"] = kbias
+        e = "bert.embeddings."
+        h = self.empty(R, HID)
+        s0, m0, r0 = self.empty(R, HID), self._f32(R), self._f32(R)
+        self.ln_fwd(x, None, e + "LayerNorm", R, h, s0, m0, r0, 1e-12, pdrop, 2, sv.rng + 1,
+                    table=self.F(e + "position_embeddings.weight"), period=L,
+                    table2=self.F(e + "token_type_embeddings.weight"))
+        t["emb"] = (s0, m0, r0)
+        scale = DH ** -0.5
+
+        # ---------------- BERT encoder
+        layers = []
+        for i in range(NL):
+            pre = f"bert.encoder.layer.{i}."
+            qkv = self.empty(R, 3 * HID)
+            self.linear(h, self.Wspan(pre + "attention.self.query.weight", 3).view(3 * HID, HID),
+                        self.a.span(pre + "attention.self.query.bias", 3), qkv, R)
+            ctx = self.empty(R, HID)
+            lse = torch.empty(B, NH, L, dtype=torch.float32, device=self.a.device)
+            call("eegf_attn_fwd", self.code, B, NH, L, P(qkv), 3 * HID, P(kbias), scale, P(ctx), HID, P(lse), _stream())
+            ao = self.ws.get("ao", R * HID, self.dt).view(R, HID)
+            self.linear(ctx, self.W(pre + "attention.output.dense.weight"), self.F(pre + "attention.output.dense.bias"),
+                        ao, R)
+            a1 = self.empty(R, HID)
+            s1, m1, r1 = self.empty(R, HID), self._f32(R), self._f32(R)
+            self.ln_fwd(ao, h, pre + "attention.output.LayerNorm", R, a1, s1, m1, r1, 1e-12, pdrop, 1,
+                        sv.rng + 10 + 3 * i)
+            ffpre, ffact = self.empty(R, FFN), self.empty(R, FFN)
+            self.linear(a1, self.W(pre + "intermediate.dense.weight"), self.F(pre + "intermediate.dense.bias"), ffact,
+                        R, epi=_lib.EPI_BIAS_GELU, aux=ffpre)
+            fo = self.ws.get("fo", R * HID, self.dt).view(R, HID)
+            self.linear(ffact, self.W(pre + "output.dense.weight"), self.F(pre + "output.dense.bias"), fo, R)
+            h2 = self.empty(R, HID)
+            s2, m2, r2 = self.empty(R, HID), self._f32(R), self._f32(R)
+            self.ln_fwd(fo, a1, pre + "output.LayerNorm", R, h2, s2, m2, r2, 1e-12, pdrop, 1, sv.rng + 11 + 3 * i)
+            if save:
+                layers.append(dict(h=h, qkv=qkv, ctx=ctx, lse=lse, a1=a1, ln1=(s1, m1, r1), ffpre=ffpre, ffact=ffact,
+                                   ln2=(s2, m2, r2)))
+            h = h2
+        t["layers"] = layers
+        t["mem"] = h
+        pooled = self.empty(B, HID)
+        self.linear(h, self.W("bert.pooler.dense.weight"), self.F("bert.pooler.dense.bias"), pooled, B, lda=L * HID,
+                    epi=_lib.EPI_BIAS_TANH)
+        t["pooled"] = pooled
+
+        # ---------------- action encoder
+        if cfg.contract == "W":
+            act = batch["act"]
+        else:
+            act = batch["frame_input"].reshape(B, -1)
+        act_t = act if self.dt == torch.float32 else self.empty(act.shape)
+        if self.dt != torch.float32:
+            call("eegf_cast_f32_bf16", act.numel(), P(act.contiguous()), P(act_t), _stream())
+        vis = self.empty(B, HID)
+        self.linear(act_t, self.W("visual_encoder.weight"), self.F("visual_encoder.bias"), vis, B)
+        t["act"], t["vis"] = act_t, vis
+
+        # ---------------- decoder (single query token)
+        x = vis
+        dl = []
+        for d in range(DEC_L):
+            pre = f"multi_head_decoder.layers.{d}."
+            in_w, in_b = self.W(pre + "self_attn.in_proj_weight"), self.F(pre + "self_attn.in_proj_bias")
+            v = self.empty(B, HID)
+            self.linear(x, in_w[2 * HID:], in_b[2 * HID:], v, B)
+            sa = self.ws.get("dsa", B * HID, self.dt).view(B, HID)
+            self.linear(v, self.W(pre + "self_attn.out_proj.weight"), self.F(pre + "self_attn.out_proj.bias"), sa, B)
+            x1, ln1 = self.empty(B, HID), (self.empty(B, HID), self._f32(B), self._f32(B))
+            self.ln_fwd(sa, x, pre + "norm1", B, x1, *ln1, 1e-5, ddrop, 1, sv.rng + 100 + 8 * d)
+            cw, cb = self.W(pre + "multihead_attn.in_proj_weight"), self.F(pre + "multihead_attn.in_proj_bias")
+            q = self.empty(B, HID)
+            self.linear(x1, cw[:HID], cb[:HID], q, B)
+            qp = self.empty(B, NH, HID)
+            # qp[b,h,:] = Wk_h^T q_h / 8   (batched over heads)
+            self.gemm(q, cw[HID:2 * HID], qp, B, HID, DH, 1, 0, HID, HID, NH * HID, alpha=scale, batch=NH, sA=DH,
+                      sB=DH * HID, sC=HID)
+            probs = torch.empty(B, NH, L, dtype=torch.float32, device=self.a.device)
+            cc = self.empty(B, NH, HID)
+            call("eegf_xattn_fwd", self.code, B, L, P(h), P(qp), P(kbias), P(probs), P(cc), _stream())
+            ctxd = self.empty(B, HID)
+            # ctx[b, h*64+n] = sum_c cc[b,h,c] Wv[h*64+n, c] + bv[h*64+n]
+            self.gemm(cc, cw[2 * HID:], ctxd, B, DH, HID, 1, 1, NH * HID, HID, HID, epi=_lib.EPI_BIAS,
+                      bias=cb[2 * HID:], batch=NH, sA=HID, sB=DH * HID, sC=DH, sBias=DH)
+            ca = self.ws.get("dca", B * HID, self.dt).view(B, HID)
+            self.linear(ctxd, self.W(pre + "multihead_attn.out_proj.weight"),
+                        self.F(pre + "multihead_attn.out_proj.bias"), ca, B)
+            x2, ln2 = self.empty(B, HID), (self.empty(B, HID), self._f32(B), self._f32(B))
+            self.ln_fwd(ca, x1, pre + "norm2", B, x2, *ln2, 1e-5, ddrop, 1, sv.rng + 101 + 8 * d)
+            f1 = self.empty(B, DEC_FF)
+            self.linear(x2, self.W(pre + "linear1.weight"), self.F(pre + "linear1.bias"), f1, B, epi=_lib.EPI_BIAS_RELU)
+            f2 = self.ws.get("df2", B * HID, self.dt).view(B, HID)
+            self.linear(f1, self.W(pre + "linear2.weight"), self.F(pre + "linear2.bias"), f2, B)
+            x3, ln3 = self.empty(B, HID), (self.empty(B, HID), self._f32(B), self._f32(B))
+            self.ln_fwd(f2, x2, pre + "norm3", B, x3, *ln3, 1e-5, ddrop, 1, sv.rng + 102 + 8 * d)
+            dl.append(dict(x=x, v=v, x1=x1, ln1=ln1, q=q, qp=qp, probs=probs, cc=cc, ctx=ctxd, x2=x2, ln2=ln2, f1=f1,
+                           ln3=ln3))
+            x = x3
+        t["dec"] = dl
+        cross = x
+
+        # ---------------- fusion + privacy stage
+        g = self.empty(B, FUSED)
+        xn = self._f32(B, FUSED)
+        amin = torch.empty(B, dtype=torch.int32, device=self.a.device)
+        amax = torch.empty_like(amin)
+        rng_ = self._f32(B)
+        inj = self.injected or {}
+        eps_a = math.exp(cfg.eps)
+        call("eegf_fusion_fwd", self.code, B, self.variant, P(pooled), HID, P(vis), HID, P(cross), HID,
+             P(self.F("DP")) if "DP" in self.a.offsets else None, P(inj.get("noise")), P(inj.get("gumbels")),
+             P(inj.get("row_noise")), int(hard), 0 if cfg.eps_mode == "newfrac" else 1, eps_a, 1.0 / cfg.eps,
+             self.cfg.seed, sv.rng + 200, P(g), P(xn), P(amin), P(amax), P(rng_), _stream())
+        t["fuse"] = dict(g=g, xn=xn, amin=amin, amax=amax, range=rng_, inj=inj, cross=cross)
+
+        # ---------------- head
+        z1 = self.empty(B, FUSED)
+        self.linear(g, self.W("fc_layers.0.weight"), self.F("fc_layers.0.bias"), z1, B, epi=_lib.EPI_BIAS_RELU)
+        z2 = self.empty(B, HID)
+        self.linear(z1, self.W("fc_layers.2.weight"), self.F("fc_layers.2.bias"), z2, B, epi=_lib.EPI_BIAS_TANH)
+        logits = self.empty(B, 2)
+        self.linear(z2, self.W("classifier.weight"), self.F("classifier.bias"), logits, B)
+        t["head"] = dict(z1=z1, z2=z2)
+        return logits, sv
+
+    def _f32(self, *shape):
+        return torch.empty(*shape, dtype=torch.float32, device=self.a.device)
+
+    # =================================================================== backward
+    def backward(self, sv: Saved, dlogits: torch.Tensor, head_only: bool = False):
+        """Accumulate parameter gradients into the arena grad buffer (beta = 1 everywhere; the
+        caller zeroes the ranges it overwrites).  head_only: stop after the privacy stage
+        (DP gradient only — the PriGumbel DP pass)."""
+        cfg = self.cfg
+        t = sv.t
+        B, L = sv.B, sv.L
+        R = B * L
+        pdrop = cfg.hidden_dropout if sv.training else 0.0
+        ddrop = cfg.dec_dropout if sv.training else 0.0
+        dlogits = dlogits.to(self.dt).contiguous()
+        hd = t["head"]
+        fz = t["fuse"]
+        g = fz["g"]
+
+        # ---------------- head
+        self.wgrad(dlogits, hd["z2"], "classifier.weight", B)
+        self.bgrad(dlogits, "classifier.bias", B)
+        dz2 = self.empty(B, HID)
+        self.dgrad(dlogits, self.W("classifier.weight"), dz2, B, epi=_lib.EPI_DTANH, aux=hd["z2"])
+        self.wgrad(dz2, hd["z1"], "fc_layers.2.weight", B)
+        self.bgrad(dz2, "fc_layers.2.bias", B)
+        dz1 = self.empty(B, FUSED)
+        self.dgrad(dz2, self.W("fc_layers.2.weight"), dz1, B, epi=_lib.EPI_DRELU, aux=hd["z1"])
+        self.wgrad(dz1, g, "fc_layers.0.weight", B)
+        self.bgrad(dz1, "fc_layers.0.bias", B)
+        dg = self.empty(B, FUSED)
+        self.dgrad(dz1, self.W("fc_layers.0.weight"), dg, B)
+
+        # ---------------- fusion / privacy stage
+        dpooled, dvis, dcross = self.empty(B, HID), self.empty(B, HID), self.empty(B, HID)
+        has_dp = "DP" in self.a.offsets and self.variant == _lib.FUSE_PRIGUMBEL and self.need("DP")
+        ddp = self._f32(B, FUSED) if has_dp else None
+        inj = fz["inj"]
+        call("eegf_fusion_bwd", self.code, B, self.variant, P(dg), P(fz["xn"]), P(fz["amin"]), P(fz["amax"]),
+             P(fz["range"]), P(self.F("DP")) if "DP" in self.a.offsets else None, P(inj.get("noise")),
+             P(inj.get("gumbels")), int(sv.hard), 0 if cfg.eps_mode == "newfrac" else 1, math.exp(cfg.eps),
+             self.cfg.seed, sv.rng + 200, P(dpooled), HID, P(dvis), HID, P(dcross), HID, P(ddp), _stream())
+        if has_dp:
+            self.bgrad(ddp, "DP", B, FUSED)
+        if head_only:
+            return
+
+        # ---------------- decoder backward
+        mem = t["mem"]
+        dmem = self.empty(R, HID)
+        dx3 = dcross
+        scale = DH ** -0.5
+        for d in reversed(range(DEC_L)):
+            pre = f"multi_head_decoder.layers.{d}."
+            s = t["dec"][d]
+            # LN3: x3 = LN(drop(f2) + x2)
+            df2, dx2 = self.empty(B, HID), self.empty(B, HID)
+            self.ln_bwd(dx3, *s["ln3"], pre + "norm3", B, df2, dx2, ddrop, 1, sv.rng + 102 + 8 * d)
+            self.wgrad(df2, s["f1"], pre + "linear2.weight", B)
+            self.bgrad(df2, pre + "linear2.bias", B)
+            df1 = self.empty(B, DEC_FF)
+            self.dgrad(df2, self.W(pre + "linear2.weight"), df1, B, epi=_lib.EPI_DRELU, aux=s["f1"])
+            self.wgrad(df1, s["x2"], pre + "linear1.weight", B)
+            self.bgrad(df1, pre + "linear1.bias", B)
+            self.dgrad(df1, self.W(pre + "linear1.weight"), dx2, B, beta=1.0)
+            # LN2: x2 = LN(drop(ca) + x1)
+            dca, dx1 = self.empty(B, HID), self.empty(B, HID)
+            self.ln_bwd(dx2, *s["ln2"], pre + "norm2", B, dca, dx1, ddrop, 1, sv.rng + 101 + 8 * d)
+            self.wgrad(dca, s["ctx"], pre + "multihead_attn.out_proj.weight", B)
+            self.bgrad(dca, pre + "multihead_attn.out_proj.bias", B)
+            dctx = self.empty(B, HID)
+            self.dgrad(dca, self.W(pre + "multihead_attn.out_proj.weight"), dctx, B)
+            cw = self.W(pre + "multihead_attn.in_proj_weight")
+            gname = pre + "multihead_attn.in_proj_weight"
+            bname = pre + "multihead_attn.in_proj_bias"
+            if self.need(gname):
+                gw = self.G(gname)
+                # dWv_h[n, c] = sum_b dctx[b, h*64+n] cc[b,h,c]
+                self.gemm(dctx, s["cc"], gw[2 * HID:], DH, HID, B, 0, 0, HID, NH * HID, HID, beta=1.0, batch=NH,
+                          sA=DH, sB=HID, sC=DH * HID)
+            if self.need(bname):
+                self.bgrad(dctx, bname, B, out=self.G(bname)[2 * HID:])
+            dcc = self.empty(B, NH, HID)
+            # dcc[b,h,c] = sum_n dctx[b, h*64+n] Wv[h*64+n, c]
+            self.gemm(dctx, cw[2 * HID:], dcc, B, HID, DH, 1, 0, HID, HID, NH * HID, batch=NH, sA=DH, sB=DH * HID,
+                      sC=HID)
+            dqp = self.empty(B, NH, HID)
+            call("eegf_xattn_bwd", self.code, B, L, P(mem), P(s["qp"]), P(s["probs"]), P(dcc), P(dmem),
+                 0.0 if d == DEC_L - 1 else 1.0, P(dqp), _stream())
+            dq = self.empty(B, HID)
+            # dq[b, h*64+i] = sum_c dqp[b,h,c] Wk[h*64+i, c] / 8
+            self.gemm(dqp, cw[HID:2 * HID], dq, B, DH, HID, 1, 1, NH * HID, HID, HID, alpha=scale, batch=NH, sA=HID,
+                      sB=DH * HID, sC=DH)
+            if self.need(gname):
+                # dWk_h[i, c] = sum_b q[b, h*64+i] dqp[b,h,c] / 8
+                self.gemm(s["q"], dqp, gw[HID:2 * HID], DH, HID, B, 0, 0, HID, NH * HID, HID, alpha=scale, beta=1.0,
+                          batch=NH, sA=DH, sB=HID, sC=DH * HID)
+                self.gemm(dq, s["x1"], gw[:HID], HID, HID, B, 0, 0, HID, HID, HID, beta=1.0)
+            if self.need(bname):
+                self.bgrad(dq, bname, B, out=self.G(bname)[:HID])
+            self.dgrad(dq, cw[:HID], dx1, B, beta=1.0)
+            # LN1: x1 = LN(drop(sa) + x)
+            dsa, dx = self.empty(B, HID), self.empty(B, HID)
+            self.ln_bwd(dx1, *s["ln1"], pre + "norm1", B, dsa, dx, ddrop, 1, sv.rng + 100 + 8 * d)
+            self.wgrad(dsa, s["v"], pre + "self_attn.out_proj.weight", B)
+            self.bgrad(dsa, pre + "self_attn.out_proj.bias", B)
+            dv = self.empty(B, HID)
+            self.dgrad(dsa, self.W(pre + "self_attn.out_proj.weight"), dv, B)
+            sw = self.W(pre + "self_attn.in_proj_weight")
+            if self.need(pre + "self_attn.in_proj_weight"):
+                self.gemm(dv, s["x"], self.G(pre + "self_attn.in_proj_weight")[2 * HID:], HID, HID, B, 0, 0, HID, HID,
+                          HID, beta=1.0)
+            if self.need(pre + "self_attn.in_proj_bias"):
+                self.bgrad(dv, pre + "self_attn.in_proj_bias", B, out=self.G(pre + "self_attn.in_proj_bias")[2 * HID:])
+            self.dgrad(dv, sw[2 * HID:], dx, B, beta=1.0)
+            dx3 = dx
+        # vis receives the fusion path + the decoder path
+        call("eegf_axpby", self.code, B * HID, 1.0, P(dx3), 1.0, P(dvis), _stream())
+        self.wgrad(dvis, t["act"], "visual_encoder.weight", B)
+        self.bgrad(dvis, "visual_encoder.bias", B)
+
+        # ---------------- pooler
+        pooled = t["pooled"]
+        dpp = self.empty(B, HID)
+        call("eegf_tanh_bwd", self.code, B * HID, P(dpooled), P(pooled), P(dpp), _stream())
+        self.wgrad(dpp, mem, "bert.pooler.dense.weight", B, ldx=L * HID)
+        self.bgrad(dpp, "bert.pooler.dense.bias", B)
+        self.dgrad(dpp, self.W("bert.pooler.dense.weight"), dmem, B, ldo=L * HID, beta=1.0)
+
+        # ---------------- BERT encoder backward
+        dh = dmem
+        dfo = self.ws.get("b_dfo", R * HID, self.dt).view(R, HID)
+        da = self.ws.get("b_da", R * HID, self.dt).view(R, HID)
+        dffp = self.ws.get("b_dffp", R * FFN, self.dt).view(R, FFN)
+        dao = self.ws.get("b_dao", R * HID, self.dt).view(R, HID)
+        dctx = self.ws.get("b_dctx", R * HID, self.dt).view(R, HID)
+        dqkv = self.ws.get("b_dqkv", R * 3 * HID, self.dt).view(R, 3 * HID)
+        dq_ws_n = _lib.lib().eegf_attn_bwd_workspace(B, L)
+        dq_ws = self.ws.get("b_dqws", dq_ws_n, torch.float32) if dq_ws_n > 0 else None
+        lowest = self._lowest_needed_layer()
+        for i in reversed(range(NL)):
+            if i < lowest:
+                break
+            pre = f"bert.encoder.layer.{i}."
+            s = t["layers"][i]
+            dhn = self.ws.get(f"b_dh{i % 2}", R * HID, self.dt).view(R, HID)
+            self.ln_bwd(dh, *s["ln2"], pre + "output.LayerNorm", R, dfo, da, pdrop, 1, sv.rng + 11 + 3 * i)
+            self.wgrad(dfo, s["ffact"], pre + "output.dense.weight", R)
+            self.bgrad(dfo, pre + "output.dense.bias", R)
+            self.dgrad(dfo, self.W(pre + "output.dense.weight"), dffp, R, epi=_lib.EPI_DGELU, aux=s["ffpre"])
+            self.wgrad(dffp, s["a1"], pre + "intermediate.dense.weight", R)
+            self.bgrad(dffp, pre + "intermediate.dense.bias", R)
+            self.dgrad(dffp, self.W(pre + "intermediate.dense.weight"), da, R, beta=1.0)
+            self.ln_bwd(da, *s["ln1"], pre + "attention.output.LayerNorm", R, dao, dhn, pdrop, 1, sv.rng + 10 + 3 * i)
+            self.wgrad(dao, s["ctx"], pre + "attention.output.dense.weight", R)
+            self.bgrad(dao, pre + "attention.output.dense.bias", R)
+            self.dgrad(dao, self.W(pre + "attention.output.dense.weight"), dctx, R)
+            call("eegf_attn_bwd", self.code, B, NH, L, P(s["qkv"]), 3 * HID, P(t["kbias"]), scale, P(s["ctx"]),
+                 P(dctx), HID, P(s["lse"]), P(dqkv), P(dq_ws), _stream())
+            qn = pre + "attention.self.query.weight"
+            if self.need(qn):
+                gq = self.a.span(qn, 3, self.a.grad).view(3 * HID, HID)
+                self.gemm(dqkv, s["h"], gq, 3 * HID, HID, R, 0, 0, 3 * HID, HID, HID, beta=1.0)
+            bn = pre + "attention.self.query.bias"
+            if self.need(bn):
+                self.bgrad(dqkv, bn, R, width=3 * HID, out=self.a.span(bn, 3, self.a.grad))
+            if i > lowest or lowest == 0:
+                self.dgrad(dqkv, self.Wspan(qn, 3).view(3 * HID, HID), dhn, R, beta=1.0)
+            dh = dhn
+        if lowest > 0:
+            return
+        # ---------------- embeddings
+        e = "bert.embeddings."
+        demb = self.ws.get("b_demb", R * HID, self.dt).view(R, HID)
+        self.ln_bwd(dh, *t["emb"], e + "LayerNorm", R, demb, None, pdrop, 2, sv.rng + 1)
+        if self.need(e + "position_embeddings.weight"):
+            self.bgrad(demb, e + "position_embeddings.weight", R, width=HID, period=L,
+                       out=self.G(e + "position_embeddings.weight")[:L])
+        if self.need(e + "token_type_embeddings.weight"):
+            self.bgrad(demb, e + "token_type_embeddings.weight", R, width=HID,
+                       out=self.G(e + "token_type_embeddings.weight")[0])
+        if cfg.contract == "W":
+            self.wgrad(demb, t["tok"], "eeg_encoder.weight", R)
+            self.bgrad(demb, "eeg_encoder.bias", R)
+        elif self.need(e + "word_embeddings.weight"):
+            call("eegf_embed_scatter_add", self.code, R, HID, P(t["ids"]), P(demb),
+                 P(self.G(e + "word_embeddings.weight")), _stream())
+
+    def _lowest_needed_layer(self) -> int:
+        if self.needs_grad is None:
+            return 0
+        emb = any(n.startswith(("bert.embeddings", "eeg_encoder")) for n in self.needs_grad)
+        if emb:
+            return 0
+        for i in range(NL):
+            if any(n.startswith(f"bert.encoder.layer.{i}.") for n in self.needs_grad):
+                return i
+        return NL
+
+    # ------------------------------------------------------------- graph membership
+    def graph_params(self) -> set[str]:
+        """Parameters that take part in the forward graph (others keep grad None, as in torch)."""
+        out = set()
+        for n in self.a.offsets:
+            if n.startswith("multi_head_decoderlayer."):
+                continue                                  # unused template layer (model.py:20)
+            if n == "bert.embeddings.word_embeddings.weight" and self.cfg.contract == "W":
+                continue
+            if n == "DP" and self.variant != _lib.FUSE_PRIGUMBEL:
+                continue
+            out.add(n)
+        return out
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _code(t):
+    return F32 if t.dtype == torch.float32 else BF16

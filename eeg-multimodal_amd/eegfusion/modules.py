@@ -1,0 +1,322 @@
+"""Drop-in nn.Module mirrors of the reference model classes, backed by the HIP engine.
+
+The module tree reproduces the reference's attribute names and state_dict keys exactly
+(`bert.embeddings.*`, `bert.encoder.layer.{i}.*`, `bert.pooler.dense.*`, `visual_encoder.*`,
+`multi_head_decoderlayer.*` (unused template, model.py:20), `multi_head_decoder.layers.{0,1,2}.*`,
+`fc_layers.{0,2}.*`, `classifier.*`, `DP`), so `load_state_dict` of a reference checkpoint works and
+callers that touch `.bert.encoder.layer[-1]`, `.fc_layers`, `.classifier`, `.DP`, `.eps`
+(train.py:139, main_0430.py:144-151) keep working.  The submodules are parameter holders only:
+every parameter is a view into the engine's ParamArena and every FLOP runs in libeegfusion.so.
+There is no CPU compute path: forward on CPU tensors raises.
+"""
+from __future__ import annotations
+
+import math
+import os
+
+import torch
+import torch.nn as nn
+
+from .arena import ParamArena
+from .engine import DEC_FF, DEC_L, FFN, FUSED, HID, NL, EngineConfig, FusionEngine
+
+# ------------------------------------------------------------------- name-holding modules
+
+
+class _Holder(nn.Module):
+    def forward(self, *a, **k):  # pragma: no cover - never called
+        raise RuntimeError("eegfusion submodules are parameter holders; call the top-level model")
+
+
+def _linear(i, o, bias=True):
+    m = nn.Linear(i, o, bias=bias)
+    return m
+
+
+def _bert(vocab=30522, max_pos=512):
+    bert = _Holder()
+    emb = _Holder()
+    emb.word_embeddings = nn.Embedding(vocab, HID, padding_idx=0)
+    emb.position_embeddings = nn.Embedding(max_pos, HID)
+    emb.token_type_embeddings = nn.Embedding(2, HID)
+    emb.LayerNorm = nn.LayerNorm(HID, eps=1e-12)
+    bert.embeddings = emb
+    enc = _Holder()
+    layers = []
+    for _ in range(NL):
+        L = _Holder()
+        att = _Holder()
+        selfa = _Holder()
+        selfa.query, selfa.key, selfa.value = _linear(HID, HID), _linear(HID, HID), _linear(HID, HID)
+        att.self = selfa
+        out = _Holder()
+        out.dense = _linear(HID, HID)
+        out.LayerNorm = nn.LayerNorm(HID, eps=1e-12)
+        att.output = out
+        L.attention = att
+        inter = _Holder()
+        inter.dense = _linear(HID, FFN)
+        L.intermediate = inter
+        o2 = _Holder()
+        o2.dense = _linear(FFN, HID)
+        o2.LayerNorm = nn.LayerNorm(HID, eps=1e-12)
+        L.output = o2
+        layers.append(L)
+    enc.layer = nn.ModuleList(layers)
+    bert.encoder = enc
+    pool = _Holder()
+    pool.dense = _linear(HID, HID)
+    bert.pooler = pool
+    return bert
+
+
+def _init_bert_(bert: nn.Module, std=0.02):
+    """BertPreTrainedModel._init_weights: normal(0, 0.02) Linear/Embedding, zero bias, LN = (1, 0)."""
+    for m in bert.modules():
+        if isinstance(m, nn.Linear):
+            nn.init.normal_(m.weight, 0.0, std)
+            nn.init.zeros_(m.bias)
+        elif isinstance(m, nn.Embedding):
+            nn.init.normal_(m.weight, 0.0, std)
+            if m.padding_idx is not None:
+                with torch.no_grad():
+                    m.weight[m.padding_idx].zero_()
+        elif isinstance(m, nn.LayerNorm):
+            nn.init.ones_(m.weight)
+            nn.init.zeros_(m.bias)
+
+
+def _qkv_first_order(named):
+    """Order parameters so each layer's Q/K/V weights then Q/K/V biases are adjacent in the arena."""
+    named = list(named)
+    out, seen = [], set()
+    for n, p in named:
+        if n in seen:
+            continue
+        if n.endswith("attention.self.query.weight"):
+            base = n[: -len("query.weight")]
+            for k in ("query.weight", "key.weight", "value.weight", "query.bias", "key.bias", "value.bias"):
+                out.append((base + k, dict(named)[base + k]))
+                seen.add(base + k)
+        elif ".attention.self." in n:
+            continue
+        else:
+            out.append((n, p))
+            seen.add(n)
+    return out
+
+
+class _PathFunction(torch.autograd.Function):
+    """One autograd node for the whole path: forward/backward are HIP launch sequences; parameter
+    gradients are written straight into the arena and published as `.grad` views."""
+
+    @staticmethod
+    def forward(ctx, model, batch_keys, hard, *tensors):
+        batch = dict(zip(batch_keys, tensors[: len(batch_keys)]))
+        logits, saved = model._engine.forward(batch, hard, model.training, save=True)
+        ctx.model, ctx.saved = model, saved
+        return logits.float()
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        ctx.model._backward(ctx.saved, dlogits)
+        ctx.saved = None
+        return (None, None, None) + (None,) * (len(ctx.needs_input_grad) - 3)
+
+
+class FusionModel(nn.Module):
+    """Common body of ConcatModel / PriConcat / PriGumbel / TICA_LapDropout."""
+
+    def __init__(self, variant: str, contract: str = "T", eps: float = 1.0, eps_mode: str = "newfrac",
+                 dtype: torch.dtype = torch.float32, eeg_channels: int = 64, act_dim: int = 32, frame_dim: int = 512,
+                 with_dp: bool = True, dp_init: torch.Tensor | None = None, dropout: float = 0.1, seed: int = 980616):
+        super().__init__()
+        self._variant, self._contract = variant, contract
+        self.bert = _bert()
+        _init_bert_(self.bert)
+        if contract == "W":
+            self.eeg_encoder = nn.Linear(eeg_channels, HID)
+            self.visual_encoder = nn.Linear(act_dim, HID)
+        else:
+            self.visual_encoder = nn.Linear(frame_dim, HID)
+        self.multi_head_decoderlayer = nn.TransformerDecoderLayer(d_model=HID, nhead=12)
+        self.multi_head_decoder = nn.TransformerDecoder(self.multi_head_decoderlayer, num_layers=DEC_L)
+        self.dropout = nn.Dropout(0.1)
+        self.fc_layers = nn.Sequential(nn.Linear(FUSED, FUSED), nn.ReLU(), nn.Linear(FUSED, HID), nn.Tanh())
+        self.classifier = nn.Linear(HID, 2)
+        if with_dp:
+            self.DP = nn.Parameter(torch.zeros(1, FUSED) if dp_init is None else dp_init.reshape(1, FUSED).float())
+        self.noiser = torch.distributions.laplace.Laplace(torch.tensor([0.0]), torch.tensor([1.0]))
+        self.eps = torch.tensor(eps)
+        self._cfg = EngineConfig(contract=contract, variant=variant, dtype=dtype, eps=float(eps), eps_mode=eps_mode,
+                                 hidden_dropout=dropout, attn_dropout=dropout, dec_dropout=dropout,
+                                 eeg_channels=eeg_channels, act_dim=act_dim, seed=seed)
+        self._build_arena(torch.device("cpu"))
+
+    # ------------------------------------------------------------------ arena binding
+    def _build_arena(self, device):
+        named = _qkv_first_order(self.named_parameters())
+        arena = ParamArena([(n, tuple(p.shape)) for n, p in named], device)
+        with torch.no_grad():
+            for n, p in named:
+                arena.view(n).copy_(p.detach().to(device))
+                p.data = arena.view(n)
+        self._arena = arena
+        self._engine = FusionEngine(arena, self._cfg)
+
+    def _apply(self, fn, recurse=True):
+        # .cuda()/.to()/.half() would re-allocate each parameter separately; instead move the
+        # arena once and re-bind every parameter view (dtype conversions are not supported).
+        probe = fn(torch.zeros(1))
+        if probe.dtype != torch.float32:
+            raise RuntimeError("eegfusion models keep fp32 master weights; use compute_dtype= for bf16")
+        if probe.device != self._arena.device:
+            self._arena.to(probe.device)
+            for n, p in self.named_parameters():
+                p.data = self._arena.view(n)
+                p.grad = None
+            self._engine = FusionEngine(self._arena, self._engine.cfg)
+        return self
+
+    def set_compute_dtype(self, dtype: torch.dtype):
+        self._cfg.dtype = dtype
+        self._engine = FusionEngine(self._arena, self._cfg)
+        return self
+
+    @property
+    def engine(self) -> FusionEngine:
+        return self._engine
+
+    @property
+    def arena(self) -> ParamArena:
+        return self._arena
+
+    # ------------------------------------------------------------------ forward / backward
+    def _check_device(self, *ts):
+        if not self._arena.device.type == "cuda":
+            raise RuntimeError("eegfusion runs on the GPU only (libeegfusion.so); call model.cuda() first")
+        for t in ts:
+            if t is not None and not t.is_cuda:
+                raise RuntimeError("eegfusion: inputs must be device tensors (no CPU path)")
+
+    def _run(self, batch: dict, hard: bool) -> torch.Tensor:
+        self._check_device(*batch.values())
+        self._engine.cfg.eps = float(self.eps)
+        params = [p for p in self.parameters() if p.requires_grad]
+        if torch.is_grad_enabled() and params:
+            keys = tuple(batch)
+            return _PathFunction.apply(self, keys, bool(hard), *batch.values(), *params)
+        logits, _ = self._engine.forward(batch, bool(hard), self.training, save=False)
+        return logits.float()
+
+    def _backward(self, saved, dlogits):
+        eng = self._engine
+        names = dict(self.named_parameters())
+        in_graph = eng.graph_params()
+        need = {n for n, p in names.items() if p.requires_grad and n in in_graph}
+        eng.needs_grad = need
+        a = self._arena
+        # grad routing: overwrite (zero first) params whose .grad is None, accumulate into our views
+        for n in need:
+            p = names[n]
+            gv = a.gview(n)
+            if p.grad is None:
+                gv.zero_()
+            elif p.grad.data_ptr() != gv.data_ptr():
+                gv.copy_(p.grad)
+        eng.backward(saved, dlogits)
+        for n in need:
+            p = names[n]
+            if p.grad is None or p.grad.data_ptr() != a.gview(n).data_ptr():
+                p.grad = a.gview(n)
+        eng.needs_grad = None
+
+    def forward_window(self, eeg: torch.Tensor, act: torch.Tensor, hard: bool = True) -> torch.Tensor:
+        """Contract W: eeg [B, C, T] (channel x time) fp32, act [B, A] fp32 -> logits [B, 2]."""
+        return self._run({"eeg": eeg.contiguous().float(), "act": act.contiguous().float()}, hard)
+
+    def _token_batch(self, frame_input, vedio_mask, title_input, text_mask):
+        if self._contract == "W":
+            # contract-W models accept the window through the reference's argument slots:
+            # title_input <- eeg [B,C,T], frame_input <- act [B,1,A]
+            return {"eeg": title_input.contiguous().float(), "act": frame_input.reshape(frame_input.shape[0], -1)
+                    .contiguous().float()}
+        return {"title_input": title_input.contiguous().long(), "text_mask": text_mask.contiguous().long(),
+                "frame_input": frame_input.contiguous().float()}
+
+    def extra_repr(self):
+        return f"variant={self._variant}, contract={self._contract}, compute={self._cfg.dtype}"
+
+
+# ============================================================ reference-signature classes
+class ConcatModel(FusionModel):
+    """model.py:14-64 — ConcatModel(); forward(x, hard=True) with x = (frame_input [B,1,512],
+    vedio_mask [B,1], title_input [B,512], text_mask [B,512]); min-max fused feature, no gate."""
+
+    def __init__(self, contract: str = "T", **kw):
+        super().__init__("concat", contract=contract, **kw)
+
+    def feature(self, x):
+        frame_input, vedio_mask, title_input, text_mask = x
+        batch = self._token_batch(frame_input, vedio_mask, title_input, text_mask)
+        self._check_device(*batch.values())
+        with torch.no_grad():
+            _, sv = self._engine.forward(batch, True, self.training, save=False)
+        return sv.t["fuse"]["g"].float()
+
+    def forward(self, x, hard=True):
+        frame_input, vedio_mask, title_input, text_mask = x
+        return self._run(self._token_batch(frame_input, vedio_mask, title_input, text_mask), hard)
+
+
+class PriConcatModel(FusionModel):
+    """main_0430.py:88-123 — ConcatModel(args, dp_mode=None); forward(frame_input, vedio_mask,
+    title_input, text_mask).  DP_guarantee is called with dp_mode=None there (:118), i.e. identity;
+    honor_dp_mode=True applies 'feature_all_lap' (min-max + Laplace(0, 1/EPSILON) per row)."""
+
+    def __init__(self, args=None, dp_mode=None, contract: str = "T", honor_dp_mode: bool = False, **kw):
+        eps = float(getattr(args, "EPSILON", 1.0)) if args is not None else 1.0
+        variant = "priconcat_lap" if (honor_dp_mode and dp_mode == "feature_all_lap") else "priconcat"
+        super().__init__(variant, contract=contract, eps=eps, with_dp=False, **kw)
+        self.dp_mode = dp_mode
+        self.EPSILON = eps
+
+    def forward(self, frame_input, vedio_mask, title_input, text_mask):
+        return self._run(self._token_batch(frame_input, vedio_mask, title_input, text_mask), True)
+
+
+class PriGumbelModel(FusionModel):
+    """past_acc.py:79-139 — ConcatModel(epsilon); forward(frame_input, vedio_mask, title_input,
+    text_mask, hard): Laplace noise scaled by eps_hat = 1/ln((e^eps - w)/(1 - w)), w = sigmoid(DP),
+    then the Gumbel-softmax gate."""
+
+    def __init__(self, epsilon: float = 1.0, contract: str = "T", eps_mode: str = "newfrac", **kw):
+        super().__init__("prigumbel", contract=contract, eps=float(epsilon), eps_mode=eps_mode, **kw)
+
+    def forward(self, frame_input, vedio_mask, title_input, text_mask, hard):
+        return self._run(self._token_batch(frame_input, vedio_mask, title_input, text_mask), hard)
+
+
+class TICA_LapDropout(FusionModel):
+    """python/src/custom_models/models.py:28-82 — TICA_LapDropout(bert_coef); forward(eeg_txt_input,
+    eeg_txt_mask, act_img_input, act_img_mask, epsilon, hard).  `bert_coef` names pretrained BERT
+    weights: a local directory/safetensors path is loaded if it exists (no network)."""
+
+    def __init__(self, bert_coef: str = "bert-base-uncased", contract: str = "T", **kw):
+        super().__init__("prigumbel", contract=contract, **kw)
+        if bert_coef and os.path.exists(str(bert_coef)):
+            load_bert_weights(self, bert_coef)
+
+    def forward(self, eeg_txt_input, eeg_txt_mask, act_img_input, act_img_mask, epsilon, hard):
+        self.eps = torch.tensor(float(epsilon))
+        return self._run(self._token_batch(act_img_input, act_img_mask, eeg_txt_input, eeg_txt_mask), hard)
+
+
+def load_bert_weights(model: FusionModel, path: str):
+    """Load `bert.*` weights from a local safetensors file or HF directory (no network)."""
+    from safetensors.torch import load_file
+    f = path if path.endswith(".safetensors") else os.path.join(path, "model.safetensors")
+    sd = load_file(f)
+    sd = {("bert." + k if not k.startswith("bert.") else k): v for k, v in sd.items()}
+    missing = model.load_state_dict({k: v for k, v in sd.items() if k in model.state_dict()}, strict=False)
+    return missing

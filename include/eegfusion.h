@@ -51,8 +51,101 @@ int eegf_gemm(int dtype, int out_dtype, int a_kcontig, int b_kcontig, int epi,
               const void* A, long lda, long strideA,
               const void* B, long ldb, long strideB,
               void* C, long ldc, long strideC,
-              const float* bias, void* aux, long ldaux, long strideAux,
+              const float* bias, long strideBias, void* aux, long ldaux, long strideAux,
               float alpha, float beta, float epi_scale, hipStream_t stream);
+
+/* fusion variants (eegf_fusion_fwd/bwd) */
+#define FUSE_CONCAT 0        /* model.py ConcatModel.feature: minmax(cat)            model.py:46-50      */
+#define FUSE_PRICONCAT 1     /* main_0430 ConcatModel: DP_guarantee(dp_mode=None)=id main_0430.py:118    */
+#define FUSE_PRICONCAT_LAP 2 /* DP_guarantee('feature_all_lap'): minmax + row Laplace main_0430.py:76-85 */
+#define FUSE_PRIGUMBEL 3     /* past_acc / TICA_LapDropout gate                      past_acc.py:120-136 */
+
+/* Residual + dropout + LayerNorm, one row of `width` (multiple of 256, <= 1024) per wave:
+ *   v = drop(x) [drop_mode 1] + r + table[row % table_period] + table2;  y = LN(v) [drop on y: mode 2]
+ * Replaces BertEmbeddings LN+dropout (modeling_bert.py:95-105), BertSelfOutput/BertOutput
+ * (:282-293, :340-351) and the decoder's norm1/2/3 (transformer.py:1158-1200).  Stores the
+ * pre-LN sum `s_out` and per-row mean/rstd for the backward. */
+int eegf_ln_fwd(int dtype, long rows, int width, const void* x, const void* r, const float* table,
+                int table_period, const float* table2, const float* gamma, const float* beta, float eps,
+                float drop_p, int drop_mode, unsigned long long seed, unsigned long long offset,
+                void* y, void* s_out, float* mean, float* rstd, hipStream_t stream);
+/* rows handled per workgroup by eegf_ln_bwd: partial dgamma/dbeta buffers are ceil(rows/this) x width */
+long eegf_ln_bwd_partial_rows(long rows);
+/* LayerNorm backward: dx = grad wrt x (dropout mask applied for mode 1), dr = grad wrt the
+ * residual / table inputs (nullable); per-block partial dgamma/dbeta (reduce with eegf_colsum). */
+int eegf_ln_bwd(int dtype, long rows, int width, const void* dy, const void* s, const float* mean,
+                const float* rstd, const float* gamma, float drop_p, int drop_mode,
+                unsigned long long seed, unsigned long long offset, void* dx, void* dr,
+                float* dgamma_part, float* dbeta_part, hipStream_t stream);
+/* out[p, c] = sum_{r = p mod period} in[r*ld + c] (+ beta*out); fp32 accumulation, two passes,
+ * deterministic.  Bias gradients (period 1), position-embedding gradients (period L), LayerNorm
+ * partial reduction.  ws: scratch of ws_elems floats. */
+int eegf_colsum(int dtype, const void* in, long ld, long rows, int width, int period, float* ws,
+                long ws_elems, float* out, float beta, hipStream_t stream);
+
+/* Multi-head self-attention (12 x 64) over the fused QKV projection [B, L, ld_qkv>=2304]
+ * (BertSelfAttention, modeling_bert.py:139-199).  key_bias [B, L]: 0 or -1e30 (nullable).
+ * out [B, L, ld_out>=768]; lse [B, 12, L] saved for the backward.  L % 128 == 0. */
+int eegf_attn_fwd(int dtype, int B, int H, int L, const void* qkv, long ld_qkv, const float* key_bias,
+                  float scale, void* out, long ld_out, float* lse, hipStream_t stream);
+/* fp32 workspace (elements) eegf_attn_bwd needs for dQ accumulation (0 when L <= 256). */
+long eegf_attn_bwd_workspace(int B, int L);
+/* Attention backward: writes dQ|dK|dV into dqkv [B, L, ld_qkv] (same layout as qkv). L % 256 == 0. */
+int eegf_attn_bwd(int dtype, int B, int H, int L, const void* qkv, long ld_qkv, const float* key_bias,
+                  float scale, const void* out, const void* dout, long ld_out, const float* lse,
+                  void* dqkv, float* dq_workspace, hipStream_t stream);
+
+/* Decoder cross-attention over the BERT memory with a single query token
+ * (TransformerDecoderLayer._mha_block, transformer.py:1177-1196; model.py:40-43), in the
+ * reduced form: qp [B,12,768] = Wk_h^T q_h / 8 (by eegf_gemm); probs [B,12,S] saved;
+ * ctx [B,12,768] = sum_j p_j M_j.  key_bias [B,S] nullable. */
+int eegf_xattn_fwd(int dtype, int B, int S, const void* mem, const void* qp, const float* key_bias,
+                   float* probs, void* ctx, hipStream_t stream);
+/* Backward: dmem [B,S,768] (= result + beta*dmem), dqp [B,12,768]. */
+int eegf_xattn_bwd(int dtype, int B, int S, const void* mem, const void* qp, const float* probs,
+                   const void* dctx, void* dmem, float beta, void* dqp, hipStream_t stream);
+
+/* Fused concat [pooled|img|cross] -> min-max -> privacy stage (variant FUSE_*), one row per
+ * workgroup (model.py:46-61, past_acc.py:120-136, main_0430.py:76-85).  noise/gumbels (fp32
+ * [B,2304] / [2,B,2304]) and row_noise [B] are injected draws (parity) or NULL: Philox(seed,
+ * offset).  eps_mode 0 = newfrac 1/ln(.), 1 = new ln(.); eps_a = exp(eps); lap_scale = 1/eps.
+ * Saves xn (normalised feature), argmin/argmax/range per row for the backward. */
+int eegf_fusion_fwd(int dtype, int B, int variant, const void* pooled, long ld_pooled, const void* img,
+                    long ld_img, const void* cross, long ld_cross, const float* DP, const float* noise,
+                    const float* gumbels, const float* row_noise, int hard, int eps_mode, float eps_a,
+                    float lap_scale, unsigned long long seed, unsigned long long offset, void* out,
+                    float* xn, int* amin, int* amax, float* range, hipStream_t stream);
+/* Backward to the three encoder outputs; ddp_rows [B,2304] (nullable) receives per-row dL/dDP
+ * (reduce with eegf_colsum). */
+int eegf_fusion_bwd(int dtype, int B, int variant, const void* dout, const float* xn, const int* amin,
+                    const int* amax, const float* range, const float* DP, const float* noise,
+                    const float* gumbels, int hard, int eps_mode, float eps_a, unsigned long long seed,
+                    unsigned long long offset, void* d_pooled, long ld_pooled, void* d_img, long ld_img,
+                    void* d_cross, long ld_cross, float* ddp_rows, hipStream_t stream);
+/* F.cross_entropy (reduction 0 = mean: past_acc.py:73; 1 = sum: train.py:69,111) + argmax
+ * correct count; dlogits = dL/dlogits * dscale (nullable). */
+int eegf_cross_entropy(int dtype, int B, int C, const void* logits, const long long* labels,
+                       int reduction, float dscale, float* loss, int* correct, void* dlogits,
+                       hipStream_t stream);
+
+/* y = alpha*x + beta*y ; dx = dy*(1-y^2) */
+int eegf_axpby(int dtype, long n, float alpha, const void* x, float beta, void* y, hipStream_t stream);
+int eegf_tanh_bwd(int dtype, long n, const void* dy, const void* y, void* dx, hipStream_t stream);
+
+/* torch.optim.Adam step over a contiguous fp32 range (+ optional bf16 shadow refresh). */
+int eegf_adam(long n, float* p, const float* g, float* m, float* v, void* bf16_shadow, float lr,
+              float beta1, float beta2, float eps, float weight_decay, int step, hipStream_t stream);
+int eegf_cast_f32_bf16(long n, const float* src, void* dst, hipStream_t stream);
+/* attention_mask (int64, 1 = keep) -> additive key bias (0 / -1e30) */
+int eegf_key_bias(long n, const long long* mask, float* bias, hipStream_t stream);
+
+/* EEG window [B,C,T] fp32 (channel x time) -> time-major tokens [B*T, C] (contract W). */
+int eegf_window_tokens(int dtype, int B, int C, int T, const float* eeg, void* tokens, hipStream_t stream);
+/* word-embedding gather / scatter-add (contract T; modeling_bert.py:101-102) */
+int eegf_embed_gather(int dtype, long rows, int width, const long long* ids, const float* table, void* out,
+                      hipStream_t stream);
+int eegf_embed_scatter_add(int dtype, long rows, int width, const long long* ids, const void* d,
+                           float* table_grad, hipStream_t stream);
 
 #ifdef __cplusplus
 }

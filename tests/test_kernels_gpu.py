@@ -1,0 +1,303 @@
+"""GPU numerics of the non-GEMM kernels against float64 torch references of the same op.
+
+Tolerances: fp32 ≤ 1e-4 relative to the reference's max magnitude (fp32 storage / fp32 math);
+bf16 ≤ 3e-2 relative (bf16 storage, fp32 math).
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DT = [torch.float32, torch.bfloat16]
+
+
+def _tol(dt):
+    return 1e-4 if dt == torch.float32 else 3e-2
+
+
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+
+
+def _lib():
+    from eegfusion import _lib
+    return _lib
+
+
+def _s():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _code(dt):
+    return 0 if dt == torch.float32 else 1
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_layernorm_fwd_bwd(dt, mode):
+    L = _lib()
+    torch.manual_seed(0)
+    R, W = 300, 768
+    x = torch.randn(R, W, device="cuda").to(dt)
+    r = torch.randn(R, W, device="cuda").to(dt)
+    g = (1 + 0.1 * torch.randn(W, device="cuda"))
+    b = 0.1 * torch.randn(W, device="cuda")
+    y = torch.empty_like(x)
+    s = torch.empty_like(x)
+    mean = torch.empty(R, device="cuda")
+    rstd = torch.empty(R, device="cuda")
+    p = 0.0 if mode == 0 else 0.25
+    L.call("eegf_ln_fwd", _code(dt), R, W, x.data_ptr(), r.data_ptr(), None, 1, None, g.data_ptr(), b.data_ptr(),
+           1e-12, p, mode, 123, 7, y.data_ptr(), s.data_ptr(), mean.data_ptr(), rstd.data_ptr(), _s())
+    torch.cuda.synchronize()
+    # recover the dropout masks from the kernel output (scale 1/(1-p) or 0)
+    xd, rd = x.double(), r.double()
+    if mode == 1:
+        m = ((s.double() - rd) != 0).double() / (1 - p)      # dropped lanes store s == r exactly
+        assert abs(1 - (1 - p) * m.mean().item() - p) < 0.02
+        v = xd * m + rd
+        assert _rel(s, v) < _tol(dt)
+    else:
+        v = xd + rd
+    ref = F.layer_norm(v, (W,), g.double(), b.double(), 1e-12)
+    if mode == 2:
+        kept = y.double().abs() > 0
+        assert abs(1 - kept.double().mean().item() - p) < 0.02
+        ref = torch.where(kept, ref / (1 - p), torch.zeros_like(ref))
+    assert _rel(y, ref) < _tol(dt)
+    # backward vs autograd (mode 0 only: masks already checked)
+    if mode == 0:
+        vv = v.clone().requires_grad_()
+        gg = g.double().clone().requires_grad_()
+        bb = b.double().clone().requires_grad_()
+        out = F.layer_norm(vv, (W,), gg, bb, 1e-12)
+        dy = torch.randn(R, W, device="cuda").to(dt)
+        out.backward(dy.double())
+        dx = torch.empty_like(x)
+        nb = (R + 63) // 64
+        part = torch.empty(2, nb, W, device="cuda")
+        L.call("eegf_ln_bwd", _code(dt), R, W, dy.data_ptr(), s.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+               g.data_ptr(), 0.0, 0, 0, 0, dx.data_ptr(), None, part[0].data_ptr(), part[1].data_ptr(), _s())
+        torch.cuda.synchronize()
+        assert _rel(dx, vv.grad) < _tol(dt) * 3
+        assert _rel(part[0].sum(0), gg.grad) < _tol(dt)
+        assert _rel(part[1].sum(0), bb.grad) < _tol(dt)
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("period", [1, 7, 256])
+def test_colsum(dt, period):
+    L = _lib()
+    rows, W = 1536, 300
+    x = torch.randn(rows, W, device="cuda").to(dt)
+    out = torch.randn(period, W, device="cuda")
+    ws = torch.empty(1 << 22, device="cuda")
+    ref = out.double() * 0.5 + x.double().view(rows // period if rows % period == 0 else -1, period, W).sum(0) \
+        if rows % period == 0 else None
+    if ref is None:
+        ref = out.double() * 0.5
+        for p in range(period):
+            ref[p] += x.double()[p::period].sum(0)
+    L.call("eegf_colsum", _code(dt), x.data_ptr(), W, rows, W, period, ws.data_ptr(), ws.numel(), out.data_ptr(),
+           0.5, _s())
+    torch.cuda.synchronize()
+    assert _rel(out, ref) < 1e-5
+
+
+def _attn_ref(qkv, B, L, kbias):
+    q, k, v = qkv.double().view(B, L, 3, 12, 64).unbind(2)
+    q, k, v = (t.transpose(1, 2) for t in (q, k, v))
+    s = q @ k.transpose(-1, -2) / 8.0
+    if kbias is not None:
+        s = s + kbias.double()[:, None, None, :]
+    p = s.softmax(-1)
+    return (p @ v).transpose(1, 2).reshape(B, L, 768)
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("L", [256, 512])
+@pytest.mark.parametrize("masked", [False, True])
+def test_attention_fwd_bwd(dt, L, masked):
+    lib = _lib()
+    torch.manual_seed(1)
+    B = 2
+    qkv = torch.randn(B, L, 2304, device="cuda").to(dt)
+    kbias = None
+    if masked:
+        lens = [L // 3, L]
+        mask = torch.zeros(B, L, dtype=torch.long, device="cuda")
+        for i, n in enumerate(lens):
+            mask[i, :n] = 1
+        kbias = torch.empty(B, L, device="cuda")
+        lib.call("eegf_key_bias", B * L, mask.data_ptr(), kbias.data_ptr(), _s())
+    out = torch.empty(B, L, 768, device="cuda", dtype=dt)
+    lse = torch.empty(B, 12, L, device="cuda")
+    lib.call("eegf_attn_fwd", _code(dt), B, 12, L, qkv.data_ptr(), 2304, None if kbias is None else kbias.data_ptr(),
+             0.125, out.data_ptr(), 768, lse.data_ptr(), _s())
+    torch.cuda.synchronize()
+    qr = qkv.double().clone().requires_grad_()
+    ref = _attn_ref(qr, B, L, kbias)
+    assert _rel(out, ref) < _tol(dt)
+    dout = torch.randn(B, L, 768, device="cuda").to(dt)
+    ref.backward(dout.double())
+    dqkv = torch.empty_like(qkv)
+    ws_n = lib.lib().eegf_attn_bwd_workspace(B, L)
+    ws = torch.empty(max(ws_n, 1), device="cuda")
+    lib.call("eegf_attn_bwd", _code(dt), B, 12, L, qkv.data_ptr(), 2304, None if kbias is None else kbias.data_ptr(),
+             0.125, out.data_ptr(), dout.data_ptr(), 768, lse.data_ptr(), dqkv.data_ptr(), ws.data_ptr(), _s())
+    torch.cuda.synchronize()
+    for sl, name in ((slice(0, 768), "dq"), (slice(768, 1536), "dk"), (slice(1536, 2304), "dv")):
+        e = _rel(dqkv[..., sl], qr.grad[..., sl])
+        assert e < _tol(dt) * 3, (name, e)
+
+
+@pytest.mark.parametrize("dt", DT)
+def test_xattn_fwd_bwd(dt):
+    lib = _lib()
+    torch.manual_seed(2)
+    B, S = 3, 256
+    mem = torch.randn(B, S, 768, device="cuda").to(dt)
+    qp = (0.05 * torch.randn(B, 12, 768, device="cuda")).to(dt)
+    probs = torch.empty(B, 12, S, device="cuda")
+    cc = torch.empty(B, 12, 768, device="cuda", dtype=dt)
+    lib.call("eegf_xattn_fwd", _code(dt), B, S, mem.data_ptr(), qp.data_ptr(), None, probs.data_ptr(), cc.data_ptr(),
+             _s())
+    torch.cuda.synchronize()
+    m = mem.double().clone().requires_grad_()
+    q = qp.double().clone().requires_grad_()
+    p = torch.einsum("bhc,bjc->bhj", q, m).softmax(-1)
+    c = torch.einsum("bhj,bjc->bhc", p, m)
+    assert _rel(probs, p) < _tol(dt)
+    assert _rel(cc, c) < _tol(dt)
+    dc = torch.randn(B, 12, 768, device="cuda").to(dt)
+    c.backward(dc.double())
+    dmem = torch.randn_like(mem)
+    dmem0 = dmem.double().clone()
+    dqp = torch.empty_like(qp)
+    lib.call("eegf_xattn_bwd", _code(dt), B, S, mem.data_ptr(), qp.data_ptr(), probs.data_ptr(), dc.data_ptr(),
+             dmem.data_ptr(), 1.0, dqp.data_ptr(), _s())
+    torch.cuda.synchronize()
+    assert _rel(dmem.double() - dmem0, m.grad) < _tol(dt) * 3
+    assert _rel(dqp, q.grad) < _tol(dt) * 3
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("hard", [False, True])
+@pytest.mark.parametrize("eps", [0.1, 1.0, 10.0])
+def test_fusion_prigumbel_injected(dt, hard, eps):
+    """Fusion kernel vs the oracle gate on injected draws (fp64 autograd of the same formulas)."""
+    import sys
+    from oracle import fusion_oracle as O
+    lib = _lib()
+    torch.manual_seed(3)
+    B = 5
+    parts = [torch.randn(B, 768, device="cuda").to(dt) for _ in range(3)]
+    DP = 0.5 * torch.randn(1, 2304, device="cuda")
+    noise = O.laplace_from_uniform(torch.rand(B, 2304, device="cuda") * 2 - 1).float()
+    gumb = -torch.log(-torch.log(torch.rand(2, B, 2304, device="cuda").clamp(1e-6, 1 - 1e-6)))
+    out = torch.empty(B, 2304, device="cuda", dtype=dt)
+    xn = torch.empty(B, 2304, device="cuda")
+    amin = torch.empty(B, dtype=torch.int32, device="cuda")
+    amax = torch.empty_like(amin)
+    rg = torch.empty(B, device="cuda")
+    lib.call("eegf_fusion_fwd", _code(dt), B, 3, parts[0].data_ptr(), 768, parts[1].data_ptr(), 768,
+             parts[2].data_ptr(), 768, DP.data_ptr(), noise.data_ptr(), gumb.data_ptr(), None, int(hard), 0,
+             math.exp(eps), 1 / eps, 0, 0, out.data_ptr(), xn.data_ptr(), amin.data_ptr(), amax.data_ptr(),
+             rg.data_ptr(), _s())
+    torch.cuda.synchronize()
+    ps = [p.double().clone().requires_grad_() for p in parts]
+    dp = DP.double().clone().requires_grad_()
+    f = O.minmax(torch.cat(ps, 1))
+    ref = O.prigumbel_gate(f, dp, noise.double(), gumb.double(), eps, "newfrac", hard)
+    assert _rel(out, ref) < _tol(dt)
+    dout = torch.randn(B, 2304, device="cuda").to(dt)
+    ref.backward(dout.double())
+    d = [torch.empty_like(p) for p in parts]
+    ddp = torch.empty(B, 2304, device="cuda")
+    lib.call("eegf_fusion_bwd", _code(dt), B, 3, dout.data_ptr(), xn.data_ptr(), amin.data_ptr(), amax.data_ptr(),
+             rg.data_ptr(), DP.data_ptr(), noise.data_ptr(), gumb.data_ptr(), int(hard), 0, math.exp(eps), 0, 0,
+             d[0].data_ptr(), 768, d[1].data_ptr(), 768, d[2].data_ptr(), 768, ddp.data_ptr(), _s())
+    torch.cuda.synchronize()
+    for a, b in zip(d, ps):
+        assert _rel(a, b.grad) < _tol(dt) * 3
+    assert _rel(ddp.sum(0, keepdim=True), dp.grad) < _tol(dt) * 3
+
+
+@pytest.mark.parametrize("dt", DT)
+def test_fusion_philox_statistics(dt):
+    """Without injected draws the kernel's Laplace noise has the Laplace(0,1) law."""
+    lib = _lib()
+    B = 256
+    z = torch.zeros(B, 768, device="cuda", dtype=dt)
+    z[:, 0] = 1.0                                   # min 0, max 1 -> xn = input
+    DP = torch.zeros(1, 2304, device="cuda")        # w = 0.5
+    out = torch.empty(B, 2304, device="cuda", dtype=dt)
+    xn = torch.empty(B, 2304, device="cuda")
+    ai = torch.empty(B, dtype=torch.int32, device="cuda")
+    rg = torch.empty(B, device="cuda")
+    eps = 1.0
+    lib.call("eegf_fusion_fwd", _code(dt), B, 3, z.data_ptr(), 768, z.data_ptr(), 768, z.data_ptr(), 768,
+             DP.data_ptr(), None, None, None, 0, 0, math.exp(eps), 1.0, 42, 0, out.data_ptr(), xn.data_ptr(),
+             ai.data_ptr(), ai.data_ptr(), rg.data_ptr(), _s())
+    torch.cuda.synchronize()
+    eh = 1.0 / math.log((math.e - 0.5) / 0.5)
+    n = ((out.double() - xn.double()) / eh)[:, 1:]
+    assert abs(n.mean().item()) < 0.02
+    assert abs(n.abs().mean().item() - 1.0) < 0.03      # E|Laplace(0,1)| = 1
+    assert abs(n.var().item() - 2.0) < 0.1              # Var = 2
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("reduction", [0, 1])
+def test_cross_entropy(dt, reduction):
+    lib = _lib()
+    B = 300
+    z = torch.randn(B, 2, device="cuda").to(dt)
+    y = torch.randint(0, 2, (B,), device="cuda")
+    loss = torch.empty(1, device="cuda")
+    corr = torch.empty(1, dtype=torch.int32, device="cuda")
+    dz = torch.empty_like(z)
+    lib.call("eegf_cross_entropy", _code(dt), B, 2, z.data_ptr(), y.data_ptr(), reduction, 1.0, loss.data_ptr(),
+             corr.data_ptr(), dz.data_ptr(), _s())
+    torch.cuda.synchronize()
+    zr = z.double().clone().requires_grad_()
+    ref = F.cross_entropy(zr, y, reduction="mean" if reduction == 0 else "sum")
+    ref.backward()
+    assert abs(loss.item() - ref.item()) < 1e-4 * max(1, abs(ref.item()))
+    assert corr.item() == (z.float().argmax(1) == y).sum().item()
+    assert _rel(dz, zr.grad) < _tol(dt)
+
+
+def test_adam_matches_torch():
+    lib = _lib()
+    torch.manual_seed(4)
+    n = 10000 + 3
+    p = torch.randn(n, device="cuda")
+    p_ref = p.clone().requires_grad_()
+    opt = torch.optim.Adam([p_ref], lr=1e-3, weight_decay=0.01)
+    m = torch.zeros(n, device="cuda")
+    v = torch.zeros(n, device="cuda")
+    shadow = torch.empty(n, dtype=torch.bfloat16, device="cuda")
+    for step in range(1, 4):
+        g = torch.randn(n, device="cuda")
+        p_ref.grad = g.clone()
+        opt.step()
+        lib.call("eegf_adam", n, p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), shadow.data_ptr(), 1e-3, 0.9,
+                 0.999, 1e-8, 0.01, step, _s())
+    torch.cuda.synchronize()
+    assert (p - p_ref.detach()).abs().max().item() < 1e-6
+    assert (shadow.float() - p).abs().max().item() <= 1e-2 * p.abs().max().item()
+
+
+@pytest.mark.parametrize("dt", DT)
+def test_window_tokens(dt):
+    lib = _lib()
+    eeg = torch.randn(3, 64, 256, device="cuda")
+    tok = torch.empty(3 * 256, 64, device="cuda", dtype=dt)
+    lib.call("eegf_window_tokens", _code(dt), 3, 64, 256, eeg.data_ptr(), tok.data_ptr(), _s())
+    torch.cuda.synchronize()
+    assert torch.equal(tok, eeg.transpose(1, 2).reshape(-1, 64).to(dt))
