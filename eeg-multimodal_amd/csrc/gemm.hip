@@ -24,11 +24,52 @@ struct GemmArgs {
   long sA, sB, sC, sAux, sBias;
   int M, N, K;
   float alpha, beta, epi_scale;
+  int ksplit;          // >0: split-K slice length (grid.z = slices, C = fp32 slabs [z][M][N])
 };
 
-DEV float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+// erf(x/sqrt 2) by Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7), sharing exp(-x^2/2) with the
+// GELU derivative: one v_exp + one v_rcp instead of the library erff's branchy polynomial.
+DEV float erf_half(float x, float e) {            // e = exp(-x*x/2)
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __frcp_rn(1.0f + 0.3275911f * z);
+  const float poly = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
+  return copysignf(1.0f - poly * e, x);
+}
+DEV float gelu_f(float x) {
+  const float e = __expf(-0.5f * x * x);
+  return 0.5f * x * (1.0f + erf_half(x, e));
+}
 DEV float gelu_grad(float x) {
-  return 0.5f * (1.0f + erff(x * 0.70710678118654752f)) + x * 0.39894228040143268f * __expf(-0.5f * x * x);
+  const float e = __expf(-0.5f * x * x);
+  return 0.5f * (1.0f + erf_half(x, e)) + x * 0.39894228040143268f * e;
+}
+
+DEV void load4(const float* p, float (&v)[4]) { const f32x4 x = *(const f32x4*)p; v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3]; }
+DEV void load4(const bf16* p, float (&v)[4]) { const bf16x4 x = *(const bf16x4*)p; v[0] = (float)x[0]; v[1] = (float)x[1]; v[2] = (float)x[2]; v[3] = (float)x[3]; }
+DEV void store4(float* p, const float (&v)[4]) { *(f32x4*)p = f32x4{v[0], v[1], v[2], v[3]}; }
+DEV void store4(bf16* p, const float (&v)[4]) {
+  bf16x4 x; x[0] = (bf16)v[0]; x[1] = (bf16)v[1]; x[2] = (bf16)v[2]; x[3] = (bf16)v[3];
+  *(bf16x4*)p = x;
+}
+
+// Coalesced copy of a 128x128 bf16 tile between LDS [128][ldl] and global (rows m0.., cols n0..),
+// 16 B per lane (16 lanes per 256-B row), edge-guarded.  LOAD: global -> LDS, else LDS -> global.
+template <bool LOAD>
+DEV void tile_io(bf16* lds, int ldl, bf16* gp, long ld, int m0, int n0, int M, int N, int tid) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int c = tid + 256 * k;
+    const int r = c >> 4, cc = (c & 15) * 8;
+    const int m = m0 + r, n = n0 + cc;
+    if (m >= M || n >= N) continue;
+    bf16* g = gp + (long)m * ld + n;
+    bf16* l = lds + r * ldl + cc;
+    if (n + 8 <= N && ((uintptr_t)g & 15) == 0) {
+      if (LOAD) st16(l, ld16(g)); else st16(g, ld16(l));
+    } else {
+      for (int e = 0; e < 8 && n + e < N; ++e) { if (LOAD) l[e] = g[e]; else g[e] = l[e]; }
+    }
+  }
 }
 
 template <typename T>
@@ -104,11 +145,15 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmArgs g) {
   const int tm = t / tiles_n, tn = t % tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
   const int z = blockIdx.y;
+  int kbeg = 0, kend = g.K;
+  if (g.ksplit > 0) { kbeg = blockIdx.z * g.ksplit; kend = min(g.K, kbeg + g.ksplit); }
 
   const T* A = (const T*)g.A + (long)z * g.sA;
   const T* B = (const T*)g.B + (long)z * g.sB;
-  TO* Cp = (TO*)g.C + (long)z * g.sC;
 
+  // acc[i][j] holds the TRANSPOSED 16x16 tile (operands swapped in the MFMA): lane l owns
+  // C[m = m0 + wm*64 + 16i + (l&15)][n = n0 + wn*64 + 16j + 4*(l>>4) + r], r = 0..3, i.e. four
+  // consecutive columns of one row -> 8/16-byte epilogue loads and stores.
   f32x4 acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -116,9 +161,9 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmArgs g) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   u32x4 ra[4], rb[4];
-  const int nk = (g.K + C::KT - 1) / C::KT;
-  load_tile<T, AKC>(ra, A, g.lda, m0, 0, g.M, g.K, tid);
-  load_tile<T, BKC>(rb, B, g.ldb, n0, 0, g.N, g.K, tid);
+  const int nk = (kend - kbeg + C::KT - 1) / C::KT;
+  load_tile<T, AKC>(ra, A, g.lda, m0, kbeg, g.M, kend, tid);
+  load_tile<T, BKC>(rb, B, g.ldb, n0, kbeg, g.N, kend, tid);
 
   for (int kt = 0; kt < nk; ++kt) {
     __syncthreads();                     // previous k-step's LDS reads are done
@@ -126,8 +171,8 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmArgs g) {
     store_tile<T, BKC>(Bs, rb, tid);
     __syncthreads();
     if (kt + 1 < nk) {                   // issue next k-step's global loads under the MFMAs
-      load_tile<T, AKC>(ra, A, g.lda, m0, (kt + 1) * C::KT, g.M, g.K, tid);
-      load_tile<T, BKC>(rb, B, g.ldb, n0, (kt + 1) * C::KT, g.N, g.K, tid);
+      load_tile<T, AKC>(ra, A, g.lda, m0, kbeg + (kt + 1) * C::KT, g.M, kend, tid);
+      load_tile<T, BKC>(rb, B, g.ldb, n0, kbeg + (kt + 1) * C::KT, g.N, kend, tid);
     }
 #pragma unroll
     for (int kc = 0; kc < C::KT / 32; ++kc) {
@@ -148,48 +193,191 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmArgs g) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mma16(a[i], b[j], acc[i][j]);
+        for (int j = 0; j < 4; ++j) acc[i][j] = mma16(b[j], a[i], acc[i][j]);
     }
   }
 
   // ---- epilogue ----
-  TO* aux = (TO*)g.aux + (long)z * g.sAux;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int n = n0 + wn * 64 + j * 16 + (lane & 15);
-    if (n >= g.N) continue;
-    float bias = 0.f;
-    if (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_TANH) bias = g.bias[(long)z * g.sBias + n];
+  if (g.ksplit > 0) {                    // split-K: raw fp32 partial slab, reduced by gemm_splitk_reduce
+    float* slab = (float*)g.C + (long)blockIdx.z * g.M * g.N;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
+      const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+      if (m >= g.M) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+        float* cp = slab + (long)m * g.N + n;
+        if (n + 3 < g.N && ((uintptr_t)cp & 15) == 0) *(f32x4*)cp = acc[i][j];
+        else
+          for (int r = 0; r < 4; ++r) if (n + r < g.N) cp[r] = acc[i][j][r];
+      }
+    }
+    return;
+  }
+  TO* Cp = (TO*)g.C + (long)z * g.sC;
+  TO* aux = (TO*)g.aux + (long)z * g.sAux;
+  const float* biasp = g.bias ? g.bias + (long)z * g.sBias : nullptr;
+  constexpr bool HAS_BIAS = EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_TANH;
+  constexpr bool HAS_AUX = EPI == EPI_BIAS_GELU || EPI == EPI_DGELU || EPI == EPI_DRELU || EPI == EPI_DTANH;
+  constexpr bool AUX_IN = EPI == EPI_DGELU || EPI == EPI_DRELU || EPI == EPI_DTANH;
+  if constexpr (sizeof(TO) == 2 && sizeof(T) == 2) {
+    if (g.beta == 0.f) {
+      // LDS-staged epilogue: the 128x128 bf16 tile goes through LDS so every global access is a
+      // full 16-B-per-lane row segment (a wave writes 4 x 256-B rows per instruction).
+      constexpr int LDC = BN + 8;
+      bf16* ct = (bf16*)lds;
+      __syncthreads();
+      if (AUX_IN) {
+        tile_io<true>(ct, LDC, (bf16*)aux, g.ldaux, m0, n0, g.M, g.N, tid);
+        __syncthreads();
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int nl = wn * 64 + j * 16 + 4 * (lane >> 4);
+        const int n = n0 + nl;
+        float bias[4] = {0.f, 0.f, 0.f, 0.f};
+        if (HAS_BIAS)
+          for (int r = 0; r < 4; ++r) bias[r] = (n + r < g.N) ? biasp[n + r] : 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int ml = wm * 64 + i * 16 + (lane & 15);
+          bf16* lp = ct + ml * LDC + nl;
+          float av[4] = {0.f, 0.f, 0.f, 0.f};
+          if (AUX_IN) load4(lp, av);
+          float o[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = g.alpha * acc[i][j][r];
+            if (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) v += bias[r];
+            else if (EPI == EPI_BIAS_RELU) v = fmaxf(v + bias[r], 0.f);
+            else if (EPI == EPI_BIAS_TANH) v = tanhf(v + bias[r]);
+            else if (EPI == EPI_DGELU) v *= gelu_grad(av[r]);
+            else if (EPI == EPI_DRELU) v = av[r] > 0.f ? v * g.epi_scale : 0.f;
+            else if (EPI == EPI_DTANH) v *= (1.f - av[r] * av[r]);
+            acc[i][j][r] = v;                 // BIAS_GELU keeps the pre-activation
+            o[r] = v;
+          }
+          store4(lp, o);
+        }
+      }
+      __syncthreads();
+      if (EPI == EPI_BIAS_GELU) {
+        tile_io<false>(ct, LDC, (bf16*)aux, g.ldaux, m0, n0, g.M, g.N, tid);
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float o[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = gelu_f(acc[i][j][r]);
+            store4(ct + (wm * 64 + i * 16 + (lane & 15)) * LDC + wn * 64 + j * 16 + 4 * (lane >> 4), o);
+          }
+        __syncthreads();
+      }
+      tile_io<false>(ct, LDC, (bf16*)Cp, g.ldc, m0, n0, g.M, g.N, tid);
+      return;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+    if (n >= g.N) continue;
+    const bool nfull = n + 3 < g.N;
+    float bias[4] = {0.f, 0.f, 0.f, 0.f};
+    if (HAS_BIAS) {
+      if (nfull && ((uintptr_t)(biasp + n) & 15) == 0) {
+        const f32x4 bv = *(const f32x4*)(biasp + n);
+        bias[0] = bv[0]; bias[1] = bv[1]; bias[2] = bv[2]; bias[3] = bv[3];
+      } else {
+        for (int r = 0; r < 4; ++r) if (n + r < g.N) bias[r] = biasp[n + r];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+      if (m >= g.M) continue;
+      TO* cp = Cp + (long)m * g.ldc + n;
+      TO* ap = HAS_AUX ? aux + (long)m * g.ldaux + n : nullptr;
+      const bool vec = nfull && ((uintptr_t)cp & (4 * sizeof(TO) - 1)) == 0 &&
+                       (!HAS_AUX || ((uintptr_t)ap & (4 * sizeof(TO) - 1)) == 0);
+      float av[4] = {0.f, 0.f, 0.f, 0.f}, cv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (vec) {
+        if (EPI == EPI_DGELU || EPI == EPI_DRELU || EPI == EPI_DTANH) load4(ap, av);
+        if (g.beta != 0.f) load4(cp, cv);
+      } else {
+        for (int r = 0; r < 4; ++r)
+          if (n + r < g.N) {
+            if (EPI == EPI_DGELU || EPI == EPI_DRELU || EPI == EPI_DTANH) av[r] = to_f32(ap[r]);
+            if (g.beta != 0.f) cv[r] = to_f32(cp[r]);
+          }
+      }
+      float o[4], pre[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * 64 + i * 16 + 4 * (lane >> 4) + r;
-        if (m >= g.M) continue;
         float v = g.alpha * acc[i][j][r];
-        if (EPI == EPI_BIAS) v += bias;
-        else if (EPI == EPI_BIAS_GELU) {
-          v += bias;
-          aux[(long)m * g.ldaux + n] = from_f32<TO>(v);
-          v = gelu_f(v);
-        } else if (EPI == EPI_BIAS_RELU) v = fmaxf(v + bias, 0.f);
-        else if (EPI == EPI_BIAS_TANH) v = tanhf(v + bias);
-        else if (EPI == EPI_DGELU) v *= gelu_grad(to_f32(aux[(long)m * g.ldaux + n]));
-        else if (EPI == EPI_DRELU) v = to_f32(aux[(long)m * g.ldaux + n]) > 0.f ? v * g.epi_scale : 0.f;
-        else if (EPI == EPI_DTANH) { const float y = to_f32(aux[(long)m * g.ldaux + n]); v *= (1.f - y * y); }
-        TO* cp = Cp + (long)m * g.ldc + n;
-        if (g.beta != 0.f) v += g.beta * to_f32(*cp);
-        *cp = from_f32<TO>(v);
+        if (EPI == EPI_BIAS) v += bias[r];
+        else if (EPI == EPI_BIAS_GELU) { v += bias[r]; pre[r] = v; v = gelu_f(v); }
+        else if (EPI == EPI_BIAS_RELU) v = fmaxf(v + bias[r], 0.f);
+        else if (EPI == EPI_BIAS_TANH) v = tanhf(v + bias[r]);
+        else if (EPI == EPI_DGELU) v *= gelu_grad(av[r]);
+        else if (EPI == EPI_DRELU) v = av[r] > 0.f ? v * g.epi_scale : 0.f;
+        else if (EPI == EPI_DTANH) v *= (1.f - av[r] * av[r]);
+        if (g.beta != 0.f) v += g.beta * cv[r];
+        o[r] = v;
+      }
+      if (vec) {
+        store4(cp, o);
+        if (EPI == EPI_BIAS_GELU) store4(ap, pre);
+      } else {
+        for (int r = 0; r < 4; ++r)
+          if (n + r < g.N) {
+            cp[r] = from_f32<TO>(o[r]);
+            if (EPI == EPI_BIAS_GELU) ap[r] = from_f32<TO>(pre[r]);
+          }
       }
     }
   }
 }
 
+__global__ void __launch_bounds__(256) gemm_splitk_reduce(const float* __restrict__ slabs, int splits, int M, int N,
+                                                          void* C, int c_is_bf16, long ldc, float beta) {
+  const long i4 = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
+  const long total = (long)M * N;
+  if (i4 >= total) return;
+  float o[4] = {0.f, 0.f, 0.f, 0.f};
+  const bool vec = (i4 + 4 <= total) && (N % 4 == 0);
+  for (int s = 0; s < splits; ++s) {
+    const float* p = slabs + (long)s * total + i4;
+    if (vec) { const f32x4 v = *(const f32x4*)p; o[0] += v[0]; o[1] += v[1]; o[2] += v[2]; o[3] += v[3]; }
+    else for (int r = 0; r < 4 && i4 + r < total; ++r) o[r] += p[r];
+  }
+  for (int r = 0; r < 4 && i4 + r < total; ++r) {
+    const long e = i4 + r, m = e / N, n = e % N;
+    if (c_is_bf16) {
+      bf16* c = (bf16*)C + m * ldc + n;
+      *c = (bf16)(o[r] + (beta != 0.f ? beta * (float)*c : 0.f));
+    } else {
+      float* c = (float*)C + m * ldc + n;
+      *c = o[r] + (beta != 0.f ? beta * *c : 0.f);
+    }
+  }
+}
+
 template <typename T, bool AKC, bool BKC, typename TO, int EPI>
-int launch(const GemmArgs& a, int batch, hipStream_t s) {
+int launch(const GemmArgs& a, int batch, hipStream_t s, int splits = 1) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  hipLaunchKernelGGL((gemm_kernel<T, AKC, BKC, TO, EPI>), dim3(tiles, batch), dim3(NT), 0, s, a);
+  hipLaunchKernelGGL((gemm_kernel<T, AKC, BKC, TO, EPI>), dim3(tiles, batch, splits), dim3(NT), 0, s, a);
   return (int)hipGetLastError();
+}
+
+template <typename T, typename TO>
+int dispatch_layout_split(int akc, int bkc, const GemmArgs& a, hipStream_t s, int splits) {
+  if (akc && bkc) return launch<T, true, true, TO, EPI_NONE>(a, 1, s, splits);
+  if (akc && !bkc) return launch<T, true, false, TO, EPI_NONE>(a, 1, s, splits);
+  if (!akc && !bkc) return launch<T, false, false, TO, EPI_NONE>(a, 1, s, splits);
+  return launch<T, false, true, TO, EPI_NONE>(a, 1, s, splits);
 }
 
 template <typename T, typename TO, int EPI>
@@ -223,7 +411,8 @@ extern "C" int eegf_gemm(int dtype, int out_dtype, int a_kcontig, int b_kcontig,
                          const void* B, long ldb, long strideB,
                          void* C, long ldc, long strideC,
                          const float* bias, long strideBias, void* aux, long ldaux, long strideAux,
-                         float alpha, float beta, float epi_scale, hipStream_t stream) {
+                         float alpha, float beta, float epi_scale, void* workspace, long ws_bytes,
+                         hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0 || batch <= 0 || !A || !B || !C) return EEGF_ERR_ARG;
   if (batch > 65535) return EEGF_ERR_ARG;
   const bool has_bias = epi == EPI_BIAS || epi == EPI_BIAS_GELU || epi == EPI_BIAS_RELU || epi == EPI_BIAS_TANH;
@@ -234,7 +423,30 @@ extern "C" int eegf_gemm(int dtype, int out_dtype, int a_kcontig, int b_kcontig,
     if (fwd && !(a_kcontig && b_kcontig)) return EEGF_ERR_ARG;
     if (!fwd && !(a_kcontig && !b_kcontig)) return EEGF_ERR_ARG;
   }
-  GemmArgs a{A, B, C, bias, aux, lda, ldb, ldc, ldaux, strideA, strideB, strideC, strideAux, strideBias, M, N, K, alpha, beta, epi_scale};
+  GemmArgs a{A, B, C, bias, aux, lda, ldb, ldc, ldaux, strideA, strideB, strideC, strideAux, strideBias, M, N, K, alpha, beta, epi_scale, 0};
+  // split-K for under-filled grids with a long contraction (weight gradients: K = tokens)
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  if (epi == EPI_NONE && batch == 1 && workspace && tiles < 512 && K >= 4096) {
+    const int kt = dtype == EEGF_F32 ? 32 : 64;
+    int splits = 1;
+    while (splits * tiles < 768 && K / (splits * 2) >= 1024) splits *= 2;
+    while (splits > 1 && (long)splits * M * N * 4 > ws_bytes) splits /= 2;
+    if (splits > 1) {
+      int ks = (K + splits - 1) / splits;
+      ks = (ks + kt - 1) / kt * kt;
+      splits = (K + ks - 1) / ks;
+      GemmArgs b = a;
+      b.C = workspace; b.ksplit = ks; b.alpha = alpha;
+      int st;
+      if (dtype == EEGF_F32) st = dispatch_layout_split<float, float>(a_kcontig, b_kcontig, b, stream, splits);
+      else st = dispatch_layout_split<bf16, float>(a_kcontig, b_kcontig, b, stream, splits);
+      if (st) return st;
+      const long n4 = ((long)M * N + 3) / 4;
+      hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, stream,
+                         (const float*)workspace, splits, M, N, C, out_dtype == EEGF_BF16, ldc, beta);
+      return (int)hipGetLastError();
+    }
+  }
   if (dtype == EEGF_F32) {
     if (out_dtype != EEGF_F32) return EEGF_ERR_ARG;
     return dispatch_epi<float, float>(epi, a_kcontig, b_kcontig, a, batch, stream);

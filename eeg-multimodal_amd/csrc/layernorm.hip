@@ -9,6 +9,7 @@
 // eegf_colsum reduces them (and bias / position-embedding gradients) in a second pass.
 #include "common.h"
 #include "eegfusion_internal.h"
+#include <algorithm>
 
 namespace {
 
@@ -185,37 +186,85 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
 }
 
 // ---- strided column sums: out[p, c] = sum_{r = p (mod period)} in[r*ld + c]  (+ beta*out) ----
+// A period-P sum over contiguous rows is a plain column sum over rows/P rows of width P*width.
+// Stage 1: each thread sums 8 adjacent columns (one 16-B bf16 / 2x16-B fp32 load per row) over a
+// chunk of rows → fp32 partial [chunk][width].  Stage 2: 4 waves split the chunks of 64 columns,
+// LDS combine, fixed order → bitwise reproducible.
 template <typename T>
-__global__ void __launch_bounds__(256) colsum_stage1(const T* in, long ld, long rows, int width, int period,
-                                                      int splits, float* ws) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  const int p = blockIdx.y, s = blockIdx.z;
-  if (c >= width) return;
-  float acc = 0.f;
-  for (long r = p + (long)period * s; r < rows; r += (long)period * splits) acc += to_f32(in[r * ld + c]);
-  ws[((long)s * period + p) * width + c] = acc;
+__global__ void __launch_bounds__(256) colsum_chunks(const T* __restrict__ in, long ld, long rows, int width,
+                                                     long rows_per_chunk, float* __restrict__ ws) {
+  const int c0 = (blockIdx.x * 256 + threadIdx.x) * 8;
+  if (c0 >= width) return;
+  const long r0 = (long)blockIdx.y * rows_per_chunk;
+  const long r1 = min(rows, r0 + rows_per_chunk);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c0 + 8 <= width) {
+    for (long r = r0; r < r1; ++r) {
+      const T* p = in + r * ld + c0;
+      if (sizeof(T) == 2) {
+        const bf16x8 v = *(const bf16x8*)p;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += (float)v[e];
+      } else {
+        const f32x4 v0 = *(const f32x4*)p, v1 = *(const f32x4*)(p + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { acc[e] += v0[e]; acc[4 + e] += v1[e]; }
+      }
+    }
+  } else {
+    for (long r = r0; r < r1; ++r)
+      for (int e = 0; e < 8 && c0 + e < width; ++e) acc[e] += to_f32(in[r * ld + c0 + e]);
+  }
+  float* o = ws + (long)blockIdx.y * width + c0;
+  for (int e = 0; e < 8 && c0 + e < width; ++e) o[e] = acc[e];
 }
 
-__global__ void __launch_bounds__(256) colsum_stage2(const float* ws, int splits, long n, float* out, float beta) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
+template <typename T>
+__global__ void __launch_bounds__(256) colsum_scalar(const T* __restrict__ in, long ld, long rows, int width,
+                                                     long rows_per_chunk, float* __restrict__ ws) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= width) return;
+  const long r0 = (long)blockIdx.y * rows_per_chunk, r1 = min(rows, r0 + rows_per_chunk);
   float acc = 0.f;
-  for (int s = 0; s < splits; ++s) acc += ws[(long)s * n + i];
-  out[i] = beta != 0.f ? acc + beta * out[i] : acc;
+  for (long r = r0; r < r1; ++r) acc += to_f32(in[r * ld + c]);
+  ws[(long)blockIdx.y * width + c] = acc;
+}
+
+__global__ void __launch_bounds__(256) colsum_combine(const float* __restrict__ ws, int chunks, int width,
+                                                      float* __restrict__ out, float beta) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  float acc = 0.f;
+  if (c < width)
+    for (int k = wave; k < chunks; k += 4) acc += ws[(long)k * width + c];
+  red[wave][lane] = acc;
+  __syncthreads();
+  if (wave == 0 && c < width) {
+    const float v = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    out[c] = beta != 0.f ? v + beta * out[c] : v;
+  }
 }
 
 template <typename T>
 int colsum_t(const void* in, long ld, long rows, int width, int period, float* ws, long ws_elems, float* out,
              float beta, hipStream_t st) {
-  const long per = (rows + period - 1) / period;              // rows per output element
-  int splits = (int)((per + 63) / 64);
-  while ((long)splits * period * width > ws_elems && splits > 1) splits = (splits + 1) / 2;
-  if ((long)splits * period * width > ws_elems) return EEGF_ERR_ARG;
-  if (splits > 65535) splits = 65535;
-  hipLaunchKernelGGL(colsum_stage1<T>, dim3((width + 255) / 256, period, splits), dim3(256), 0, st,
-                     (const T*)in, ld, rows, width, period, splits, ws);
-  const long n = (long)period * width;
-  hipLaunchKernelGGL(colsum_stage2, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, ws, splits, n, out, beta);
+  if (period > 1) {
+    if (ld != width || rows % period != 0) return EEGF_ERR_ARG;
+    rows /= period;
+    width *= period;
+    ld = width;
+  }
+  const bool vec = (width % 8 == 0) && (ld % 8 == 0) && (((uintptr_t)in & 15) == 0);
+  const int xblocks = vec ? (width + 2047) / 2048 : (width + 255) / 256;
+  long chunks = std::max(1L, std::min(rows / 32, (long)(1024 + xblocks - 1) / xblocks));
+  while (chunks * width > ws_elems && chunks > 1) chunks = (chunks + 1) / 2;
+  if (chunks * width > ws_elems) return EEGF_ERR_ARG;
+  const long rpc = (rows + chunks - 1) / chunks;
+  chunks = (rows + rpc - 1) / rpc;
+  if (vec) hipLaunchKernelGGL(colsum_chunks<T>, dim3(xblocks, (unsigned)chunks), dim3(256), 0, st, (const T*)in, ld, rows, width, rpc, ws);
+  else hipLaunchKernelGGL(colsum_scalar<T>, dim3(xblocks, (unsigned)chunks), dim3(256), 0, st, (const T*)in, ld, rows, width, rpc, ws);
+  hipLaunchKernelGGL(colsum_combine, dim3((width + 63) / 64), dim3(256), 0, st, ws, (int)chunks, width, out, beta);
   return (int)hipGetLastError();
 }
 

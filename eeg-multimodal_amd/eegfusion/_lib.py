@@ -24,7 +24,7 @@ i32, i64, f32, u64, vp = C.c_int, C.c_long, C.c_float, C.c_uint64, C.c_void_p
 SIGNATURES: dict[str, list] = {
     "eegf_gemm": [i32, i32, i32, i32, i32, i32, i32, i32, i32,
                   vp, i64, i64, vp, i64, i64, vp, i64, i64,
-                  vp, i64, vp, i64, i64, f32, f32, f32, vp],
+                  vp, i64, vp, i64, i64, f32, f32, f32, vp, i64, vp],
     "eegf_ln_fwd": [i32, i64, i32, vp, vp, vp, i32, vp, vp, vp, f32, f32, i32, u64, u64, vp, vp, vp, vp, vp],
     "eegf_ln_bwd_partial_rows": [i64],
     "eegf_ln_bwd": [i32, i64, i32, vp, vp, vp, vp, vp, f32, i32, u64, u64, vp, vp, vp, vp, vp],

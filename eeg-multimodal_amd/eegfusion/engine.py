@@ -33,6 +33,7 @@ from .arena import ParamArena
 HID, NH, DH, FFN, NL = 768, 12, 64, 3072, 12
 DEC_FF, DEC_L = 2048, 3
 FUSED = 3 * HID
+SPLITK_WS = 24 << 20          # fp32 elements of split-K slab workspace (96 MB)
 VARIANTS = {"concat": _lib.FUSE_CONCAT, "priconcat": _lib.FUSE_PRICONCAT,
             "priconcat_lap": _lib.FUSE_PRICONCAT_LAP, "prigumbel": _lib.FUSE_PRIGUMBEL}
 
@@ -92,6 +93,7 @@ class FusionEngine:
         self.rng_counter = 0
         self.injected = None        # parity hook: dict(noise=..., gumbels=..., row_noise=...)
         self.needs_grad: set[str] | None = None
+        self.probe: dict | None = None   # tag -> [(start_event, end_event)] (bench.py live timing)
 
     # ------------------------------------------------------------------ parameter access
     def _refresh_shadow(self):
@@ -129,17 +131,34 @@ class FusionEngine:
 
     def gemm(self, A, B, C, M, N, K, a_kc, b_kc, lda, ldb, ldc, epi=_lib.EPI_NONE, bias=None, aux=None, ldaux=0,
              alpha=1.0, beta=0.0, scale=1.0, batch=1, sA=0, sB=0, sC=0, sAux=0, sBias=0):
+        ws = self.ws.get("splitk", SPLITK_WS, torch.float32) if (epi == _lib.EPI_NONE and K >= 4096) else None
         call("eegf_gemm", self.code, F32 if C.dtype == torch.float32 else BF16, a_kc, b_kc, epi, M, N, K, batch,
              P(A), lda, sA, P(B), ldb, sB, P(C), ldc, sC, P(bias), sBias, P(aux), ldaux, sAux,
-             float(alpha), float(beta), float(scale), _stream())
+             float(alpha), float(beta), float(scale), P(ws), (ws.numel() * 4 if ws is not None else 0), _stream())
         return C
 
-    def linear(self, x, w, b, out, M, lda=None, epi=None, aux=None):
+    def linear(self, x, w, b, out, M, lda=None, epi=None, aux=None, tag=None):
         N, K = w.shape
         if epi is None:
             epi = _lib.EPI_BIAS if b is not None else _lib.EPI_NONE
-        return self.gemm(x, w, out, M, N, K, 1, 1, lda or K, K, out.shape[-1], epi=epi, bias=b, aux=aux,
-                         ldaux=(aux.shape[-1] if aux is not None else 0))
+        ev = self._ev_start(tag)
+        self.gemm(x, w, out, M, N, K, 1, 1, lda or K, K, out.shape[-1], epi=epi, bias=b, aux=aux,
+                  ldaux=(aux.shape[-1] if aux is not None else 0))
+        self._ev_end(tag, ev)
+        return out
+
+    def _ev_start(self, tag):
+        if self.probe is None or tag not in self.probe:
+            return None
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return ev
+
+    def _ev_end(self, tag, ev):
+        if ev is not None:
+            e2 = torch.cuda.Event(enable_timing=True)
+            e2.record()
+            self.probe[tag].append((ev, e2))
 
     def dgrad(self, dy, w, out, M, ldd=None, ldo=None, epi=_lib.EPI_NONE, aux=None, scale=1.0, beta=0.0):
         N, K = w.shape
@@ -227,10 +246,12 @@ class FusionEngine:
             pre = f"bert.encoder.layer.{i}."
             qkv = self.empty(R, 3 * HID)
             self.linear(h, self.Wspan(pre + "attention.self.query.weight", 3).view(3 * HID, HID),
-                        self.a.span(pre + "attention.self.query.bias", 3), qkv, R)
+                        self.a.span(pre + "attention.self.query.bias", 3), qkv, R, tag="qkv_fwd")
             ctx = self.empty(R, HID)
             lse = torch.empty(B, NH, L, dtype=torch.float32, device=self.a.device)
+            ev = self._ev_start("attn_fwd")
             call("eegf_attn_fwd", self.code, B, NH, L, P(qkv), 3 * HID, P(kbias), scale, P(ctx), HID, P(lse), _stream())
+            self._ev_end("attn_fwd", ev)
             ao = self.ws.get("ao", R * HID, self.dt).view(R, HID)
             self.linear(ctx, self.W(pre + "attention.output.dense.weight"), self.F(pre + "attention.output.dense.bias"),
                         ao, R)
@@ -240,9 +261,10 @@ class FusionEngine:
                         sv.rng + 10 + 3 * i)
             ffpre, ffact = self.empty(R, FFN), self.empty(R, FFN)
             self.linear(a1, self.W(pre + "intermediate.dense.weight"), self.F(pre + "intermediate.dense.bias"), ffact,
-                        R, epi=_lib.EPI_BIAS_GELU, aux=ffpre)
+                        R, epi=_lib.EPI_BIAS_GELU, aux=ffpre, tag="ffn1_fwd")
             fo = self.ws.get("fo", R * HID, self.dt).view(R, HID)
-            self.linear(ffact, self.W(pre + "output.dense.weight"), self.F(pre + "output.dense.bias"), fo, R)
+            self.linear(ffact, self.W(pre + "output.dense.weight"), self.F(pre + "output.dense.bias"), fo, R,
+                        tag="ffn2_fwd")
             h2 = self.empty(R, HID)
             s2, m2, r2 = self.empty(R, HID), self._f32(R), self._f32(R)
             self.ln_fwd(fo, a1, pre + "output.LayerNorm", R, h2, s2, m2, r2, 1e-12, pdrop, 1, sv.rng + 11 + 3 * i)

@@ -43,13 +43,15 @@ def _req(cond: bool, msg: str) -> None:
 
 # ----------------------------------------------------------------------------------- GEMM
 def gemm(A, B, C, *, M, N, K, a_kc, b_kc, lda, ldb, ldc, epi="none", bias=None, aux=None,
-         ldaux=0, alpha=1.0, beta=0.0, epi_scale=1.0, batch=1, sA=0, sB=0, sC=0, sAux=0, sBias=0):
+         ldaux=0, alpha=1.0, beta=0.0, epi_scale=1.0, batch=1, sA=0, sB=0, sC=0, sAux=0, sBias=0,
+         workspace=None):
     """Raw strided/batched GEMM (see include/eegfusion.h: eegf_gemm)."""
     _req(A.dtype == B.dtype, "A and B must share a dtype")
     _req(bias is None or bias.dtype == torch.float32, "bias must be fp32")
     call("eegf_gemm", code(A), code(C), int(a_kc), int(b_kc), EPI[epi], M, N, K, batch,
          ptr(A), lda, sA, ptr(B), ldb, sB, ptr(C), ldc, sC,
-         ptr(bias), sBias, ptr(aux), ldaux, sAux, float(alpha), float(beta), float(epi_scale), stream())
+         ptr(bias), sBias, ptr(aux), ldaux, sAux, float(alpha), float(beta), float(epi_scale),
+         ptr(workspace), (workspace.numel() * workspace.element_size() if workspace is not None else 0), stream())
     return C
 
 

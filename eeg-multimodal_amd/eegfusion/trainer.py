@@ -1,0 +1,141 @@
+"""PriGumbel / PriConcat training iterations on the engine (no autograd on the hot path).
+
+`PriGumbelTrainer.step` restates one batch of past_acc.main2's loop (past_acc.py:194-212) and of
+TrainAndTest.train's 'lapacian_dropout' branch (base_train.py:167-210):
+
+  1. DP_optimizer.zero_grad(); fwd(hard=False); CE(mean); backward; DP_optimizer.step()
+  2. model_optimizer.zero_grad(); fwd(hard=True); CE(mean); backward; model_optimizer.step()
+
+Only the DP gradient of pass 1 is ever used (model_optimizer.zero_grad() discards the rest), so
+pass 1 runs the encoders forward without saving activations and backpropagates only through the
+head and the privacy stage; pass 2's DP gradient is likewise dead (DP_optimizer.zero_grad()
+clears it before its next use) and is not computed.  Parameter values after the step are
+identical to the reference loop.  With world_size > 1 the gradients are averaged over ranks with
+RCCL all-reduce on the flat arena grad buffer (one launch per bucket) before each Adam.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from . import _lib
+from ._lib import call
+from .engine import FusionEngine
+
+
+def _s():
+    return torch.cuda.current_stream().cuda_stream
+
+
+class FlatAdam:
+    """torch.optim.Adam over one contiguous arena range, one fused launch per step (eegf_adam)."""
+
+    def __init__(self, engine: FusionEngine, rng: tuple[int, int], lr=1e-6, betas=(0.9, 0.999), eps=1e-8,
+                 weight_decay=0.0, write_shadow=True):
+        self.e = engine
+        self.lo, self.hi = rng
+        a = engine.a
+        n = self.hi - self.lo
+        self.m = torch.zeros(n, dtype=torch.float32, device=a.device)
+        self.v = torch.zeros(n, dtype=torch.float32, device=a.device)
+        self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
+        self.t = 0
+        self.write_shadow = write_shadow
+
+    def zero_grad(self):
+        self.e.a.grad[self.lo:self.hi].zero_()
+
+    def step(self):
+        a = self.e.a
+        self.t += 1
+        sh = None
+        if self.write_shadow and self.e.dt == torch.bfloat16:
+            self.e._refresh_shadow()
+            sh = a.shadow[self.lo:self.hi].data_ptr()
+        call("eegf_adam", self.hi - self.lo, a.master[self.lo:].data_ptr(), a.grad[self.lo:].data_ptr(),
+             self.m.data_ptr(), self.v.data_ptr(), sh, float(self.lr), float(self.betas[0]), float(self.betas[1]),
+             float(self.eps), float(self.wd), self.t, _s())
+
+
+class GradReducer:
+    """Average a flat gradient range over ranks: RCCL all_reduce(SUM) in buckets, then scale."""
+
+    def __init__(self, bucket_elems: int = 32 << 20):
+        self.bucket = bucket_elems
+        self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+
+    def __call__(self, g: torch.Tensor):
+        if self.world == 1:
+            return
+        for i in range(0, g.numel(), self.bucket):
+            dist.all_reduce(g[i: i + self.bucket], op=dist.ReduceOp.SUM)
+        g.mul_(1.0 / self.world)
+
+
+class PriGumbelTrainer:
+    def __init__(self, engine: FusionEngine, lr: float = 1e-6, reducer: GradReducer | None = None):
+        self.e = engine
+        a = engine.a
+        self.model_opt = FlatAdam(engine, a.model_range, lr=lr)
+        self.dp_opt = FlatAdam(engine, a.dp_range, lr=lr, write_shadow=False)
+        gp = engine.graph_params()
+        self.model_params = {n for n in gp if n != "DP"}
+        self.reduce = reducer or GradReducer()
+        dev = a.device
+        self.loss = torch.zeros(2, dtype=torch.float32, device=dev)
+        self.correct = torch.zeros(2, dtype=torch.int32, device=dev)
+
+    def _ce(self, logits, labels, i):
+        B = logits.shape[0]
+        dl = torch.empty_like(logits)
+        call("eegf_cross_entropy", self.e.code, B, 2, logits.data_ptr(), labels.data_ptr(), 0, 1.0,
+             self.loss[i:].data_ptr(), self.correct[i:].data_ptr(), dl.data_ptr(), _s())
+        return dl
+
+    def step(self, batch: dict, labels: torch.Tensor):
+        e = self.e
+        # ---- pass 1: DP parameters (hard=False)
+        logits, sv = e.forward(batch, hard=False, training=True, save=False)
+        dl = self._ce(logits, labels, 0)
+        self.dp_opt.zero_grad()
+        e.needs_grad = {"DP"}
+        e.backward(sv, dl, head_only=True)
+        self.reduce(e.a.grad[self.dp_opt.lo:self.dp_opt.hi])
+        self.dp_opt.step()
+        # ---- pass 2: model parameters (hard=True)
+        logits, sv = e.forward(batch, hard=True, training=True, save=True)
+        dl = self._ce(logits, labels, 1)
+        self.model_opt.zero_grad()
+        e.needs_grad = self.model_params
+        e.backward(sv, dl)
+        e.needs_grad = None
+        self.reduce(e.a.grad[self.model_opt.lo:self.model_opt.hi])
+        self.model_opt.step()
+        return self.loss, self.correct
+
+
+class SinglePassTrainer:
+    """PriConcat / ConcatModel step: one fwd(hard=True) + bwd + Adam over all graph params
+    (main_0430.train finetune loop :177-187; train.py:94-113)."""
+
+    def __init__(self, engine: FusionEngine, lr: float = 1e-6, reducer: GradReducer | None = None):
+        self.e = engine
+        self.opt = FlatAdam(engine, (0, engine.a.numel), lr=lr)
+        self.params = engine.graph_params()
+        self.reduce = reducer or GradReducer()
+        self.loss = torch.zeros(1, dtype=torch.float32, device=engine.a.device)
+        self.correct = torch.zeros(1, dtype=torch.int32, device=engine.a.device)
+
+    def step(self, batch, labels):
+        e = self.e
+        logits, sv = e.forward(batch, hard=True, training=True, save=True)
+        dl = torch.empty_like(logits)
+        call("eegf_cross_entropy", e.code, logits.shape[0], 2, logits.data_ptr(), labels.data_ptr(), 0, 1.0,
+             self.loss.data_ptr(), self.correct.data_ptr(), dl.data_ptr(), _s())
+        self.opt.zero_grad()
+        e.needs_grad = self.params
+        e.backward(sv, dl)
+        e.needs_grad = None
+        self.reduce(e.a.grad)
+        self.opt.step()
+        return self.loss, self.correct

@@ -45,14 +45,17 @@ extern "C" {
  * (model.py:24-32,62-63), and their input-/weight-gradient GEMMs.
  *   C[z][m,n] = epi(alpha * sum_k A(m,k) B(k,n)) + beta*C[z][m,n]
  *   a_kcontig: A(m,k)=A[m*lda+k] else A[k*lda+m];  b_kcontig: B(k,n)=B[n*ldb+k] else B[k*ldb+n]
- * dtype: EEGF_F32 (out F32) or EEGF_BF16 (out BF16, or F32 for weight gradients). */
+ * dtype: EEGF_F32 (out F32) or EEGF_BF16 (out BF16, or F32 for weight gradients).
+ * workspace (nullable, ws_bytes): fp32 split-K slabs; used when the tile grid under-fills the chip
+ * and K is long (weight gradients over B*L tokens); the slabs are reduced in a fixed order. */
 int eegf_gemm(int dtype, int out_dtype, int a_kcontig, int b_kcontig, int epi,
               int M, int N, int K, int batch,
               const void* A, long lda, long strideA,
               const void* B, long ldb, long strideB,
               void* C, long ldc, long strideC,
               const float* bias, long strideBias, void* aux, long ldaux, long strideAux,
-              float alpha, float beta, float epi_scale, hipStream_t stream);
+              float alpha, float beta, float epi_scale, void* workspace, long ws_bytes,
+              hipStream_t stream);
 
 /* fusion variants (eegf_fusion_fwd/bwd) */
 #define FUSE_CONCAT 0        /* model.py ConcatModel.feature: minmax(cat)            model.py:46-50      */

@@ -129,3 +129,27 @@ def test_gemm_wgrad_beta_and_batch(dt):
            sA=70 * 64, sB=50 * 64, sC=70 * 50)
     torch.cuda.synchronize()
     _check(C, A.double() @ B.double().transpose(1, 2), dt)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,N,K", [(768, 768, 16384), (2304, 768, 8192), (300, 200, 9000)])
+def test_gemm_wgrad_splitk(dt, M, N, K):
+    """Split-K path (under-filled grid, long contraction): fixed-order fp32 slab reduction + beta."""
+    k = _k()
+    torch.manual_seed(6)
+    dy = torch.randn(K, M, device="cuda").to(dt)
+    x = torch.randn(K, N, device="cuda").to(dt)
+    dw = torch.randn(M, N, device="cuda")
+    ref = dw.double() * 0.5 + dy.double().t() @ x.double()
+    ws = torch.empty(64 << 20, device="cuda")
+    k.gemm(dy, x, dw, M=M, N=N, K=K, a_kc=0, b_kc=0, lda=M, ldb=N, ldc=N, beta=0.5, workspace=ws)
+    torch.cuda.synchronize()
+    # long fp32 contraction: error relative to the output scale (sqrt(K) growth of fp32 rounding)
+    err = ((dw.double() - ref).abs().max() / ref.abs().max()).item()
+    assert err <= (1e-5 if dt == torch.float32 else 2e-2), err
+    dw2 = torch.empty(M, N, device="cuda")
+    k.gemm(dy, x, dw2, M=M, N=N, K=K, a_kc=0, b_kc=0, lda=M, ldb=N, ldc=N, workspace=ws)
+    dw3 = torch.empty(M, N, device="cuda")
+    k.gemm(dy, x, dw3, M=M, N=N, K=K, a_kc=0, b_kc=0, lda=M, ldb=N, ldc=N, workspace=ws)
+    torch.cuda.synchronize()
+    assert torch.equal(dw2, dw3)          # deterministic

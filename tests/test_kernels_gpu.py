@@ -89,7 +89,7 @@ def test_layernorm_fwd_bwd(dt, mode):
 
 
 @pytest.mark.parametrize("dt", DT)
-@pytest.mark.parametrize("period", [1, 7, 256])
+@pytest.mark.parametrize("period", [1, 6, 256])
 def test_colsum(dt, period):
     L = _lib()
     rows, W = 1536, 300

@@ -1,0 +1,81 @@
+"""Time eegf_gemm on every GEMM shape of the B=256 PriGumbel step (and torch.matmul on the same
+shapes as a calibration point for what the chip sustains).  Usage: python tools/gemm_bench.py"""
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "eeg-multimodal_amd"))
+import torch  # noqa: E402
+
+from eegfusion import kernels as K  # noqa: E402
+
+R = 256 * 256
+# (name, M, N, K, layout, epi)
+SHAPES = [
+    ("qkv_fwd", R, 2304, 768, "fwd", "bias"),
+    ("ao_fwd", R, 768, 768, "fwd", "bias"),
+    ("ffn1_fwd", R, 3072, 768, "fwd", "bias_gelu"),
+    ("ffn1_fwd_nogelu", R, 3072, 768, "fwd", "bias"),
+    ("ffn2_fwd", R, 768, 3072, "fwd", "bias"),
+    ("ffn2_dgrad_dgelu", R, 3072, 768, "dgrad", "dgelu"),
+    ("ffn2_dgrad_plain", R, 3072, 768, "dgrad", "none"),
+    ("ffn1_dgrad", R, 768, 3072, "dgrad", "none"),
+    ("qkv_dgrad", R, 768, 2304, "dgrad", "none"),
+    ("ao_dgrad", R, 768, 768, "dgrad", "none"),
+    ("qkv_wgrad", 2304, 768, R, "wgrad", "none"),
+    ("ffn1_wgrad", 3072, 768, R, "wgrad", "none"),
+    ("ffn2_wgrad", 768, 3072, R, "wgrad", "none"),
+    ("ao_wgrad", 768, 768, R, "wgrad", "none"),
+]
+
+
+def run(name, M, N, Kd, layout, epi, iters=20):
+    dt = torch.bfloat16
+    dev = "cuda"
+    ws = torch.empty(24 << 20, device=dev)
+    if layout == "fwd":
+        A = torch.randn(M, Kd, device=dev, dtype=dt)
+        B = torch.randn(N, Kd, device=dev, dtype=dt) * 0.05
+        C = torch.empty(M, N, device=dev, dtype=dt)
+        bias = torch.randn(N, device=dev)
+        aux = torch.empty(M, N, device=dev, dtype=dt) if epi == "bias_gelu" else None
+        f = lambda: K.gemm(A, B, C, M=M, N=N, K=Kd, a_kc=1, b_kc=1, lda=Kd, ldb=Kd, ldc=N, epi=epi, bias=bias,
+                           aux=aux, ldaux=N)
+        bb = bias.to(dt)
+        tf = lambda: torch.nn.functional.linear(A, B, bb)
+    elif layout == "dgrad":
+        A = torch.randn(M, Kd, device=dev, dtype=dt)
+        B = torch.randn(Kd, N, device=dev, dtype=dt) * 0.05
+        C = torch.empty(M, N, device=dev, dtype=dt)
+        aux = torch.randn(M, N, device=dev, dtype=dt) if epi != "none" else None
+        f = lambda: K.gemm(A, B, C, M=M, N=N, K=Kd, a_kc=1, b_kc=0, lda=Kd, ldb=N, ldc=N, epi=epi, aux=aux, ldaux=N)
+        tf = lambda: A @ B
+    else:
+        A = torch.randn(Kd, M, device=dev, dtype=dt)
+        B = torch.randn(Kd, N, device=dev, dtype=dt)
+        C = torch.zeros(M, N, device=dev, dtype=torch.float32)
+        f = lambda: K.gemm(A, B, C, M=M, N=N, K=Kd, a_kc=0, b_kc=0, lda=M, ldb=N, ldc=N, beta=1.0, workspace=ws)
+        tf = lambda: A.t() @ B
+    res = []
+    for fn in (f, tf):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(iters):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        ms = s.elapsed_time(e) / iters
+        res.append((ms, 2.0 * M * N * Kd / ms / 1e9))
+    print(f"{name:20s} M={M:6d} N={N:5d} K={Kd:6d}  eegf {res[0][0]*1e3:8.1f} us {res[0][1]:7.1f} TF | "
+          f"torch {res[1][0]*1e3:8.1f} us {res[1][1]:7.1f} TF", flush=True)
+
+
+if __name__ == "__main__":
+    only = sys.argv[1:]
+    for s in SHAPES:
+        if not only or s[0] in only:
+            run(*s)
