@@ -28,10 +28,10 @@ DEV void load_row12(const T* row, int lane, float (&v)[NCOL]) {
 DEV int col_of(int lane, int k) { return (lane + 64 * (k >> 2)) * 4 + (k & 3); }
 
 // ---- forward: scores, softmax (saved), context c[b,h,:] ----
-template <typename T>
-__global__ void __launch_bounds__(256) xattn_fwd_kernel(const T* __restrict__ mem, const T* __restrict__ qp,
+template <typename T, typename TQ>
+__global__ void __launch_bounds__(256) xattn_fwd_kernel(const T* __restrict__ mem, const TQ* __restrict__ qp,
                                                         const float* __restrict__ kbias, int S, float* __restrict__ probs,
-                                                        T* __restrict__ ctx) {
+                                                        TQ* __restrict__ ctx) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* qs = sm;               // [NH][E]
   float* ps = sm + NH * E;      // [NH][S]
@@ -92,16 +92,16 @@ __global__ void __launch_bounds__(256) xattn_fwd_kernel(const T* __restrict__ me
 #pragma unroll
   for (int h = 0; h < NH; ++h)
 #pragma unroll
-    for (int k = 0; k < 3; ++k) ctx[((long)b * NH + h) * E + c0 + 64 * k] = from_f32<T>(acc[h][k]);
+    for (int k = 0; k < 3; ++k) ctx[((long)b * NH + h) * E + c0 + 64 * k] = from_f32<TQ>(acc[h][k]);
 }
 
 // ---- backward ----
 // dp[h][j] = dc[h].M[j];  dsc = p (dp - sum_j p dp);  dq'[h] = sum_j dsc[h][j] M[j];
 // dM[j] (+)= sum_h p[h][j] dc[h] + dsc[h][j] q'[h]
-template <typename T>
-__global__ void __launch_bounds__(256) xattn_bwd_kernel(const T* __restrict__ mem, const T* __restrict__ qp,
-                                                        const float* __restrict__ probs, const T* __restrict__ dc, int S,
-                                                        T* __restrict__ dmem, float beta, T* __restrict__ dqp) {
+template <typename T, typename TQ>
+__global__ void __launch_bounds__(256) xattn_bwd_kernel(const T* __restrict__ mem, const TQ* __restrict__ qp,
+                                                        const float* __restrict__ probs, const TQ* __restrict__ dc, int S,
+                                                        T* __restrict__ dmem, float beta, TQ* __restrict__ dqp) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* qs = sm;                  // [NH][E] q'
   float* dcs = qs + NH * E;        // [NH][E] dc
@@ -162,7 +162,7 @@ __global__ void __launch_bounds__(256) xattn_bwd_kernel(const T* __restrict__ me
 #pragma unroll
     for (int h = 0; h < NH; ++h)
 #pragma unroll
-      for (int k = 0; k < 3; ++k) dqp[((long)b * NH + h) * E + c0 + 64 * k] = from_f32<T>(acc[h][k]);
+      for (int k = 0; k < 3; ++k) dqp[((long)b * NH + h) * E + c0 + 64 * k] = from_f32<TQ>(acc[h][k]);
   }
   // dM[j][col] = sum_h p[h][j] dc[h][col] + dsc[h][j] q'[h][col]; each thread owns 3 columns
   {
@@ -192,38 +192,42 @@ __global__ void __launch_bounds__(256) xattn_bwd_kernel(const T* __restrict__ me
 
 }  // namespace
 
-extern "C" int eegf_xattn_fwd(int dtype, int B, int S, const void* mem, const void* qp, const float* key_bias,
-                              float* probs, void* ctx, hipStream_t stream) {
-  if (B <= 0 || S <= 0 || S > 2048 || !mem || !qp || !probs || !ctx) return EEGF_ERR_ARG;
+template <typename T, typename TQ>
+int xfwd(int B, int S, const void* mem, const void* qp, const float* kb, float* probs, void* ctx, hipStream_t st) {
   const size_t lds = sizeof(float) * (NH * E + NH * S);
-  if (dtype == EEGF_F32) {
-    hipFuncSetAttribute((const void*)xattn_fwd_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(xattn_fwd_kernel<float>, dim3(B), dim3(256), lds, stream, (const float*)mem, (const float*)qp,
-                       key_bias, S, probs, (float*)ctx);
-  } else if (dtype == EEGF_BF16) {
-    hipFuncSetAttribute((const void*)xattn_fwd_kernel<bf16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(xattn_fwd_kernel<bf16>, dim3(B), dim3(256), lds, stream, (const bf16*)mem, (const bf16*)qp,
-                       key_bias, S, probs, (bf16*)ctx);
-  } else {
-    return EEGF_ERR_ARG;
-  }
+  hipFuncSetAttribute((const void*)xattn_fwd_kernel<T, TQ>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL((xattn_fwd_kernel<T, TQ>), dim3(B), dim3(256), lds, st, (const T*)mem, (const TQ*)qp, kb, S, probs,
+                     (TQ*)ctx);
+  return (int)hipGetLastError();
+}
+template <typename T, typename TQ>
+int xbwd(int B, int S, const void* mem, const void* qp, const float* probs, const void* dctx, void* dmem, float beta,
+         void* dqp, hipStream_t st) {
+  const size_t lds = sizeof(float) * (2 * NH * E + 2 * NH * S);
+  hipFuncSetAttribute((const void*)xattn_bwd_kernel<T, TQ>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL((xattn_bwd_kernel<T, TQ>), dim3(B), dim3(256), lds, st, (const T*)mem, (const TQ*)qp, probs,
+                     (const TQ*)dctx, S, (T*)dmem, beta, (TQ*)dqp);
   return (int)hipGetLastError();
 }
 
-extern "C" int eegf_xattn_bwd(int dtype, int B, int S, const void* mem, const void* qp, const float* probs,
-                              const void* dctx, void* dmem, float beta, void* dqp, hipStream_t stream) {
+extern "C" int eegf_xattn_fwd(int mem_dtype, int q_dtype, int B, int S, const void* mem, const void* qp,
+                              const float* key_bias, float* probs, void* ctx, hipStream_t stream) {
+  if (B <= 0 || S <= 0 || S > 2048 || !mem || !qp || !probs || !ctx) return EEGF_ERR_ARG;
+  if (mem_dtype == EEGF_F32 && q_dtype == EEGF_F32) return xfwd<float, float>(B, S, mem, qp, key_bias, probs, ctx, stream);
+  if (mem_dtype == EEGF_BF16 && q_dtype == EEGF_BF16) return xfwd<bf16, bf16>(B, S, mem, qp, key_bias, probs, ctx, stream);
+  if (mem_dtype == EEGF_BF16 && q_dtype == EEGF_F32) return xfwd<bf16, float>(B, S, mem, qp, key_bias, probs, ctx, stream);
+  return EEGF_ERR_ARG;
+}
+
+extern "C" int eegf_xattn_bwd(int mem_dtype, int q_dtype, int B, int S, const void* mem, const void* qp,
+                              const float* probs, const void* dctx, void* dmem, float beta, void* dqp,
+                              hipStream_t stream) {
   if (B <= 0 || S <= 0 || S > 2048 || !mem || !qp || !probs || !dctx || !dmem || !dqp) return EEGF_ERR_ARG;
-  const size_t lds = sizeof(float) * (2 * NH * E + 2 * NH * S);
-  if (dtype == EEGF_F32) {
-    hipFuncSetAttribute((const void*)xattn_bwd_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(xattn_bwd_kernel<float>, dim3(B), dim3(256), lds, stream, (const float*)mem, (const float*)qp,
-                       probs, (const float*)dctx, S, (float*)dmem, beta, (float*)dqp);
-  } else if (dtype == EEGF_BF16) {
-    hipFuncSetAttribute((const void*)xattn_bwd_kernel<bf16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(xattn_bwd_kernel<bf16>, dim3(B), dim3(256), lds, stream, (const bf16*)mem, (const bf16*)qp,
-                       probs, (const bf16*)dctx, S, (bf16*)dmem, beta, (bf16*)dqp);
-  } else {
-    return EEGF_ERR_ARG;
-  }
-  return (int)hipGetLastError();
+  if (mem_dtype == EEGF_F32 && q_dtype == EEGF_F32)
+    return xbwd<float, float>(B, S, mem, qp, probs, dctx, dmem, beta, dqp, stream);
+  if (mem_dtype == EEGF_BF16 && q_dtype == EEGF_BF16)
+    return xbwd<bf16, bf16>(B, S, mem, qp, probs, dctx, dmem, beta, dqp, stream);
+  if (mem_dtype == EEGF_BF16 && q_dtype == EEGF_F32)
+    return xbwd<bf16, float>(B, S, mem, qp, probs, dctx, dmem, beta, dqp, stream);
+  return EEGF_ERR_ARG;
 }

@@ -13,6 +13,7 @@
 // through registers one k-step ahead of the MFMAs (issue early, write LDS after the barrier).
 #include "common.h"
 #include "eegfusion_internal.h"
+#include <cstdlib>
 
 namespace {
 
@@ -25,6 +26,7 @@ struct GemmArgs {
   int M, N, K;
   float alpha, beta, epi_scale;
   int ksplit;          // >0: split-K slice length (grid.z = slices, C = fp32 slabs [z][M][N])
+  int lds_epi;         // LDS-staged coalesced epilogue (bf16 out, beta == 0)
 };
 
 // erf(x/sqrt 2) by Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7), sharing exp(-x^2/2) with the
@@ -222,7 +224,7 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmArgs g) {
   constexpr bool HAS_AUX = EPI == EPI_BIAS_GELU || EPI == EPI_DGELU || EPI == EPI_DRELU || EPI == EPI_DTANH;
   constexpr bool AUX_IN = EPI == EPI_DGELU || EPI == EPI_DRELU || EPI == EPI_DTANH;
   if constexpr (sizeof(TO) == 2 && sizeof(T) == 2) {
-    if (g.beta == 0.f) {
+    if (g.beta == 0.f && g.lds_epi) {
       // LDS-staged epilogue: the 128x128 bf16 tile goes through LDS so every global access is a
       // full 16-B-per-lane row segment (a wave writes 4 x 256-B rows per instruction).
       constexpr int LDC = BN + 8;
@@ -405,6 +407,20 @@ int dispatch_epi(int epi, int akc, int bkc, const GemmArgs& a, int batch, hipStr
 
 }  // namespace
 
+int eegf_gemm_big(int a_kc, int b_kc, int epi, int M, int N, int K, const void* A, long lda, const void* B, long ldb,
+                  void* C, long ldc, const float* bias, void* aux, long ldaux, float alpha, float beta,
+                  float epi_scale, hipStream_t stream);
+
+static int lds_epi_enabled() {
+  static const int on = [] { const char* e = getenv("EEGF_GEMM_LDS_EPI"); return (e && e[0] == '0') ? 0 : 1; }();
+  return on;
+}
+
+static bool big_enabled() {
+  static const int on = [] { const char* e = getenv("EEGF_GEMM_BIG"); return (e && e[0] == '0') ? 0 : 1; }();
+  return on != 0;
+}
+
 extern "C" int eegf_gemm(int dtype, int out_dtype, int a_kcontig, int b_kcontig, int epi,
                          int M, int N, int K, int batch,
                          const void* A, long lda, long strideA,
@@ -423,7 +439,8 @@ extern "C" int eegf_gemm(int dtype, int out_dtype, int a_kcontig, int b_kcontig,
     if (fwd && !(a_kcontig && b_kcontig)) return EEGF_ERR_ARG;
     if (!fwd && !(a_kcontig && !b_kcontig)) return EEGF_ERR_ARG;
   }
-  GemmArgs a{A, B, C, bias, aux, lda, ldb, ldc, ldaux, strideA, strideB, strideC, strideAux, strideBias, M, N, K, alpha, beta, epi_scale, 0};
+  GemmArgs a{A, B, C, bias, aux, lda, ldb, ldc, ldaux, strideA, strideB, strideC, strideAux, strideBias, M, N, K, alpha, beta, epi_scale, 0,
+             lds_epi_enabled()};
   // split-K for under-filled grids with a long contraction (weight gradients: K = tokens)
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   if (epi == EPI_NONE && batch == 1 && workspace && tiles < 512 && K >= 4096) {
@@ -452,11 +469,13 @@ extern "C" int eegf_gemm(int dtype, int out_dtype, int a_kcontig, int b_kcontig,
     return dispatch_epi<float, float>(epi, a_kcontig, b_kcontig, a, batch, stream);
   }
   if (dtype == EEGF_BF16) {
-    if (out_dtype == EEGF_BF16) return dispatch_epi<bf16, bf16>(epi, a_kcontig, b_kcontig, a, batch, stream);
-    if (out_dtype == EEGF_F32) {
-      if (epi != EPI_NONE) return EEGF_ERR_ARG;
-      return dispatch_layout<bf16, float, EPI_NONE>(a_kcontig, b_kcontig, a, batch, stream);
+    if (out_dtype == EEGF_BF16 && batch == 1 && big_enabled()) {
+      const int st = eegf_gemm_big(a_kcontig, b_kcontig, epi, M, N, K, A, lda, B, ldb, C, ldc, bias, aux, ldaux, alpha,
+                                   beta, epi_scale, stream);
+      if (st != 1) return st;
     }
+    if (out_dtype == EEGF_BF16) return dispatch_epi<bf16, bf16>(epi, a_kcontig, b_kcontig, a, batch, stream);
+    if (out_dtype == EEGF_F32) return dispatch_epi<bf16, float>(epi, a_kcontig, b_kcontig, a, batch, stream);
   }
   return EEGF_ERR_ARG;
 }

@@ -1,0 +1,261 @@
+// gemm_big.hip — bf16 MFMA GEMM for the token-sized projections (M = B*L rows).
+//
+// Used by eegf_gemm for the BERT forward (x W^T + bias [+GELU]) and input-gradient (dY W [*act'])
+// GEMMs when M, N, K are large and aligned.  Structure (cdna_hip_programming.md §5, "minimum
+// 2-phase" + T1/T2):
+//   * 256x256 output tile, 512 threads = 8 waves as 2 (M) x 4 (N), wave tile 128x64 = 8x4 MFMA
+//     16x16x32 accumulators (kept transposed: a lane owns 4 consecutive columns of one row);
+//   * BK = 64; operands staged global -> LDS with global_load_lds_dwordx4 (no VGPR round trip)
+//     into two LDS buffers: the next k-step's loads fly while the current one is consumed; one
+//     barrier per k-step;
+//   * XOR-swizzled LDS images written lane-linearly (swizzle applied to the SOURCE address):
+//     row-major [256][64] operands use chunk ^= (row>>1)&7 (conflict-free ds_read_b128); k-major
+//     [64][256] operands use chunk ^= 2*((k&3) | ((k>>3)&1)<<2) (spread ds_read_b64_tr_b16);
+//   * XCD-aware tile order; LDS-staged coalesced epilogue (bias, GELU / act' from aux).
+// Edges: rows/cols beyond M/N are clamped to valid memory and never stored; K % 64 == 0.
+#include "common.h"
+#include "eegfusion_internal.h"
+
+namespace {
+
+constexpr int TM = 256, TN = 256, BK = 64, NT = 512;
+constexpr int TILE = TM * BK;                 // elements per operand tile (32 KB)
+constexpr int LDC = TN + 8;                   // epilogue tile row stride (elements)
+constexpr int LDS_ELEMS = TM * LDC;           // 135168 B >= 4 * TILE * 2 B
+
+struct BigArgs {
+  const bf16* A; const bf16* B; bf16* C; const float* bias; bf16* aux;
+  long lda, ldb, ldc, ldaux;
+  int M, N, K;
+  float alpha, epi_scale;
+};
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) const void glb_void;
+
+DEV void glds16(const bf16* g, bf16* lds_base) {
+  __builtin_amdgcn_global_load_lds((glb_void*)g, (lds_void*)lds_base, 16, 0, 0);
+}
+
+DEV int swz_row(int r) { return (r >> 1) & 7; }
+DEV int swz_k(int k) { return 2 * ((k & 3) | (((k >> 3) & 1) << 2)); }
+
+// Row-major operand tile rows [r0, r0+256) x k [k0, k0+64): 4 glds per wave.
+DEV void stage_rowmajor(bf16* dst, const bf16* src, long ld, int r0, int rmax, int k0, int wave, int lane) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int R0 = (wave * 4 + j) * 8;
+    const int r = R0 + (lane >> 3);
+    const int c = (lane & 7) ^ swz_row(r);
+    const int gr = min(r0 + r, rmax - 1);
+    glds16(src + (long)gr * ld + k0 + c * 8, dst + R0 * BK);
+  }
+}
+
+// k-major operand tile k [k0, k0+64) x cols [c0, c0+256): 4 glds per wave.
+DEV void stage_kmajor(bf16* dst, const bf16* src, long ld, int c0, int cmax, int k0, int wave, int lane) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int K0 = (wave * 4 + j) * 2;
+    const int k = K0 + (lane >> 5);
+    const int c = (lane & 31) ^ swz_k(k);
+    const int col = min(c0 + c * 8, cmax - 8);
+    glds16(src + (long)(k0 + k) * ld + col, dst + K0 * TN);
+  }
+}
+
+DEV bf16x8 rd_row(const bf16* t, int r, int chunk) {
+  return *(const bf16x8*)(t + r * BK + ((chunk ^ swz_row(r)) << 3));
+}
+
+// 8 k-values (k0+0..3, k0+4..7 of the lane's 16-group) of column c0 + (lane&15) from a k-major tile
+DEV bf16x8 rd_col(const bf16* t, int k0, int c0, int lane) {
+  const int i = lane & 15, q = i >> 2, p = i & 3;
+  const int col = c0 + 4 * p;
+  const int ch = col >> 3, off = col & 7;
+  const int ka = k0 + q, kb = k0 + 4 + q;
+  const bf16* a0 = t + ka * TN + (((ch ^ swz_k(ka)) << 3) | off);
+  const bf16* a1 = t + kb * TN + (((ch ^ swz_k(kb)) << 3) | off);
+  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)a0);
+  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)a1);
+  bf16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+DEV float erf_half(float x, float e) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __frcp_rn(1.0f + 0.3275911f * z);
+  const float poly = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
+  return copysignf(1.0f - poly * e, x);
+}
+DEV float gelu_f(float x) { const float e = __expf(-0.5f * x * x); return 0.5f * x * (1.0f + erf_half(x, e)); }
+DEV float gelu_grad(float x) {
+  const float e = __expf(-0.5f * x * x);
+  return 0.5f * (1.0f + erf_half(x, e)) + x * 0.39894228040143268f * e;
+}
+
+template <bool LOAD>
+DEV void tile_io(bf16* lds, bf16* gp, long ld, int m0, int n0, int M, int N, int tid) {
+#pragma unroll 4
+  for (int k = 0; k < (TM * TN / 8) / NT; ++k) {
+    const int c = tid + NT * k;
+    const int r = c >> 5, cc = (c & 31) * 8;
+    const int m = m0 + r, n = n0 + cc;
+    if (m >= M || n >= N) continue;
+    bf16* g = gp + (long)m * ld + n;
+    bf16* l = lds + r * LDC + cc;
+    if (n + 8 <= N) {
+      if (LOAD) st16(l, ld16(g)); else st16(g, ld16(l));
+    } else {
+      for (int e = 0; e < 8 && n + e < N; ++e) { if (LOAD) l[e] = g[e]; else g[e] = l[e]; }
+    }
+  }
+}
+
+DEV void ld4(const bf16* p, float (&v)[4]) { const bf16x4 x = *(const bf16x4*)p; v[0] = (float)x[0]; v[1] = (float)x[1]; v[2] = (float)x[2]; v[3] = (float)x[3]; }
+DEV void st4(bf16* p, const float (&v)[4]) { bf16x4 x; x[0] = (bf16)v[0]; x[1] = (bf16)v[1]; x[2] = (bf16)v[2]; x[3] = (bf16)v[3]; *(bf16x4*)p = x; }
+
+template <bool BKC, int EPI>
+__global__ void __launch_bounds__(NT, 1) gemm_big_kernel(BigArgs g) {
+  __shared__ __attribute__((aligned(16))) bf16 lds[LDS_ELEMS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int tiles_n = (g.N + TN - 1) / TN, tiles_m = (g.M + TM - 1) / TM;
+  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int tm = t / tiles_n, tn = t % tiles_n;
+  const int m0 = tm * TM, n0 = tn * TN;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = g.K / BK;
+  stage_rowmajor(lds, g.A, g.lda, m0, g.M, 0, wave, lane);
+  if (BKC) stage_rowmajor(lds + TILE, g.B, g.ldb, n0, g.N, 0, wave, lane);
+  else stage_kmajor(lds + TILE, g.B, g.ldb, n0, g.N, 0, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = (kt & 1) * 2 * TILE, nxt = 2 * TILE - cur;
+    if (kt + 1 < nk) {
+      stage_rowmajor(lds + nxt, g.A, g.lda, m0, g.M, (kt + 1) * BK, wave, lane);
+      if (BKC) stage_rowmajor(lds + nxt + TILE, g.B, g.ldb, n0, g.N, (kt + 1) * BK, wave, lane);
+      else stage_kmajor(lds + nxt + TILE, g.B, g.ldb, n0, g.N, (kt + 1) * BK, wave, lane);
+    }
+    const bf16* As = lds + cur;
+    const bf16* Bs = lds + cur + TILE;
+#pragma unroll
+    for (int kc = 0; kc < 2; ++kc) {
+      bf16x8 b[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = wn * 64 + j * 16;
+        if (BKC) b[j] = rd_row(Bs, c + (lane & 15), 4 * kc + (lane >> 4));
+        else b[j] = rd_col(Bs, 32 * kc + 8 * (lane >> 4), c, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const bf16x8 a = rd_row(As, wm * 128 + i * 16 + (lane & 15), 4 * kc + (lane >> 4));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mma16(b[j], a, acc[i][j]);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---- LDS-staged epilogue ----
+  constexpr bool HAS_BIAS = EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_TANH;
+  constexpr bool AUX_IN = EPI == EPI_DGELU || EPI == EPI_DRELU || EPI == EPI_DTANH;
+  bf16* ct = lds;
+  if (AUX_IN) {
+    tile_io<true>(ct, g.aux, g.ldaux, m0, n0, g.M, g.N, tid);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int nl = wn * 64 + j * 16 + 4 * (lane >> 4);
+    const int n = n0 + nl;
+    float bias[4] = {0.f, 0.f, 0.f, 0.f};
+    if (HAS_BIAS)
+      for (int r = 0; r < 4; ++r) bias[r] = (n + r < g.N) ? g.bias[n + r] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      bf16* lp = ct + (wm * 128 + i * 16 + (lane & 15)) * LDC + nl;
+      float av[4] = {0.f, 0.f, 0.f, 0.f};
+      if (AUX_IN) ld4(lp, av);
+      float o[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = g.alpha * acc[i][j][r];
+        if (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) v += bias[r];
+        else if (EPI == EPI_BIAS_RELU) v = fmaxf(v + bias[r], 0.f);
+        else if (EPI == EPI_BIAS_TANH) v = tanhf(v + bias[r]);
+        else if (EPI == EPI_DGELU) v *= gelu_grad(av[r]);
+        else if (EPI == EPI_DRELU) v = av[r] > 0.f ? v * g.epi_scale : 0.f;
+        else if (EPI == EPI_DTANH) v *= (1.f - av[r] * av[r]);
+        acc[i][j][r] = v;
+        o[r] = v;
+      }
+      st4(lp, o);
+    }
+  }
+  __syncthreads();
+  if (EPI == EPI_BIAS_GELU) {
+    tile_io<false>(ct, g.aux, g.ldaux, m0, n0, g.M, g.N, tid);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = gelu_f(acc[i][j][r]);
+        st4(ct + (wm * 128 + i * 16 + (lane & 15)) * LDC + wn * 64 + j * 16 + 4 * (lane >> 4), o);
+      }
+    __syncthreads();
+  }
+  tile_io<false>(ct, g.C, g.ldc, m0, n0, g.M, g.N, tid);
+}
+
+template <bool BKC, int EPI>
+int launch_big(const BigArgs& a, hipStream_t s) {
+  const int tiles = ((a.M + TM - 1) / TM) * ((a.N + TN - 1) / TN);
+  hipLaunchKernelGGL((gemm_big_kernel<BKC, EPI>), dim3(tiles), dim3(NT), 0, s, a);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+// Internal entry used by eegf_gemm (gemm.hip).  Returns 1 if the shape is not eligible.
+int eegf_gemm_big(int a_kc, int b_kc, int epi, int M, int N, int K, const void* A, long lda, const void* B, long ldb,
+                  void* C, long ldc, const float* bias, void* aux, long ldaux, float alpha, float beta,
+                  float epi_scale, hipStream_t stream) {
+  if (!a_kc || beta != 0.f) return 1;
+  if (M < 2048 || N < 256 || K % BK != 0 || M % 8 != 0 || N % 8 != 0) return 1;
+  if (lda % 8 || ldb % 8 || ldc % 8 || (aux && ldaux % 8)) return 1;
+  if ((((uintptr_t)A | (uintptr_t)B | (uintptr_t)C | (uintptr_t)aux) & 15) != 0) return 1;
+  BigArgs a{(const bf16*)A, (const bf16*)B, (bf16*)C, bias, (bf16*)aux, lda, ldb, ldc, ldaux, M, N, K, alpha, epi_scale};
+  if (b_kc) {
+    switch (epi) {
+      case EPI_NONE: return launch_big<true, EPI_NONE>(a, stream);
+      case EPI_BIAS: return launch_big<true, EPI_BIAS>(a, stream);
+      case EPI_BIAS_GELU: return launch_big<true, EPI_BIAS_GELU>(a, stream);
+      case EPI_BIAS_RELU: return launch_big<true, EPI_BIAS_RELU>(a, stream);
+      case EPI_BIAS_TANH: return launch_big<true, EPI_BIAS_TANH>(a, stream);
+    }
+  } else {
+    switch (epi) {
+      case EPI_NONE: return launch_big<false, EPI_NONE>(a, stream);
+      case EPI_DGELU: return launch_big<false, EPI_DGELU>(a, stream);
+      case EPI_DRELU: return launch_big<false, EPI_DRELU>(a, stream);
+      case EPI_DTANH: return launch_big<false, EPI_DTANH>(a, stream);
+    }
+  }
+  return 1;
+}

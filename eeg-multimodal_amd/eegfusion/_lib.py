@@ -32,8 +32,8 @@ SIGNATURES: dict[str, list] = {
     "eegf_attn_fwd": [i32, i32, i32, i32, vp, i64, vp, f32, vp, i64, vp, vp],
     "eegf_attn_bwd_workspace": [i32, i32],
     "eegf_attn_bwd": [i32, i32, i32, i32, vp, i64, vp, f32, vp, vp, i64, vp, vp, vp, vp],
-    "eegf_xattn_fwd": [i32, i32, i32, vp, vp, vp, vp, vp, vp],
-    "eegf_xattn_bwd": [i32, i32, i32, vp, vp, vp, vp, vp, f32, vp, vp],
+    "eegf_xattn_fwd": [i32, i32, i32, i32, vp, vp, vp, vp, vp, vp],
+    "eegf_xattn_bwd": [i32, i32, i32, i32, vp, vp, vp, vp, vp, f32, vp, vp],
     "eegf_fusion_fwd": [i32, i32, i32, vp, i64, vp, i64, vp, i64, vp, vp, vp, vp, i32, i32, f32, f32, u64, u64,
                         vp, vp, vp, vp, vp, vp],
     "eegf_fusion_bwd": [i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, f32, u64, u64,

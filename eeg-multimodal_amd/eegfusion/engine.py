@@ -116,8 +116,12 @@ class FusionEngine:
         return self.a.span(first, n, self.a.shadow if self.dt != torch.float32 else None)
 
     def F(self, name):
-        """fp32 master (biases, LN params, tables, DP)"""
+        """fp32 master (biases, LN params, tables, DP; decoder/head weights)"""
         return self.a.view(name)
+
+    def eh(self, *shape):
+        """fp32 buffer for the decoder / fusion / head section (always fp32)"""
+        return torch.empty(*shape, dtype=torch.float32, device=self.a.device)
 
     def G(self, name):
         return self.a.gview(name)
@@ -132,7 +136,7 @@ class FusionEngine:
     def gemm(self, A, B, C, M, N, K, a_kc, b_kc, lda, ldb, ldc, epi=_lib.EPI_NONE, bias=None, aux=None, ldaux=0,
              alpha=1.0, beta=0.0, scale=1.0, batch=1, sA=0, sB=0, sC=0, sAux=0, sBias=0):
         ws = self.ws.get("splitk", SPLITK_WS, torch.float32) if (epi == _lib.EPI_NONE and K >= 4096) else None
-        call("eegf_gemm", self.code, F32 if C.dtype == torch.float32 else BF16, a_kc, b_kc, epi, M, N, K, batch,
+        call("eegf_gemm", _code(A), _code(C), a_kc, b_kc, epi, M, N, K, batch,
              P(A), lda, sA, P(B), ldb, sB, P(C), ldc, sC, P(bias), sBias, P(aux), ldaux, sAux,
              float(alpha), float(beta), float(scale), P(ws), (ws.numel() * 4 if ws is not None else 0), _stream())
         return C
@@ -183,14 +187,14 @@ class FusionEngine:
 
     def ln_fwd(self, x, r, pre, rows, out, s, mean, rstd, eps, p=0.0, mode=0, rng=0, table=None, period=1,
                table2=None):
-        call("eegf_ln_fwd", self.code, rows, HID, P(x), P(r), P(table), period, P(table2), P(self.F(pre + ".weight")),
+        call("eegf_ln_fwd", _code(x), rows, HID, P(x), P(r), P(table), period, P(table2), P(self.F(pre + ".weight")),
              P(self.F(pre + ".bias")), float(eps), float(p), int(mode if p > 0 else 0), self.cfg.seed, rng, P(out),
              P(s), P(mean), P(rstd), _stream())
 
     def ln_bwd(self, dy, s, mean, rstd, pre, rows, dx, dr, p=0.0, mode=0, rng=0):
         nb = (rows + 63) // 64
         part = self.ws.get("ln_part", 2 * nb * HID, torch.float32)
-        call("eegf_ln_bwd", self.code, rows, HID, P(dy), P(s), P(mean), P(rstd), P(self.F(pre + ".weight")), float(p),
+        call("eegf_ln_bwd", _code(dy), rows, HID, P(dy), P(s), P(mean), P(rstd), P(self.F(pre + ".weight")), float(p),
              int(mode if p > 0 else 0), self.cfg.seed, rng, P(dx), P(dr), P(part), P(part[nb * HID:]), _stream())
         self.bgrad(part[: nb * HID], pre + ".weight", nb, HID)
         self.bgrad(part[nb * HID:], pre + ".bias", nb, HID)
@@ -274,59 +278,54 @@ class FusionEngine:
             h = h2
         t["layers"] = layers
         t["mem"] = h
-        pooled = self.empty(B, HID)
+        pooled = self.eh(B, HID)                 # fp32 out of the bf16 pooler GEMM (+ tanh)
         self.linear(h, self.W("bert.pooler.dense.weight"), self.F("bert.pooler.dense.bias"), pooled, B, lda=L * HID,
                     epi=_lib.EPI_BIAS_TANH)
         t["pooled"] = pooled
 
-        # ---------------- action encoder
-        if cfg.contract == "W":
-            act = batch["act"]
-        else:
-            act = batch["frame_input"].reshape(B, -1)
-        act_t = act if self.dt == torch.float32 else self.empty(act.shape)
-        if self.dt != torch.float32:
-            call("eegf_cast_f32_bf16", act.numel(), P(act.contiguous()), P(act_t), _stream())
-        vis = self.empty(B, HID)
-        self.linear(act_t, self.W("visual_encoder.weight"), self.F("visual_encoder.bias"), vis, B)
-        t["act"], t["vis"] = act_t, vis
+        # ---------------- action encoder (fp32)
+        act = batch["act"] if cfg.contract == "W" else batch["frame_input"].reshape(B, -1)
+        act = act.contiguous().float()
+        vis = self.eh(B, HID)
+        self.linear(act, self.F("visual_encoder.weight"), self.F("visual_encoder.bias"), vis, B)
+        t["act"], t["vis"] = act, vis
 
-        # ---------------- decoder (single query token)
+        # ---------------- decoder (single query token; fp32 over the encoder-dtype memory)
         x = vis
         dl = []
         for d in range(DEC_L):
             pre = f"multi_head_decoder.layers.{d}."
-            in_w, in_b = self.W(pre + "self_attn.in_proj_weight"), self.F(pre + "self_attn.in_proj_bias")
-            v = self.empty(B, HID)
+            in_w, in_b = self.F(pre + "self_attn.in_proj_weight"), self.F(pre + "self_attn.in_proj_bias")
+            v = self.eh(B, HID)
             self.linear(x, in_w[2 * HID:], in_b[2 * HID:], v, B)
-            sa = self.ws.get("dsa", B * HID, self.dt).view(B, HID)
-            self.linear(v, self.W(pre + "self_attn.out_proj.weight"), self.F(pre + "self_attn.out_proj.bias"), sa, B)
-            x1, ln1 = self.empty(B, HID), (self.empty(B, HID), self._f32(B), self._f32(B))
+            sa = self.eh(B, HID)
+            self.linear(v, self.F(pre + "self_attn.out_proj.weight"), self.F(pre + "self_attn.out_proj.bias"), sa, B)
+            x1, ln1 = self.eh(B, HID), (self.eh(B, HID), self._f32(B), self._f32(B))
             self.ln_fwd(sa, x, pre + "norm1", B, x1, *ln1, 1e-5, ddrop, 1, sv.rng + 100 + 8 * d)
-            cw, cb = self.W(pre + "multihead_attn.in_proj_weight"), self.F(pre + "multihead_attn.in_proj_bias")
-            q = self.empty(B, HID)
+            cw, cb = self.F(pre + "multihead_attn.in_proj_weight"), self.F(pre + "multihead_attn.in_proj_bias")
+            q = self.eh(B, HID)
             self.linear(x1, cw[:HID], cb[:HID], q, B)
-            qp = self.empty(B, NH, HID)
+            qp = self.eh(B, NH, HID)
             # qp[b,h,:] = Wk_h^T q_h / 8   (batched over heads)
             self.gemm(q, cw[HID:2 * HID], qp, B, HID, DH, 1, 0, HID, HID, NH * HID, alpha=scale, batch=NH, sA=DH,
                       sB=DH * HID, sC=HID)
-            probs = torch.empty(B, NH, L, dtype=torch.float32, device=self.a.device)
-            cc = self.empty(B, NH, HID)
-            call("eegf_xattn_fwd", self.code, B, L, P(h), P(qp), P(kbias), P(probs), P(cc), _stream())
-            ctxd = self.empty(B, HID)
+            probs = self._f32(B, NH, L)
+            cc = self.eh(B, NH, HID)
+            call("eegf_xattn_fwd", _code(h), F32, B, L, P(h), P(qp), P(kbias), P(probs), P(cc), _stream())
+            ctxd = self.eh(B, HID)
             # ctx[b, h*64+n] = sum_c cc[b,h,c] Wv[h*64+n, c] + bv[h*64+n]
             self.gemm(cc, cw[2 * HID:], ctxd, B, DH, HID, 1, 1, NH * HID, HID, HID, epi=_lib.EPI_BIAS,
                       bias=cb[2 * HID:], batch=NH, sA=HID, sB=DH * HID, sC=DH, sBias=DH)
-            ca = self.ws.get("dca", B * HID, self.dt).view(B, HID)
-            self.linear(ctxd, self.W(pre + "multihead_attn.out_proj.weight"),
+            ca = self.eh(B, HID)
+            self.linear(ctxd, self.F(pre + "multihead_attn.out_proj.weight"),
                         self.F(pre + "multihead_attn.out_proj.bias"), ca, B)
-            x2, ln2 = self.empty(B, HID), (self.empty(B, HID), self._f32(B), self._f32(B))
+            x2, ln2 = self.eh(B, HID), (self.eh(B, HID), self._f32(B), self._f32(B))
             self.ln_fwd(ca, x1, pre + "norm2", B, x2, *ln2, 1e-5, ddrop, 1, sv.rng + 101 + 8 * d)
-            f1 = self.empty(B, DEC_FF)
-            self.linear(x2, self.W(pre + "linear1.weight"), self.F(pre + "linear1.bias"), f1, B, epi=_lib.EPI_BIAS_RELU)
-            f2 = self.ws.get("df2", B * HID, self.dt).view(B, HID)
-            self.linear(f1, self.W(pre + "linear2.weight"), self.F(pre + "linear2.bias"), f2, B)
-            x3, ln3 = self.empty(B, HID), (self.empty(B, HID), self._f32(B), self._f32(B))
+            f1 = self.eh(B, DEC_FF)
+            self.linear(x2, self.F(pre + "linear1.weight"), self.F(pre + "linear1.bias"), f1, B, epi=_lib.EPI_BIAS_RELU)
+            f2 = self.eh(B, HID)
+            self.linear(f1, self.F(pre + "linear2.weight"), self.F(pre + "linear2.bias"), f2, B)
+            x3, ln3 = self.eh(B, HID), (self.eh(B, HID), self._f32(B), self._f32(B))
             self.ln_fwd(f2, x2, pre + "norm3", B, x3, *ln3, 1e-5, ddrop, 1, sv.rng + 102 + 8 * d)
             dl.append(dict(x=x, v=v, x1=x1, ln1=ln1, q=q, qp=qp, probs=probs, cc=cc, ctx=ctxd, x2=x2, ln2=ln2, f1=f1,
                            ln3=ln3))
@@ -334,27 +333,27 @@ class FusionEngine:
         t["dec"] = dl
         cross = x
 
-        # ---------------- fusion + privacy stage
-        g = self.empty(B, FUSED)
+        # ---------------- fusion + privacy stage (fp32)
+        g = self.eh(B, FUSED)
         xn = self._f32(B, FUSED)
         amin = torch.empty(B, dtype=torch.int32, device=self.a.device)
         amax = torch.empty_like(amin)
         rng_ = self._f32(B)
         inj = self.injected or {}
         eps_a = math.exp(cfg.eps)
-        call("eegf_fusion_fwd", self.code, B, self.variant, P(pooled), HID, P(vis), HID, P(cross), HID,
+        call("eegf_fusion_fwd", F32, B, self.variant, P(pooled), HID, P(vis), HID, P(cross), HID,
              P(self.F("DP")) if "DP" in self.a.offsets else None, P(inj.get("noise")), P(inj.get("gumbels")),
              P(inj.get("row_noise")), int(hard), 0 if cfg.eps_mode == "newfrac" else 1, eps_a, 1.0 / cfg.eps,
              self.cfg.seed, sv.rng + 200, P(g), P(xn), P(amin), P(amax), P(rng_), _stream())
         t["fuse"] = dict(g=g, xn=xn, amin=amin, amax=amax, range=rng_, inj=inj, cross=cross)
 
-        # ---------------- head
-        z1 = self.empty(B, FUSED)
-        self.linear(g, self.W("fc_layers.0.weight"), self.F("fc_layers.0.bias"), z1, B, epi=_lib.EPI_BIAS_RELU)
-        z2 = self.empty(B, HID)
-        self.linear(z1, self.W("fc_layers.2.weight"), self.F("fc_layers.2.bias"), z2, B, epi=_lib.EPI_BIAS_TANH)
-        logits = self.empty(B, 2)
-        self.linear(z2, self.W("classifier.weight"), self.F("classifier.bias"), logits, B)
+        # ---------------- head (fp32)
+        z1 = self.eh(B, FUSED)
+        self.linear(g, self.F("fc_layers.0.weight"), self.F("fc_layers.0.bias"), z1, B, epi=_lib.EPI_BIAS_RELU)
+        z2 = self.eh(B, HID)
+        self.linear(z1, self.F("fc_layers.2.weight"), self.F("fc_layers.2.bias"), z2, B, epi=_lib.EPI_BIAS_TANH)
+        logits = self.eh(B, 2)
+        self.linear(z2, self.F("classifier.weight"), self.F("classifier.bias"), logits, B)
         t["head"] = dict(z1=z1, z2=z2)
         return logits, sv
 
@@ -372,31 +371,31 @@ class FusionEngine:
         R = B * L
         pdrop = cfg.hidden_dropout if sv.training else 0.0
         ddrop = cfg.dec_dropout if sv.training else 0.0
-        dlogits = dlogits.to(self.dt).contiguous()
+        dlogits = dlogits.float().contiguous()
         hd = t["head"]
         fz = t["fuse"]
         g = fz["g"]
 
-        # ---------------- head
+        # ---------------- head (fp32)
         self.wgrad(dlogits, hd["z2"], "classifier.weight", B)
         self.bgrad(dlogits, "classifier.bias", B)
-        dz2 = self.empty(B, HID)
-        self.dgrad(dlogits, self.W("classifier.weight"), dz2, B, epi=_lib.EPI_DTANH, aux=hd["z2"])
+        dz2 = self.eh(B, HID)
+        self.dgrad(dlogits, self.F("classifier.weight"), dz2, B, epi=_lib.EPI_DTANH, aux=hd["z2"])
         self.wgrad(dz2, hd["z1"], "fc_layers.2.weight", B)
         self.bgrad(dz2, "fc_layers.2.bias", B)
-        dz1 = self.empty(B, FUSED)
-        self.dgrad(dz2, self.W("fc_layers.2.weight"), dz1, B, epi=_lib.EPI_DRELU, aux=hd["z1"])
+        dz1 = self.eh(B, FUSED)
+        self.dgrad(dz2, self.F("fc_layers.2.weight"), dz1, B, epi=_lib.EPI_DRELU, aux=hd["z1"])
         self.wgrad(dz1, g, "fc_layers.0.weight", B)
         self.bgrad(dz1, "fc_layers.0.bias", B)
-        dg = self.empty(B, FUSED)
-        self.dgrad(dz1, self.W("fc_layers.0.weight"), dg, B)
+        dg = self.eh(B, FUSED)
+        self.dgrad(dz1, self.F("fc_layers.0.weight"), dg, B)
 
         # ---------------- fusion / privacy stage
-        dpooled, dvis, dcross = self.empty(B, HID), self.empty(B, HID), self.empty(B, HID)
+        dpooled, dvis, dcross = self.eh(B, HID), self.eh(B, HID), self.eh(B, HID)
         has_dp = "DP" in self.a.offsets and self.variant == _lib.FUSE_PRIGUMBEL and self.need("DP")
         ddp = self._f32(B, FUSED) if has_dp else None
         inj = fz["inj"]
-        call("eegf_fusion_bwd", self.code, B, self.variant, P(dg), P(fz["xn"]), P(fz["amin"]), P(fz["amax"]),
+        call("eegf_fusion_bwd", F32, B, self.variant, P(dg), P(fz["xn"]), P(fz["amin"]), P(fz["amax"]),
              P(fz["range"]), P(self.F("DP")) if "DP" in self.a.offsets else None, P(inj.get("noise")),
              P(inj.get("gumbels")), int(sv.hard), 0 if cfg.eps_mode == "newfrac" else 1, math.exp(cfg.eps),
              self.cfg.seed, sv.rng + 200, P(dpooled), HID, P(dvis), HID, P(dcross), HID, P(ddp), _stream())
@@ -405,7 +404,7 @@ class FusionEngine:
         if head_only:
             return
 
-        # ---------------- decoder backward
+        # ---------------- decoder backward (fp32; memory gradient in the encoder dtype)
         mem = t["mem"]
         dmem = self.empty(R, HID)
         dx3 = dcross
@@ -413,24 +412,22 @@ class FusionEngine:
         for d in reversed(range(DEC_L)):
             pre = f"multi_head_decoder.layers.{d}."
             s = t["dec"][d]
-            # LN3: x3 = LN(drop(f2) + x2)
-            df2, dx2 = self.empty(B, HID), self.empty(B, HID)
+            df2, dx2 = self.eh(B, HID), self.eh(B, HID)
             self.ln_bwd(dx3, *s["ln3"], pre + "norm3", B, df2, dx2, ddrop, 1, sv.rng + 102 + 8 * d)
             self.wgrad(df2, s["f1"], pre + "linear2.weight", B)
             self.bgrad(df2, pre + "linear2.bias", B)
-            df1 = self.empty(B, DEC_FF)
-            self.dgrad(df2, self.W(pre + "linear2.weight"), df1, B, epi=_lib.EPI_DRELU, aux=s["f1"])
+            df1 = self.eh(B, DEC_FF)
+            self.dgrad(df2, self.F(pre + "linear2.weight"), df1, B, epi=_lib.EPI_DRELU, aux=s["f1"])
             self.wgrad(df1, s["x2"], pre + "linear1.weight", B)
             self.bgrad(df1, pre + "linear1.bias", B)
-            self.dgrad(df1, self.W(pre + "linear1.weight"), dx2, B, beta=1.0)
-            # LN2: x2 = LN(drop(ca) + x1)
-            dca, dx1 = self.empty(B, HID), self.empty(B, HID)
+            self.dgrad(df1, self.F(pre + "linear1.weight"), dx2, B, beta=1.0)
+            dca, dx1 = self.eh(B, HID), self.eh(B, HID)
             self.ln_bwd(dx2, *s["ln2"], pre + "norm2", B, dca, dx1, ddrop, 1, sv.rng + 101 + 8 * d)
             self.wgrad(dca, s["ctx"], pre + "multihead_attn.out_proj.weight", B)
             self.bgrad(dca, pre + "multihead_attn.out_proj.bias", B)
-            dctx = self.empty(B, HID)
-            self.dgrad(dca, self.W(pre + "multihead_attn.out_proj.weight"), dctx, B)
-            cw = self.W(pre + "multihead_attn.in_proj_weight")
+            dctx = self.eh(B, HID)
+            self.dgrad(dca, self.F(pre + "multihead_attn.out_proj.weight"), dctx, B)
+            cw = self.F(pre + "multihead_attn.in_proj_weight")
             gname = pre + "multihead_attn.in_proj_weight"
             bname = pre + "multihead_attn.in_proj_bias"
             if self.need(gname):
@@ -440,14 +437,14 @@ class FusionEngine:
                           sA=DH, sB=HID, sC=DH * HID)
             if self.need(bname):
                 self.bgrad(dctx, bname, B, out=self.G(bname)[2 * HID:])
-            dcc = self.empty(B, NH, HID)
+            dcc = self.eh(B, NH, HID)
             # dcc[b,h,c] = sum_n dctx[b, h*64+n] Wv[h*64+n, c]
             self.gemm(dctx, cw[2 * HID:], dcc, B, HID, DH, 1, 0, HID, HID, NH * HID, batch=NH, sA=DH, sB=DH * HID,
                       sC=HID)
-            dqp = self.empty(B, NH, HID)
-            call("eegf_xattn_bwd", self.code, B, L, P(mem), P(s["qp"]), P(s["probs"]), P(dcc), P(dmem),
+            dqp = self.eh(B, NH, HID)
+            call("eegf_xattn_bwd", _code(mem), F32, B, L, P(mem), P(s["qp"]), P(s["probs"]), P(dcc), P(dmem),
                  0.0 if d == DEC_L - 1 else 1.0, P(dqp), _stream())
-            dq = self.empty(B, HID)
+            dq = self.eh(B, HID)
             # dq[b, h*64+i] = sum_c dqp[b,h,c] Wk[h*64+i, c] / 8
             self.gemm(dqp, cw[HID:2 * HID], dq, B, DH, HID, 1, 1, NH * HID, HID, HID, alpha=scale, batch=NH, sA=HID,
                       sB=DH * HID, sC=DH)
@@ -459,14 +456,13 @@ class FusionEngine:
             if self.need(bname):
                 self.bgrad(dq, bname, B, out=self.G(bname)[:HID])
             self.dgrad(dq, cw[:HID], dx1, B, beta=1.0)
-            # LN1: x1 = LN(drop(sa) + x)
-            dsa, dx = self.empty(B, HID), self.empty(B, HID)
+            dsa, dx = self.eh(B, HID), self.eh(B, HID)
             self.ln_bwd(dx1, *s["ln1"], pre + "norm1", B, dsa, dx, ddrop, 1, sv.rng + 100 + 8 * d)
             self.wgrad(dsa, s["v"], pre + "self_attn.out_proj.weight", B)
             self.bgrad(dsa, pre + "self_attn.out_proj.bias", B)
-            dv = self.empty(B, HID)
-            self.dgrad(dsa, self.W(pre + "self_attn.out_proj.weight"), dv, B)
-            sw = self.W(pre + "self_attn.in_proj_weight")
+            dv = self.eh(B, HID)
+            self.dgrad(dsa, self.F(pre + "self_attn.out_proj.weight"), dv, B)
+            sw = self.F(pre + "self_attn.in_proj_weight")
             if self.need(pre + "self_attn.in_proj_weight"):
                 self.gemm(dv, s["x"], self.G(pre + "self_attn.in_proj_weight")[2 * HID:], HID, HID, B, 0, 0, HID, HID,
                           HID, beta=1.0)
@@ -475,16 +471,21 @@ class FusionEngine:
             self.dgrad(dv, sw[2 * HID:], dx, B, beta=1.0)
             dx3 = dx
         # vis receives the fusion path + the decoder path
-        call("eegf_axpby", self.code, B * HID, 1.0, P(dx3), 1.0, P(dvis), _stream())
+        call("eegf_axpby", F32, B * HID, 1.0, P(dx3), 1.0, P(dvis), _stream())
         self.wgrad(dvis, t["act"], "visual_encoder.weight", B)
         self.bgrad(dvis, "visual_encoder.bias", B)
 
-        # ---------------- pooler
+        # ---------------- pooler (fp32 tanh derivative, encoder-dtype GEMMs)
         pooled = t["pooled"]
-        dpp = self.empty(B, HID)
-        call("eegf_tanh_bwd", self.code, B * HID, P(dpooled), P(pooled), P(dpp), _stream())
+        dpp32 = self.eh(B, HID)
+        call("eegf_tanh_bwd", F32, B * HID, P(dpooled), P(pooled), P(dpp32), _stream())
+        self.bgrad(dpp32, "bert.pooler.dense.bias", B)
+        if self.dt == torch.float32:
+            dpp = dpp32
+        else:
+            dpp = self.empty(B, HID)
+            call("eegf_cast_f32_bf16", B * HID, P(dpp32), P(dpp), _stream())
         self.wgrad(dpp, mem, "bert.pooler.dense.weight", B, ldx=L * HID)
-        self.bgrad(dpp, "bert.pooler.dense.bias", B)
         self.dgrad(dpp, self.W("bert.pooler.dense.weight"), dmem, B, ldo=L * HID, beta=1.0)
 
         # ---------------- BERT encoder backward

@@ -88,7 +88,7 @@ class PriGumbelTrainer:
     def _ce(self, logits, labels, i):
         B = logits.shape[0]
         dl = torch.empty_like(logits)
-        call("eegf_cross_entropy", self.e.code, B, 2, logits.data_ptr(), labels.data_ptr(), 0, 1.0,
+        call("eegf_cross_entropy", _lib.F32 if logits.dtype == torch.float32 else _lib.BF16, B, 2, logits.data_ptr(), labels.data_ptr(), 0, 1.0,
              self.loss[i:].data_ptr(), self.correct[i:].data_ptr(), dl.data_ptr(), _s())
         return dl
 
@@ -130,7 +130,7 @@ class SinglePassTrainer:
         e = self.e
         logits, sv = e.forward(batch, hard=True, training=True, save=True)
         dl = torch.empty_like(logits)
-        call("eegf_cross_entropy", e.code, logits.shape[0], 2, logits.data_ptr(), labels.data_ptr(), 0, 1.0,
+        call("eegf_cross_entropy", _lib.F32 if logits.dtype == torch.float32 else _lib.BF16, logits.shape[0], 2, logits.data_ptr(), labels.data_ptr(), 0, 1.0,
              self.loss.data_ptr(), self.correct.data_ptr(), dl.data_ptr(), _s())
         self.opt.zero_grad()
         e.needs_grad = self.params

@@ -45,7 +45,7 @@ extern "C" {
  * (model.py:24-32,62-63), and their input-/weight-gradient GEMMs.
  *   C[z][m,n] = epi(alpha * sum_k A(m,k) B(k,n)) + beta*C[z][m,n]
  *   a_kcontig: A(m,k)=A[m*lda+k] else A[k*lda+m];  b_kcontig: B(k,n)=B[n*ldb+k] else B[k*ldb+n]
- * dtype: EEGF_F32 (out F32) or EEGF_BF16 (out BF16, or F32 for weight gradients).
+ * dtype: EEGF_F32 (out F32) or EEGF_BF16 (out BF16, or F32: weight gradients, fp32 pooler output).
  * workspace (nullable, ws_bytes): fp32 split-K slabs; used when the tile grid under-fills the chip
  * and K is long (weight gradients over B*L tokens); the slabs are reduced in a fixed order. */
 int eegf_gemm(int dtype, int out_dtype, int a_kcontig, int b_kcontig, int epi,
@@ -101,12 +101,14 @@ int eegf_attn_bwd(int dtype, int B, int H, int L, const void* qkv, long ld_qkv, 
 /* Decoder cross-attention over the BERT memory with a single query token
  * (TransformerDecoderLayer._mha_block, transformer.py:1177-1196; model.py:40-43), in the
  * reduced form: qp [B,12,768] = Wk_h^T q_h / 8 (by eegf_gemm); probs [B,12,S] saved;
- * ctx [B,12,768] = sum_j p_j M_j.  key_bias [B,S] nullable. */
-int eegf_xattn_fwd(int dtype, int B, int S, const void* mem, const void* qp, const float* key_bias,
-                   float* probs, void* ctx, hipStream_t stream);
+ * ctx [B,12,768] = sum_j p_j M_j.  key_bias [B,S] nullable.  mem_dtype: the encoder's dtype;
+ * q_dtype: the decoder's (bf16 mode runs the decoder in fp32: F32 with a BF16 memory). */
+int eegf_xattn_fwd(int mem_dtype, int q_dtype, int B, int S, const void* mem, const void* qp,
+                   const float* key_bias, float* probs, void* ctx, hipStream_t stream);
 /* Backward: dmem [B,S,768] (= result + beta*dmem), dqp [B,12,768]. */
-int eegf_xattn_bwd(int dtype, int B, int S, const void* mem, const void* qp, const float* probs,
-                   const void* dctx, void* dmem, float beta, void* dqp, hipStream_t stream);
+int eegf_xattn_bwd(int mem_dtype, int q_dtype, int B, int S, const void* mem, const void* qp,
+                   const float* probs, const void* dctx, void* dmem, float beta, void* dqp,
+                   hipStream_t stream);
 
 /* Fused concat [pooled|img|cross] -> min-max -> privacy stage (variant FUSE_*), one row per
  * workgroup (model.py:46-61, past_acc.py:120-136, main_0430.py:76-85).  noise/gumbels (fp32

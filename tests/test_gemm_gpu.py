@@ -153,3 +153,37 @@ def test_gemm_wgrad_splitk(dt, M, N, K):
     k.gemm(dy, x, dw3, M=M, N=N, K=K, a_kc=0, b_kc=0, lda=M, ldb=N, ldc=N, workspace=ws)
     torch.cuda.synchronize()
     assert torch.equal(dw2, dw3)          # deterministic
+
+
+@pytest.mark.parametrize("epi", ["none", "bias", "bias_gelu", "bias_relu", "bias_tanh"])
+@pytest.mark.parametrize("M,N,K", [(4352, 808, 768), (2048, 2304, 256)])
+def test_gemm_big_fwd(epi, M, N, K):
+    """256x256 glds-pipelined bf16 kernel (M >= 2048), including M/N edge tiles."""
+    k = _k()
+    torch.manual_seed(7)
+    x = (torch.randn(M, K, device="cuda") * 0.3).to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda") * 0.3).to(torch.bfloat16)
+    b = torch.randn(N, device="cuda") if epi != "none" else None
+    aux = torch.empty(M, N, device="cuda", dtype=torch.bfloat16) if epi == "bias_gelu" else None
+    out = k.linear(x, w, b, epi=epi, aux=aux)
+    torch.cuda.synchronize()
+    ref, pre = _ref_epi(x.double() @ w.double().t(), epi, b, None, 1.0)
+    _check(out, ref, torch.bfloat16)
+    if pre is not None:
+        _check(aux, pre, torch.bfloat16)
+
+
+@pytest.mark.parametrize("epi", ["none", "dgelu", "drelu", "dtanh"])
+@pytest.mark.parametrize("M,N,K", [(4352, 808, 768), (2048, 3072, 320)])
+def test_gemm_big_dgrad(epi, M, N, K):
+    k = _k()
+    torch.manual_seed(8)
+    dy = torch.randn(M, K, device="cuda").to(torch.bfloat16)          # [M, N_out=K]
+    w = (torch.randn(K, N, device="cuda") * 0.2).to(torch.bfloat16)   # weight [N_out, N_in]
+    aux = torch.randn(M, N, device="cuda").to(torch.bfloat16) if epi != "none" else None
+    if epi == "dtanh":
+        aux = torch.tanh(aux.float()).to(torch.bfloat16)
+    out = k.linear_dgrad(dy, w, epi=epi, aux=aux, epi_scale=1.25)
+    torch.cuda.synchronize()
+    ref, _ = _ref_epi(dy.double() @ w.double(), epi, None, aux, 1.25)
+    _check(out, ref, torch.bfloat16)

@@ -156,6 +156,22 @@ def test_attention_fwd_bwd(dt, L, masked):
 
 
 @pytest.mark.parametrize("dt", DT)
+def test_xattn_mixed_dtypes(dt):
+    """bf16 memory with fp32 query/context (mixed-precision engine)."""
+    lib = _lib()
+    torch.manual_seed(9)
+    B, S = 2, 256
+    mem = torch.randn(B, S, 768, device="cuda").to(torch.bfloat16)
+    qp = 0.05 * torch.randn(B, 12, 768, device="cuda")
+    probs = torch.empty(B, 12, S, device="cuda")
+    cc = torch.empty(B, 12, 768, device="cuda")
+    lib.call("eegf_xattn_fwd", 1, 0, B, S, mem.data_ptr(), qp.data_ptr(), None, probs.data_ptr(), cc.data_ptr(), _s())
+    torch.cuda.synchronize()
+    p = torch.einsum("bhc,bjc->bhj", qp.double(), mem.double()).softmax(-1)
+    assert _rel(cc, torch.einsum("bhj,bjc->bhc", p, mem.double())) < 1e-5
+
+
+@pytest.mark.parametrize("dt", DT)
 def test_xattn_fwd_bwd(dt):
     lib = _lib()
     torch.manual_seed(2)
@@ -164,8 +180,8 @@ def test_xattn_fwd_bwd(dt):
     qp = (0.05 * torch.randn(B, 12, 768, device="cuda")).to(dt)
     probs = torch.empty(B, 12, S, device="cuda")
     cc = torch.empty(B, 12, 768, device="cuda", dtype=dt)
-    lib.call("eegf_xattn_fwd", _code(dt), B, S, mem.data_ptr(), qp.data_ptr(), None, probs.data_ptr(), cc.data_ptr(),
-             _s())
+    lib.call("eegf_xattn_fwd", _code(dt), _code(dt), B, S, mem.data_ptr(), qp.data_ptr(), None, probs.data_ptr(),
+             cc.data_ptr(), _s())
     torch.cuda.synchronize()
     m = mem.double().clone().requires_grad_()
     q = qp.double().clone().requires_grad_()
@@ -178,8 +194,8 @@ def test_xattn_fwd_bwd(dt):
     dmem = torch.randn_like(mem)
     dmem0 = dmem.double().clone()
     dqp = torch.empty_like(qp)
-    lib.call("eegf_xattn_bwd", _code(dt), B, S, mem.data_ptr(), qp.data_ptr(), probs.data_ptr(), dc.data_ptr(),
-             dmem.data_ptr(), 1.0, dqp.data_ptr(), _s())
+    lib.call("eegf_xattn_bwd", _code(dt), _code(dt), B, S, mem.data_ptr(), qp.data_ptr(), probs.data_ptr(),
+             dc.data_ptr(), dmem.data_ptr(), 1.0, dqp.data_ptr(), _s())
     torch.cuda.synchronize()
     assert _rel(dmem.double() - dmem0, m.grad) < _tol(dt) * 3
     assert _rel(dqp, q.grad) < _tol(dt) * 3
