@@ -16,7 +16,8 @@ import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-FFN1 = "gemm_big_kernelILb1ELi2E"          # mangled <true, EPI_BIAS_GELU>
+FFN1S = ("gemm_big_kernelILb1ELi2E", "gemm_big_kernel<true, 2>")   # <B_KC=true, EPI_BIAS_GELU>
+FFN1 = FFN1S[1]
 
 
 def short(name: str) -> str:
@@ -35,7 +36,7 @@ def stats(tag, d, steps):
         t = float(r["TotalDurationNs"])
         out.append(f"| {t / 1e6 / steps:.3f} | {100 * t / tot:.1f} | {int(r['Calls']) / steps:.1f} | "
                    f"{float(r['AverageNs']) / 1e3:.1f} | `{short(r['Name'])}` |")
-        if FFN1 in r["Name"]:
+        if any(k in r["Name"] for k in FFN1S):
             ffn1 = float(r["AverageNs"]) / 1e6
     if ffn1:
         out += ["", f"roofline kernel (FFN1 fwd, `{FFN1}...`): average {ffn1:.4f} ms = "
@@ -47,7 +48,7 @@ def stats(tag, d, steps):
 def pmc(d, counter):
     f = next(Path(d).glob("*counter_collection.csv"))
     vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(f))
-            if FFN1 in r["Kernel_Name"] and r["Counter_Name"] == counter]
+            if any(k in r["Kernel_Name"] for k in FFN1S) and r["Counter_Name"] == counter]
     return sum(vals) / len(vals) if vals else None
 
 
