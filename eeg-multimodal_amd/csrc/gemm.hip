@@ -210,9 +210,10 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmArgs g) {
       for (int j = 0; j < 4; ++j) {
         const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
         float* cp = slab + (long)m * g.N + n;
-        if (n + 3 < g.N && ((uintptr_t)cp & 15) == 0) *(f32x4*)cp = acc[i][j];
+        const f32x4 v = acc[i][j] * g.alpha;
+        if (n + 3 < g.N && ((uintptr_t)cp & 15) == 0) *(f32x4*)cp = v;
         else
-          for (int r = 0; r < 4; ++r) if (n + r < g.N) cp[r] = acc[i][j][r];
+          for (int r = 0; r < 4; ++r) if (n + r < g.N) cp[r] = v[r];
       }
     }
     return;
@@ -343,28 +344,57 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmArgs g) {
   }
 }
 
+// out = epi(sum_s slab[s] + bias) (+ beta*out): the split-K combine, elementwise with the epilogue
+// (slabs already hold alpha*AB).  Fixed summation order -> bitwise reproducible.
+template <typename TO, int EPI>
 __global__ void __launch_bounds__(256) gemm_splitk_reduce(const float* __restrict__ slabs, int splits, int M, int N,
-                                                          void* C, int c_is_bf16, long ldc, float beta) {
-  const long i4 = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
+                                                          TO* C, long ldc, float beta, const float* bias, TO* aux,
+                                                          long ldaux, float epi_scale) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
   const long total = (long)M * N;
-  if (i4 >= total) return;
-  float o[4] = {0.f, 0.f, 0.f, 0.f};
-  const bool vec = (i4 + 4 <= total) && (N % 4 == 0);
-  for (int s = 0; s < splits; ++s) {
-    const float* p = slabs + (long)s * total + i4;
-    if (vec) { const f32x4 v = *(const f32x4*)p; o[0] += v[0]; o[1] += v[1]; o[2] += v[2]; o[3] += v[3]; }
-    else for (int r = 0; r < 4 && i4 + r < total; ++r) o[r] += p[r];
+  if (e >= total) return;
+  float v = 0.f;
+  for (int s = 0; s < splits; ++s) v += slabs[(long)s * total + e];
+  const long m = e / N, n = e % N;
+  TO* c = C + m * ldc + n;
+  if (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_TANH) v += bias[n];
+  if (EPI == EPI_BIAS_GELU) { aux[m * ldaux + n] = from_f32<TO>(v); v = gelu_f(v); }
+  else if (EPI == EPI_BIAS_RELU) v = fmaxf(v, 0.f);
+  else if (EPI == EPI_BIAS_TANH) v = tanhf(v);
+  else if (EPI == EPI_DGELU) v *= gelu_grad(to_f32(aux[m * ldaux + n]));
+  else if (EPI == EPI_DRELU) v = to_f32(aux[m * ldaux + n]) > 0.f ? v * epi_scale : 0.f;
+  else if (EPI == EPI_DTANH) { const float y = to_f32(aux[m * ldaux + n]); v *= 1.f - y * y; }
+  if (beta != 0.f) v += beta * to_f32(*c);
+  *c = from_f32<TO>(v);
+}
+
+template <typename TO>
+int splitk_reduce_t(int epi, const float* ws, int splits, int M, int N, void* C, long ldc, float beta,
+                    const float* bias, void* aux, long ldaux, float scale, hipStream_t st) {
+  const dim3 grid((unsigned)(((long)M * N + 255) / 256));
+#define RED(E) hipLaunchKernelGGL((gemm_splitk_reduce<TO, E>), grid, dim3(256), 0, st, ws, splits, M, N, (TO*)C, ldc, \
+                                  beta, bias, (TO*)aux, ldaux, scale)
+  switch (epi) {
+    case EPI_NONE: RED(EPI_NONE); break;
+    case EPI_BIAS: RED(EPI_BIAS); break;
+    case EPI_BIAS_GELU: RED(EPI_BIAS_GELU); break;
+    case EPI_BIAS_RELU: RED(EPI_BIAS_RELU); break;
+    case EPI_BIAS_TANH: RED(EPI_BIAS_TANH); break;
+    case EPI_DGELU: RED(EPI_DGELU); break;
+    case EPI_DRELU: RED(EPI_DRELU); break;
+    case EPI_DTANH: RED(EPI_DTANH); break;
+    default: return EEGF_ERR_ARG;
   }
-  for (int r = 0; r < 4 && i4 + r < total; ++r) {
-    const long e = i4 + r, m = e / N, n = e % N;
-    if (c_is_bf16) {
-      bf16* c = (bf16*)C + m * ldc + n;
-      *c = (bf16)(o[r] + (beta != 0.f ? beta * (float)*c : 0.f));
-    } else {
-      float* c = (float*)C + m * ldc + n;
-      *c = o[r] + (beta != 0.f ? beta * *c : 0.f);
-    }
-  }
+#undef RED
+  return (int)hipGetLastError();
+}
+
+int splitk_reduce_dispatch(int epi, int out_bf16, const float* ws, int splits, int M, int N, void* C, long ldc,
+                           float beta, float alpha, const float* bias, void* aux, long ldaux, float scale,
+                           hipStream_t st) {
+  (void)alpha;
+  return out_bf16 ? splitk_reduce_t<bf16>(epi, ws, splits, M, N, C, ldc, beta, bias, aux, ldaux, scale, st)
+                  : splitk_reduce_t<float>(epi, ws, splits, M, N, C, ldc, beta, bias, aux, ldaux, scale, st);
 }
 
 template <typename T, bool AKC, bool BKC, typename TO, int EPI>
@@ -407,9 +437,9 @@ int dispatch_epi(int epi, int akc, int bkc, const GemmArgs& a, int batch, hipStr
 
 }  // namespace
 
-int eegf_gemm_big(int a_kc, int b_kc, int epi, int M, int N, int K, const void* A, long lda, const void* B, long ldb,
-                  void* C, long ldc, const float* bias, void* aux, long ldaux, float alpha, float beta,
-                  float epi_scale, hipStream_t stream);
+int eegf_gemm_big(int a_kc, int b_kc, int epi, int out_f32, int M, int N, int K, const void* A, long lda,
+                  const void* B, long ldb, void* C, long ldc, const float* bias, void* aux, long ldaux, float alpha,
+                  float beta, float epi_scale, void* workspace, long ws_bytes, hipStream_t stream);
 
 static int lds_epi_enabled() {
   static const int on = [] { const char* e = getenv("EEGF_GEMM_LDS_EPI"); return (e && e[0] == '0') ? 0 : 1; }();
@@ -441,12 +471,19 @@ extern "C" int eegf_gemm(int dtype, int out_dtype, int a_kcontig, int b_kcontig,
   }
   GemmArgs a{A, B, C, bias, aux, lda, ldb, ldc, ldaux, strideA, strideB, strideC, strideAux, strideBias, M, N, K, alpha, beta, epi_scale, 0,
              lds_epi_enabled()};
-  // split-K for under-filled grids with a long contraction (weight gradients: K = tokens)
+  if (dtype == EEGF_BF16 && batch == 1 && big_enabled()) {
+    const int st = eegf_gemm_big(a_kcontig, b_kcontig, epi, out_dtype == EEGF_F32, M, N, K, A, lda, B, ldb, C, ldc,
+                                 bias, aux, ldaux, alpha, beta, epi_scale, workspace, ws_bytes, stream);
+    if (st != 1) return st;
+  }
+  // split-K for under-filled grids: long contractions (weight gradients, K = tokens) and the
+  // batch-row decoder / head GEMMs (M = B); the fixed-order slab reduction applies the epilogue.
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  if (epi == EPI_NONE && batch == 1 && workspace && tiles < 512 && K >= 4096) {
+  if (batch == 1 && workspace && tiles < 512 && (K >= 4096 || (tiles <= 64 && K >= 512))) {
     const int kt = dtype == EEGF_F32 ? 32 : 64;
     int splits = 1;
-    while (splits * tiles < 768 && K / (splits * 2) >= 1024) splits *= 2;
+    const int min_slice = K >= 4096 ? 1024 : 256;
+    while (splits * tiles < 768 && K / (splits * 2) >= min_slice) splits *= 2;
     while (splits > 1 && (long)splits * M * N * 4 > ws_bytes) splits /= 2;
     if (splits > 1) {
       int ks = (K + splits - 1) / splits;
@@ -458,10 +495,8 @@ extern "C" int eegf_gemm(int dtype, int out_dtype, int a_kcontig, int b_kcontig,
       if (dtype == EEGF_F32) st = dispatch_layout_split<float, float>(a_kcontig, b_kcontig, b, stream, splits);
       else st = dispatch_layout_split<bf16, float>(a_kcontig, b_kcontig, b, stream, splits);
       if (st) return st;
-      const long n4 = ((long)M * N + 3) / 4;
-      hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, stream,
-                         (const float*)workspace, splits, M, N, C, out_dtype == EEGF_BF16, ldc, beta);
-      return (int)hipGetLastError();
+      return splitk_reduce_dispatch(epi, out_dtype == EEGF_BF16, (const float*)workspace, splits, M, N, C, ldc, beta,
+                                    alpha, bias, aux, ldaux, epi_scale, stream);
     }
   }
   if (dtype == EEGF_F32) {
@@ -469,11 +504,6 @@ extern "C" int eegf_gemm(int dtype, int out_dtype, int a_kcontig, int b_kcontig,
     return dispatch_epi<float, float>(epi, a_kcontig, b_kcontig, a, batch, stream);
   }
   if (dtype == EEGF_BF16) {
-    if (out_dtype == EEGF_BF16 && batch == 1 && big_enabled()) {
-      const int st = eegf_gemm_big(a_kcontig, b_kcontig, epi, M, N, K, A, lda, B, ldb, C, ldc, bias, aux, ldaux, alpha,
-                                   beta, epi_scale, stream);
-      if (st != 1) return st;
-    }
     if (out_dtype == EEGF_BF16) return dispatch_epi<bf16, bf16>(epi, a_kcontig, b_kcontig, a, batch, stream);
     if (out_dtype == EEGF_F32) return dispatch_epi<bf16, float>(epi, a_kcontig, b_kcontig, a, batch, stream);
   }

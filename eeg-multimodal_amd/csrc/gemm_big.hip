@@ -24,10 +24,11 @@ constexpr int LDC = TN + 8;                   // epilogue tile row stride (eleme
 constexpr int LDS_ELEMS = TM * LDC;           // 135168 B >= 4 * TILE * 2 B
 
 struct BigArgs {
-  const bf16* A; const bf16* B; bf16* C; const float* bias; bf16* aux;
+  const bf16* A; const bf16* B; void* C; const float* bias; bf16* aux;
   long lda, ldb, ldc, ldaux;
   int M, N, K;
-  float alpha, epi_scale;
+  float alpha, beta, epi_scale;
+  int ksplit;            // >0: split-K slice length; C = fp32 slabs [blockIdx.y][M][N]
 };
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -117,7 +118,7 @@ DEV void tile_io(bf16* lds, bf16* gp, long ld, int m0, int n0, int M, int N, int
 DEV void ld4(const bf16* p, float (&v)[4]) { const bf16x4 x = *(const bf16x4*)p; v[0] = (float)x[0]; v[1] = (float)x[1]; v[2] = (float)x[2]; v[3] = (float)x[3]; }
 DEV void st4(bf16* p, const float (&v)[4]) { bf16x4 x; x[0] = (bf16)v[0]; x[1] = (bf16)v[1]; x[2] = (bf16)v[2]; x[3] = (bf16)v[3]; *(bf16x4*)p = x; }
 
-template <bool BKC, int EPI>
+template <bool AKC, bool BKC, int EPI, typename TO>
 __global__ void __launch_bounds__(NT, 1) gemm_big_kernel(BigArgs g) {
   __shared__ __attribute__((aligned(16))) bf16 lds[LDS_ELEMS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -133,19 +134,24 @@ __global__ void __launch_bounds__(NT, 1) gemm_big_kernel(BigArgs g) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = g.K / BK;
-  stage_rowmajor(lds, g.A, g.lda, m0, g.M, 0, wave, lane);
-  if (BKC) stage_rowmajor(lds + TILE, g.B, g.ldb, n0, g.N, 0, wave, lane);
-  else stage_kmajor(lds + TILE, g.B, g.ldb, n0, g.N, 0, wave, lane);
+  int kbeg = 0, kend = g.K;
+  if (g.ksplit > 0) { kbeg = blockIdx.y * g.ksplit; kend = min(g.K, kbeg + g.ksplit); }
+  const int nk = (kend - kbeg) / BK;
+  if (AKC) stage_rowmajor(lds, g.A, g.lda, m0, g.M, kbeg, wave, lane);
+  else stage_kmajor(lds, g.A, g.lda, m0, g.M, kbeg, wave, lane);
+  if (BKC) stage_rowmajor(lds + TILE, g.B, g.ldb, n0, g.N, kbeg, wave, lane);
+  else stage_kmajor(lds + TILE, g.B, g.ldb, n0, g.N, kbeg, wave, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = (kt & 1) * 2 * TILE, nxt = 2 * TILE - cur;
     if (kt + 1 < nk) {
-      stage_rowmajor(lds + nxt, g.A, g.lda, m0, g.M, (kt + 1) * BK, wave, lane);
-      if (BKC) stage_rowmajor(lds + nxt + TILE, g.B, g.ldb, n0, g.N, (kt + 1) * BK, wave, lane);
-      else stage_kmajor(lds + nxt + TILE, g.B, g.ldb, n0, g.N, (kt + 1) * BK, wave, lane);
+      const int kn = kbeg + (kt + 1) * BK;
+      if (AKC) stage_rowmajor(lds + nxt, g.A, g.lda, m0, g.M, kn, wave, lane);
+      else stage_kmajor(lds + nxt, g.A, g.lda, m0, g.M, kn, wave, lane);
+      if (BKC) stage_rowmajor(lds + nxt + TILE, g.B, g.ldb, n0, g.N, kn, wave, lane);
+      else stage_kmajor(lds + nxt + TILE, g.B, g.ldb, n0, g.N, kn, wave, lane);
     }
     const bf16* As = lds + cur;
     const bf16* Bs = lds + cur + TILE;
@@ -160,7 +166,8 @@ __global__ void __launch_bounds__(NT, 1) gemm_big_kernel(BigArgs g) {
       }
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        const bf16x8 a = rd_row(As, wm * 128 + i * 16 + (lane & 15), 4 * kc + (lane >> 4));
+        const bf16x8 a = AKC ? rd_row(As, wm * 128 + i * 16 + (lane & 15), 4 * kc + (lane >> 4))
+                             : rd_col(As, 32 * kc + 8 * (lane >> 4), wm * 128 + i * 16, lane);
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = mma16(b[j], a, acc[i][j]);
       }
@@ -169,12 +176,39 @@ __global__ void __launch_bounds__(NT, 1) gemm_big_kernel(BigArgs g) {
     __syncthreads();
   }
 
-  // ---- LDS-staged epilogue ----
+  // ---- epilogue ----
   constexpr bool HAS_BIAS = EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_TANH;
   constexpr bool AUX_IN = EPI == EPI_DGELU || EPI == EPI_DRELU || EPI == EPI_DTANH;
+  if constexpr (sizeof(TO) == 4) {
+    // fp32 output (weight gradients): direct 16-B stores of 4 consecutive columns; split-K slabs
+    float* Cf = (float*)g.C + (g.ksplit > 0 ? (long)blockIdx.y * g.M * g.N : 0);
+    const long ldc = g.ksplit > 0 ? g.N : g.ldc;
+    const float beta = g.ksplit > 0 ? 0.f : g.beta;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = m0 + wm * 128 + i * 16 + (lane & 15);
+      if (m >= g.M) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+        float* cp = Cf + (long)m * ldc + n;
+        f32x4 v = acc[i][j] * g.alpha;
+        if (n + 3 < g.N && ((uintptr_t)cp & 15) == 0) {
+          if (beta != 0.f) v += beta * *(const f32x4*)cp;
+          *(f32x4*)cp = v;
+        } else {
+          for (int r = 0; r < 4; ++r)
+            if (n + r < g.N) cp[r] = v[r] + (beta != 0.f ? beta * cp[r] : 0.f);
+        }
+      }
+    }
+    return;
+  } else {
+  // LDS-staged bf16 epilogue: every global access is a full 16-B-per-lane row segment
   bf16* ct = lds;
-  if (AUX_IN) {
-    tile_io<true>(ct, g.aux, g.ldaux, m0, n0, g.M, g.N, tid);
+  bf16* Cb = (bf16*)g.C;
+  if (AUX_IN || g.beta != 0.f) {
+    tile_io<true>(ct, AUX_IN ? g.aux : Cb, AUX_IN ? g.ldaux : g.ldc, m0, n0, g.M, g.N, tid);
     __syncthreads();
   }
 #pragma unroll
@@ -188,7 +222,7 @@ __global__ void __launch_bounds__(NT, 1) gemm_big_kernel(BigArgs g) {
     for (int i = 0; i < 8; ++i) {
       bf16* lp = ct + (wm * 128 + i * 16 + (lane & 15)) * LDC + nl;
       float av[4] = {0.f, 0.f, 0.f, 0.f};
-      if (AUX_IN) ld4(lp, av);
+      if (AUX_IN || g.beta != 0.f) ld4(lp, av);
       float o[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -199,6 +233,7 @@ __global__ void __launch_bounds__(NT, 1) gemm_big_kernel(BigArgs g) {
         else if (EPI == EPI_DGELU) v *= gelu_grad(av[r]);
         else if (EPI == EPI_DRELU) v = av[r] > 0.f ? v * g.epi_scale : 0.f;
         else if (EPI == EPI_DTANH) v *= (1.f - av[r] * av[r]);
+        else if (g.beta != 0.f) v += g.beta * av[r];         // EPI_NONE accumulate (beta * C)
         acc[i][j][r] = v;
         o[r] = v;
       }
@@ -220,41 +255,83 @@ __global__ void __launch_bounds__(NT, 1) gemm_big_kernel(BigArgs g) {
       }
     __syncthreads();
   }
-  tile_io<false>(ct, g.C, g.ldc, m0, n0, g.M, g.N, tid);
+  tile_io<false>(ct, Cb, g.ldc, m0, n0, g.M, g.N, tid);
+  }
 }
 
-template <bool BKC, int EPI>
-int launch_big(const BigArgs& a, hipStream_t s) {
+template <bool AKC, bool BKC, int EPI, typename TO>
+int launch_big(const BigArgs& a, int splits, hipStream_t s) {
   const int tiles = ((a.M + TM - 1) / TM) * ((a.N + TN - 1) / TN);
-  hipLaunchKernelGGL((gemm_big_kernel<BKC, EPI>), dim3(tiles), dim3(NT), 0, s, a);
+  hipLaunchKernelGGL((gemm_big_kernel<AKC, BKC, EPI, TO>), dim3(tiles, splits), dim3(NT), 0, s, a);
   return (int)hipGetLastError();
+}
+
+__global__ void __launch_bounds__(256) big_splitk_reduce(const float* __restrict__ slabs, int splits, long MN, int N,
+                                                         float* C, long ldc, float beta) {
+  const long i4 = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i4 >= MN) return;
+  f32x4 o = {0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < splits; ++s) o += *(const f32x4*)(slabs + (long)s * MN + i4);
+  const long m = i4 / N, n = i4 % N;          // N % 4 == 0: a 4-group never crosses a row
+  float* c = C + m * ldc + n;
+  if (beta != 0.f) o += beta * *(const f32x4*)c;
+  *(f32x4*)c = o;
 }
 
 }  // namespace
 
 // Internal entry used by eegf_gemm (gemm.hip).  Returns 1 if the shape is not eligible.
-int eegf_gemm_big(int a_kc, int b_kc, int epi, int M, int N, int K, const void* A, long lda, const void* B, long ldb,
-                  void* C, long ldc, const float* bias, void* aux, long ldaux, float alpha, float beta,
-                  float epi_scale, hipStream_t stream) {
-  if (!a_kc || beta != 0.f) return 1;
-  if (M < 2048 || N < 256 || K % BK != 0 || M % 8 != 0 || N % 8 != 0) return 1;
+//   bf16 out: token-sized forward / input-gradient GEMMs (A K-contiguous), any beta;
+//   fp32 out: weight gradients (A, B k-major, EPI_NONE), split-K over the token axis with fp32 slabs
+//             in `workspace` reduced in a fixed order (bitwise reproducible), beta applied once.
+int eegf_gemm_big(int a_kc, int b_kc, int epi, int out_f32, int M, int N, int K, const void* A, long lda,
+                  const void* B, long ldb, void* C, long ldc, const float* bias, void* aux, long ldaux, float alpha,
+                  float beta, float epi_scale, void* workspace, long ws_bytes, hipStream_t stream) {
+  if (K % BK != 0 || M % 8 != 0 || N % 8 != 0) return 1;
   if (lda % 8 || ldb % 8 || ldc % 8 || (aux && ldaux % 8)) return 1;
   if ((((uintptr_t)A | (uintptr_t)B | (uintptr_t)C | (uintptr_t)aux) & 15) != 0) return 1;
-  BigArgs a{(const bf16*)A, (const bf16*)B, (bf16*)C, bias, (bf16*)aux, lda, ldb, ldc, ldaux, M, N, K, alpha, epi_scale};
+  BigArgs a{(const bf16*)A, (const bf16*)B, C, bias, (bf16*)aux, lda, ldb, ldc, ldaux, M, N, K, alpha, beta,
+            epi_scale, 0};
+  if (out_f32) {
+    if (a_kc || b_kc || epi != EPI_NONE || M < 256 || N < 256 || K < 4096 || ldc % 4) return 1;
+    const int tiles = ((M + TM - 1) / TM) * ((N + TN - 1) / TN);
+    // pick the split count that fills whole waves of the 256 CUs best (>= 2048-deep slices, slabs
+    // within the workspace): e.g. 36 tiles x 7 = 252 workgroups, 27 x 9 = 243, 9 x 28 = 252
+    int splits = 1;
+    double best = 0.0;
+    for (int s = 1; s <= 64; ++s) {
+      if (K / s < 2048 || (long)s * M * N * 4 > ws_bytes) break;
+      const int wg = tiles * s, waves = (wg + 255) / 256;
+      const double eff = (double)wg / (waves * 256.0) * (wg >= 192 ? 1.0 : wg / 192.0);
+      if (eff > best + 1e-3) { best = eff; splits = s; }
+    }
+    if (splits == 1) return launch_big<false, false, EPI_NONE, float>(a, 1, stream);
+    int ks = (K / splits + BK - 1) / BK * BK;
+    splits = (K + ks - 1) / ks;
+    a.C = workspace;
+    a.ksplit = ks;
+    const int st = launch_big<false, false, EPI_NONE, float>(a, splits, stream);
+    if (st) return st;
+    const long MN = (long)M * N;
+    hipLaunchKernelGGL(big_splitk_reduce, dim3((unsigned)((MN / 4 + 255) / 256)), dim3(256), 0, stream,
+                       (const float*)workspace, splits, MN, N, (float*)C, ldc, beta);
+    return (int)hipGetLastError();
+  }
+  if (!a_kc || M < 2048 || N < 256) return 1;
   if (b_kc) {
     switch (epi) {
-      case EPI_NONE: return launch_big<true, EPI_NONE>(a, stream);
-      case EPI_BIAS: return launch_big<true, EPI_BIAS>(a, stream);
-      case EPI_BIAS_GELU: return launch_big<true, EPI_BIAS_GELU>(a, stream);
-      case EPI_BIAS_RELU: return launch_big<true, EPI_BIAS_RELU>(a, stream);
-      case EPI_BIAS_TANH: return launch_big<true, EPI_BIAS_TANH>(a, stream);
+      case EPI_NONE: return launch_big<true, true, EPI_NONE, bf16>(a, 1, stream);
+      case EPI_BIAS: return launch_big<true, true, EPI_BIAS, bf16>(a, 1, stream);
+      case EPI_BIAS_GELU: return launch_big<true, true, EPI_BIAS_GELU, bf16>(a, 1, stream);
+      case EPI_BIAS_RELU: return launch_big<true, true, EPI_BIAS_RELU, bf16>(a, 1, stream);
+      case EPI_BIAS_TANH: return launch_big<true, true, EPI_BIAS_TANH, bf16>(a, 1, stream);
     }
   } else {
     switch (epi) {
-      case EPI_NONE: return launch_big<false, EPI_NONE>(a, stream);
-      case EPI_DGELU: return launch_big<false, EPI_DGELU>(a, stream);
-      case EPI_DRELU: return launch_big<false, EPI_DRELU>(a, stream);
-      case EPI_DTANH: return launch_big<false, EPI_DTANH>(a, stream);
+      case EPI_NONE: return launch_big<true, false, EPI_NONE, bf16>(a, 1, stream);
+      case EPI_DGELU: return launch_big<true, false, EPI_DGELU, bf16>(a, 1, stream);
+      case EPI_DRELU: return launch_big<true, false, EPI_DRELU, bf16>(a, 1, stream);
+      case EPI_DTANH: return launch_big<true, false, EPI_DTANH, bf16>(a, 1, stream);
     }
   }
   return 1;

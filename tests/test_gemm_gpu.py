@@ -187,3 +187,67 @@ def test_gemm_big_dgrad(epi, M, N, K):
     torch.cuda.synchronize()
     ref, _ = _ref_epi(dy.double() @ w.double(), epi, None, aux, 1.25)
     _check(out, ref, torch.bfloat16)
+
+
+@pytest.mark.parametrize("epi", ["bias", "bias_gelu", "bias_relu", "bias_tanh", "dgelu", "drelu", "dtanh", "none"])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_gemm_small_m_splitk_epilogues(dt, epi):
+    """Batch-row GEMMs (M = B) take split-K with the epilogue applied in the slab reduction."""
+    k = _k()
+    torch.manual_seed(10)
+    M, N, K = 256, 768, 2304
+    ws = torch.empty(8 << 20, device="cuda")
+    x = (torch.randn(M, K, device="cuda") * 0.2).to(dt)
+    if epi.startswith("bias") or epi == "none":
+        w = (torch.randn(N, K, device="cuda") * 0.2).to(dt)
+        b = torch.randn(N, device="cuda")
+        aux = torch.empty(M, N, device="cuda", dtype=dt) if epi == "bias_gelu" else None
+        out = torch.empty(M, N, device="cuda", dtype=dt)
+        k.gemm(x, w, out, M=M, N=N, K=K, a_kc=1, b_kc=1, lda=K, ldb=K, ldc=N, epi=epi, bias=b if epi != "none" else None,
+               aux=aux, ldaux=N, workspace=ws)
+        torch.cuda.synchronize()
+        ref, pre = _ref_epi(x.double() @ w.double().t(), epi, b, None, 1.0)
+        _check(out, ref, dt)
+        if pre is not None:
+            _check(aux, pre, dt)
+    else:
+        w = (torch.randn(K, N, device="cuda") * 0.2).to(dt)
+        aux = torch.randn(M, N, device="cuda").to(dt)
+        if epi == "dtanh":
+            aux = torch.tanh(aux.float()).to(dt)
+        out = torch.empty(M, N, device="cuda", dtype=dt)
+        k.gemm(x, w, out, M=M, N=N, K=K, a_kc=1, b_kc=0, lda=K, ldb=N, ldc=N, epi=epi, aux=aux, ldaux=N,
+               epi_scale=1.25, workspace=ws)
+        torch.cuda.synchronize()
+        ref, _ = _ref_epi(x.double() @ w.double(), epi, None, aux, 1.25)
+        _check(out, ref, dt)
+
+
+@pytest.mark.parametrize("M,N,K", [(2304, 768, 65536), (768, 3072, 16384), (768, 768, 8192)])
+def test_gemm_big_wgrad_splitk(M, N, K):
+    """Weight gradients on the 256x256 kernel (k-major A and B), split-K slabs, beta accumulate."""
+    k = _k()
+    torch.manual_seed(11)
+    dy = torch.randn(K, M, device="cuda").to(torch.bfloat16)
+    x = torch.randn(K, N, device="cuda").to(torch.bfloat16)
+    dw = torch.randn(M, N, device="cuda")
+    ref = dw.double() + dy.double().t() @ x.double()
+    ws = torch.empty(24 << 20, device="cuda")
+    k.gemm(dy, x, dw, M=M, N=N, K=K, a_kc=0, b_kc=0, lda=M, ldb=N, ldc=N, beta=1.0, workspace=ws)
+    torch.cuda.synchronize()
+    err = ((dw.double() - ref).abs().max() / ref.abs().max()).item()
+    assert err <= 2e-3, err
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 768, 3072), (4096, 2304, 768)])
+def test_gemm_big_dgrad_beta(M, N, K):
+    """Input gradient accumulated onto the residual gradient (beta = 1) on the 256x256 kernel."""
+    k = _k()
+    torch.manual_seed(12)
+    dy = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(K, N, device="cuda") * 0.1).to(torch.bfloat16)
+    c = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+    ref = c.double() + dy.double() @ w.double()
+    k.linear_dgrad(dy, w, out=c, beta=1.0)
+    torch.cuda.synchronize()
+    _check(c, ref, torch.bfloat16)
