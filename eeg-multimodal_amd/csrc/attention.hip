@@ -7,7 +7,9 @@
 // Forward: grid (L/128, H, B), 8 waves x 16 queries.  S^T = K Q^T is computed "swapped" so the
 // accumulator of S^T is directly the B operand of O^T = V^T P^T (k order permuted consistently,
 // V^T read with ds_read_b64_tr_b16).  K/V tiles of 64 keys staged through LDS; online softmax.
-// Stores LSE (natural log, scaled-score units) for the backward.
+// Stores LSE (natural log, scaled-score units) for the backward.  Attention-probability dropout
+// (eager_attention_forward dropout(attn_weights), modeling_bert.py:131,198) is applied to P before PV with
+// a Philox mask regenerated in the backward.
 // Backward: grid (L/256, H, B), 8 waves x 32 keys; per 32-query chunk: S, P (from LSE), dP,
 // dS = P (dP - rowsum(dO o O)); dV += P^T dO and dK += dS^T Q accumulate in registers; dS goes
 // through LDS once for dQ = dS K.  With L <= 256 every dQ element is produced by exactly one
@@ -26,7 +28,47 @@ struct AttnArgs {
   const void* qkv; void* out; float* lse; const float* kbias;
   const void* o; const void* dout; void* dqkv; float* dq_acc;
   int B, H, L; long ld_qkv, ld_out; float scale;
+  float p; uint64_t seed, offset;   // attention-probability dropout (p = 0: off)
 };
+
+// Dropout mask of the probabilities P[q][key] of head (b,h): element ((b*H+h)*L + q)*L + key of
+// the site's keep_bits8 stream (common.h), so forward and backward agree.
+DEV uint64_t attn_elem(const AttnArgs& a, int b, int h, long q, long key) {
+  return (((uint64_t)b * a.H + h) * a.L + q) * a.L + key;
+}
+// Forward layout: lane (g, li) needs keys 16f+4g..16f+4g+3 (f = 0..3) of query q: nibble (g&1) of
+// the call for key octet 2f + (g>>1).  Lanes g and g^1 (16 apart) need the same 4 calls: each
+// draws two (f = 2(g&1), 2(g&1)+1) and swaps the partner's nibbles with one shuffle.
+DEV void attn_mask_fwd(const AttnArgs& a, int b, int h, long q, long k0, int g, uint32_t thr, uint32_t (&nib)[4]) {
+  const int par = g & 1;
+  uint32_t mine[2], give = 0;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int f = 2 * par + t;
+    const uint32_t bits = keep_bits8(a.seed, a.offset, attn_elem(a, b, h, q, k0 + 16 * f + 8 * (g >> 1)) >> 3, thr);
+    mine[t] = (bits >> (4 * par)) & 0xFu;
+    give |= ((bits >> (4 * (par ^ 1))) & 0xFu) << (4 * t);
+  }
+  const uint32_t got = (uint32_t)__shfl_xor((int)give, 16, 64);
+  nib[2 * par] = mine[0];
+  nib[2 * par + 1] = mine[1];
+  nib[2 * (par ^ 1)] = got & 0xFu;
+  nib[2 * (par ^ 1) + 1] = (got >> 4) & 0xFu;
+}
+// Backward layout: lane (g, li) needs mask[q0 + 16qf + 4g + r][kb + li] for qf = 0,1, r = 0..3.
+// Lane (g, m = li>>3, s = li&7) draws the key-octet-m row of query q0 + 16(s>>2) + 4g + (s&3); the
+// 8 lanes of the octet then gather bit (li&7) of each other's rows.
+DEV void attn_mask_bwd(const AttnArgs& a, int b, int h, long q0, long kb, int lane, uint32_t thr, uint32_t& m8) {
+  const int g = lane >> 4, li = lane & 15, mo = li >> 3, s = li & 7;
+  const uint32_t row = keep_bits8(a.seed, a.offset,
+                                  attn_elem(a, b, h, q0 + 16 * (s >> 2) + 4 * g + (s & 3), kb + 8 * mo) >> 3, thr);
+  m8 = 0;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const uint32_t rt = (uint32_t)__shfl((int)row, (lane & ~7) | t, 64);
+    m8 |= ((rt >> s) & 1u) << t;               // bit t <-> (qf = t>>2, r = t&3)
+  }
+}
 
 // Cooperative copy of `rows` x 64 elements (row stride `ld` in global) into LDS [rows][64+pad].
 template <typename T, int NTHR>
@@ -63,6 +105,8 @@ __global__ void __launch_bounds__(512) attn_fwd_kernel(AttnArgs a) {
   for (int e = 0; e < 4; ++e) o[e] = f32x4{0, 0, 0, 0};
   float m = NEG, l = 0.f;
   const float* kb = a.kbias ? a.kbias + (long)b * a.L : nullptr;
+  const uint32_t thr = thr16_of(a.p);
+  const float dscale = 1.0f / (1.0f - a.p);
 
   for (int k0 = 0; k0 < a.L; k0 += KT) {
     __syncthreads();
@@ -100,6 +144,14 @@ __global__ void __launch_bounds__(512) attn_fwd_kernel(AttnArgs a) {
     l = l * alpha + ps;
 #pragma unroll
     for (int e = 0; e < 4; ++e) o[e] *= alpha;
+    if (a.p > 0.f) {   // O accumulates dropout(P) V; the normaliser l stays the undropped sum
+      uint32_t nib[4];
+      attn_mask_fwd(a, b, h, q, k0, g, thr, nib);
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[f][r] = (nib[f] >> r) & 1u ? s[f][r] * dscale : 0.f;
+    }
     // O^T[d, q] += sum_key V[key, d] P[q, key]   (k order: {4g..4g+3 of frag 2c, of frag 2c+1})
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
@@ -147,6 +199,8 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(AttnArgs a) {
   const float* lse = a.lse + ((long)b * a.H + h) * a.L;
   const float* kbias = a.kbias ? a.kbias + (long)b * a.L : nullptr;
   const int nkb = a.L / KB;
+  const uint32_t thr = thr16_of(a.p);
+  const float dscale = 1.0f / (1.0f - a.p);
 
   // this wave's K and V as B operands (key = column): lane holds [key kw0+16f+li][d 32c+8g..]
   F kf[2][2], vf[2][2];
@@ -188,6 +242,11 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(AttnArgs a) {
     __syncthreads();
     // S = Q K^T and dP = dO V^T : rows = queries (4g+r within q-frag), cols = keys (li)
     f32x4 p[2][2], ds[2][2];
+    uint32_t m8[2] = {0xFFu, 0xFFu};
+    if (a.p > 0.f) {
+#pragma unroll
+      for (int f = 0; f < 2; ++f) attn_mask_bwd(a, b, h, q0, kw0 + 16 * f, lane, thr, m8[f]);
+    }
 #pragma unroll
     for (int qf = 0; qf < 2; ++qf) {
       F qa[2], da[2];
@@ -204,12 +263,14 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(AttnArgs a) {
           s = mma16(qa[c], kf[f][c], s);
           dp = mma16(da[c], vf[f][c], dp);
         }
+        // with dropout Z: O = (P o Z) V, so dV uses P o Z and dP = Z o (dO V^T); D = rowsum(dO o O)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int qi = 16 * qf + 4 * g + r;
           const float pv = __expf(s[r] * a.scale + kbv[f] - lse_s[qi]);
-          s[r] = pv;
-          dp[r] = pv * (dp[r] - dd_s[qi]);
+          const float mk = (m8[f] >> (4 * qf + r)) & 1u ? dscale : 0.f;
+          s[r] = pv * mk;
+          dp[r] = pv * (dp[r] * mk - dd_s[qi]);
         }
         p[qf][f] = s;
         ds[qf][f] = dp;
@@ -278,11 +339,13 @@ __global__ void dq_convert_kernel(const float* dq_acc, void* dqkv, int is_bf16, 
 }  // namespace
 
 extern "C" int eegf_attn_fwd(int dtype, int B, int H, int L, const void* qkv, long ld_qkv, const float* key_bias,
-                             float scale, void* out, long ld_out, float* lse, hipStream_t stream) {
+                             float scale, float drop_p, unsigned long long seed, unsigned long long offset,
+                             void* out, long ld_out, float* lse, hipStream_t stream) {
   if (B <= 0 || H != 12 || L <= 0 || L % 128 != 0 || !qkv || !out || !lse || ld_qkv < 2304 || ld_out < 768)
     return EEGF_ERR_ARG;
-  if (B > 65535) return EEGF_ERR_ARG;
-  AttnArgs a{qkv, out, lse, key_bias, nullptr, nullptr, nullptr, nullptr, B, H, L, ld_qkv, ld_out, scale};
+  if (B > 65535 || drop_p < 0.f || drop_p >= 1.f) return EEGF_ERR_ARG;
+  AttnArgs a{qkv, out, lse, key_bias, nullptr, nullptr, nullptr, nullptr, B, H, L, ld_qkv, ld_out, scale,
+             drop_p, seed, offset};
   const dim3 grid(L / 128, H, B);
   if (dtype == EEGF_F32) hipLaunchKernelGGL(attn_fwd_kernel<float>, grid, dim3(512), 0, stream, a);
   else if (dtype == EEGF_BF16) hipLaunchKernelGGL(attn_fwd_kernel<bf16>, grid, dim3(512), 0, stream, a);
@@ -293,14 +356,15 @@ extern "C" int eegf_attn_fwd(int dtype, int B, int H, int L, const void* qkv, lo
 extern "C" long eegf_attn_bwd_workspace(int B, int L) { return L > 256 ? (long)B * L * 768 : 0; }
 
 extern "C" int eegf_attn_bwd(int dtype, int B, int H, int L, const void* qkv, long ld_qkv, const float* key_bias,
-                             float scale, const void* out, const void* dout, long ld_out, const float* lse,
+                             float scale, float drop_p, unsigned long long seed, unsigned long long offset,
+                             const void* out, const void* dout, long ld_out, const float* lse,
                              void* dqkv, float* dq_workspace, hipStream_t stream) {
   if (B <= 0 || H != 12 || L <= 0 || L % 256 != 0 || !qkv || !out || !dout || !lse || !dqkv) return EEGF_ERR_ARG;
-  if (ld_qkv < 2304 || ld_out < 768 || B > 65535) return EEGF_ERR_ARG;
+  if (ld_qkv < 2304 || ld_out < 768 || B > 65535 || drop_p < 0.f || drop_p >= 1.f) return EEGF_ERR_ARG;
   if (L > 256 && !dq_workspace) return EEGF_ERR_ARG;
   if (L > 256) hipMemsetAsync(dq_workspace, 0, sizeof(float) * (size_t)B * L * 768, stream);
   AttnArgs a{qkv, nullptr, const_cast<float*>(lse), key_bias, out, dout, dqkv, dq_workspace, B, H, L, ld_qkv, ld_out,
-             scale};
+             scale, drop_p, seed, offset};
   const dim3 grid(L / 256, H, B);
   if (dtype == EEGF_F32) hipLaunchKernelGGL(attn_bwd_kernel<float>, grid, dim3(512), 0, stream, a);
   else if (dtype == EEGF_BF16) hipLaunchKernelGGL(attn_bwd_kernel<bf16>, grid, dim3(512), 0, stream, a);

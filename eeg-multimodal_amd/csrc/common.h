@@ -156,9 +156,10 @@ DEV uint32_t mulhilo(uint32_t a, uint32_t b, uint32_t* hi) {
   *hi = (uint32_t)(p >> 32);
   return (uint32_t)p;
 }
-DEV u32x4s philox4x32(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
+template <int ROUNDS>
+DEV u32x4s philox4x32_r(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
 #pragma unroll
-  for (int r = 0; r < 10; ++r) {
+  for (int r = 0; r < ROUNDS; ++r) {
     uint32_t hi0, hi1;
     uint32_t lo0 = mulhilo(0xD2511F53u, c0, &hi0);
     uint32_t lo1 = mulhilo(0xCD9E8D57u, c2, &hi1);
@@ -168,5 +169,43 @@ DEV u32x4s philox4x32(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32
   }
   return {c0, c1, c2, c3};
 }
+DEV u32x4s philox4x32(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
+  return philox4x32_r<10>(c0, c1, c2, c3, k0, k1);
+}
 // uniform in (0, 1]: (x + 1) * 2^-32 with x in [0, 2^32)  → never exactly 0
 DEV float u01_open0(uint32_t x) { return ((float)(x >> 8) + 1.0f) * (1.0f / 16777216.0f); }
+
+// Dropout keep-mask, shared by every dropout site: element e of a site keyed (seed, offset) is kept
+// iff word (e & 3) of philox(e >> 2, offset; seed) >= p * 2^32; kept elements scale by 1/(1-p).
+// drop_mask4 returns the 4 consecutive elements 4*e4 .. 4*e4+3.
+DEV void drop_mask4(uint64_t seed, uint64_t offset, uint64_t e4, float p, float (&m)[4]) {
+  const u32x4s r = philox4x32((uint32_t)e4, (uint32_t)(e4 >> 32), (uint32_t)offset, (uint32_t)(offset >> 32),
+                              (uint32_t)seed, (uint32_t)(seed >> 32));
+  const float scale = 1.0f / (1.0f - p);
+  const uint32_t thr = (uint32_t)fminf(p * 4294967296.0f, 4294967295.0f);
+  m[0] = r.x >= thr ? scale : 0.f;
+  m[1] = r.y >= thr ? scale : 0.f;
+  m[2] = r.z >= thr ? scale : 0.f;
+  m[3] = r.w >= thr ? scale : 0.f;
+}
+// Attention-probability stream (L^2 draws per head, the only site where the draw cost shows):
+// Philox4x32-7 (Random123: BigCrush-clean at 7 rounds), eight 16-bit draws per call.  Element e
+// is kept iff halfword (e & 7) of philox7(e >> 3, offset; seed) >= thr16 = (uint32)(p * 65536)
+// (halfword k = bits 16*(k&1).. of word k>>1).  Returns the 8 keep bits (bit k = element 8c+k).
+DEV uint32_t keep_bits8(uint64_t seed, uint64_t offset, uint64_t call, uint32_t thr16) {
+  const u32x4s r = philox4x32_r<7>((uint32_t)call, (uint32_t)(call >> 32), (uint32_t)offset,
+                                   (uint32_t)(offset >> 32), (uint32_t)seed, (uint32_t)(seed >> 32));
+  const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+  uint32_t bits = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) bits |= (uint32_t)(((w[k >> 1] >> (16 * (k & 1))) & 0xFFFFu) >= thr16) << k;
+  return bits;
+}
+DEV uint32_t thr16_of(float p) { return (uint32_t)fminf(p * 65536.0f, 65535.0f); }
+
+DEV float drop_mask1(uint64_t seed, uint64_t offset, uint64_t e, float p) {
+  float m[4];
+  drop_mask4(seed, offset, e >> 2, p, m);
+  const int k = (int)(e & 3);
+  return k == 0 ? m[0] : k == 1 ? m[1] : k == 2 ? m[2] : m[3];
+}

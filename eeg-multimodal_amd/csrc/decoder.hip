@@ -5,229 +5,312 @@
 // model.py:40-43 with tgt = the single action token.  The memory K/V projections are never
 // materialised: for head h with projected query q_h,
 //     score_j = q_h . (Wk_h M_j + bk_h) / 8 = q'_h . M_j + const,   q'_h = Wk_h^T q_h / 8
-//     ctx_h   = sum_j p_j (Wv_h M_j + bv_h) = Wv_h c_h + bv_h,        c_h = sum_j p_j M_j
-// (the constant q_h.bk_h/8 cancels in the softmax).  These kernels compute p and c_h (forward) and
-// dM, dq' (backward) by streaming M once or twice; the q', Wv c and projection GEMMs are eegf_gemm.
-// One workgroup per batch row b; HBM-bound on M (S x 768 per row).
+//     ctx_h   = sum_j p~_j (Wv_h M_j + bv_h) = Wv_h c_h + s_h bv_h,   c_h = sum_j p~_j M_j
+// where p~ = dropout(p) (attention-probability dropout, F.multi_head_attention_forward dropout_p)
+// and s_h = sum_j p~_j (1 without dropout).  The constant q_h.bk_h/8 cancels in the softmax.
+//
+// Kernels (HBM-bound on the memory M = [B, S, 768] in the encoder dtype):
+//   xrow_dot   lane = one memory row j: out[b,h,j] = v[b,h,:] . M[b,j,:]   (v uniform → scalar loads)
+//              forward: raw scores (v = q');  backward: dp~ (v = dc)
+//   xctx       per (b, 256-column slab): softmax over j (recomputed per workgroup from the raw
+//              scores), dropout, then c[h, cols] = sum_j p~[h][j] M[j][cols]; 4 waves split j
+//   xbwd_cols  per (b, 256-column slab): softmax backward, then in one pass over M:
+//              dq'[h, cols] = sum_j dsc[h][j] M[j][cols],  dM[j][cols] = sum_h p~ dc + dsc q'
+// The q'/Wv/out-proj GEMMs are eegf_gemm; the s_h bv_h term is eegf_head_bias_fwd/bwd.
 #include "common.h"
 #include "eegfusion_internal.h"
 
 namespace {
 
-constexpr int E = 768, NH = 12, NCOL = 12;  // columns per lane: 768 / 64
+constexpr int E = 768, NH = 12, SLAB = 256;
 
-template <typename T>
-DEV void load_row12(const T* row, int lane, float (&v)[NCOL]) {
+template <typename T> DEV void load4(const T* p, float (&v)[4]);
+template <> DEV void load4<float>(const float* p, float (&v)[4]) {
+  const float4 x = *(const float4*)p;
+  v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+}
+template <> DEV void load4<bf16>(const bf16* p, float (&v)[4]) {
+  const bf16x4 x = *(const bf16x4*)p;
+  v[0] = (float)x[0]; v[1] = (float)x[1]; v[2] = (float)x[2]; v[3] = (float)x[3];
+}
+template <typename T> DEV void store4(T* p, const float (&v)[4]);
+template <> DEV void store4<float>(float* p, const float (&v)[4]) { *(float4*)p = float4{v[0], v[1], v[2], v[3]}; }
+template <> DEV void store4<bf16>(bf16* p, const float (&v)[4]) {
+  bf16x4 o;
+  o[0] = (bf16)v[0]; o[1] = (bf16)v[1]; o[2] = (bf16)v[2]; o[3] = (bf16)v[3];
+  *(bf16x4*)p = o;
+}
+
+// out[b,h,j] = vec[b,h,:] . M[b,j,:] (+ kbias[b,j]); grid (ceil(S/64), B), 64 threads.
+template <typename T, typename TV>
+__global__ void __launch_bounds__(64) xrow_dot_kernel(const T* __restrict__ mem, const TV* __restrict__ vec,
+                                                      const float* __restrict__ kbias, int S, float* __restrict__ out) {
+  const int b = blockIdx.y, j = blockIdx.x * 64 + threadIdx.x;
+  const int jr = j < S ? j : S - 1;
+  const T* row = mem + ((long)b * S + jr) * E;
+  const TV* v = vec + (long)b * NH * E;
+  float acc[NH];
 #pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const int col = (lane + 64 * i) * 4;
+  for (int h = 0; h < NH; ++h) acc[h] = 0.f;
+#pragma unroll 1
+  for (int c = 0; c < E; c += 4) {       // 4 columns x 12 heads of v per step: 48 scalar registers
+    float m[4];
+    load4<T>(row + c, m);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) v[4 * i + e] = to_f32(row[col + e]);
+    for (int h = 0; h < NH; ++h)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[h] += m[e] * to_f32(v[h * E + c + e]);
+  }
+  if (j < S) {
+    const float kb = kbias ? kbias[(long)b * S + j] : 0.f;
+#pragma unroll
+    for (int h = 0; h < NH; ++h) out[((long)b * NH + h) * S + j] = acc[h] + kb;
   }
 }
-DEV int col_of(int lane, int k) { return (lane + 64 * (k >> 2)) * 4 + (k & 3); }
 
-// ---- forward: scores, softmax (saved), context c[b,h,:] ----
-template <typename T, typename TQ>
-__global__ void __launch_bounds__(256) xattn_fwd_kernel(const T* __restrict__ mem, const TQ* __restrict__ qp,
-                                                        const float* __restrict__ kbias, int S, float* __restrict__ probs,
-                                                        TQ* __restrict__ ctx) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* qs = sm;               // [NH][E]
-  float* ps = sm + NH * E;      // [NH][S]
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const T* M = mem + (long)b * S * E;
-  for (int i = tid; i < NH * E; i += 256) qs[i] = to_f32(qp[(long)b * NH * E + i]);
-  __syncthreads();
-  float qreg[NH][NCOL];
-#pragma unroll
-  for (int h = 0; h < NH; ++h)
-#pragma unroll
-    for (int k = 0; k < NCOL; ++k) qreg[h][k] = qs[h * E + col_of(lane, k)];
-  // phase 1: raw scores
-  for (int j = wave; j < S; j += 4) {
-    float m[NCOL];
-    load_row12(M + (long)j * E, lane, m);
-#pragma unroll
-    for (int h = 0; h < NH; ++h) {
-      float acc = 0.f;
-#pragma unroll
-      for (int k = 0; k < NCOL; ++k) acc += m[k] * qreg[h][k];
-      acc = wave_sum(acc);
-      if (lane == 0) ps[h * S + j] = acc + (kbias ? kbias[(long)b * S + j] : 0.f);
-    }
-  }
-  __syncthreads();
-  // phase 2: softmax over j per head (wave w: heads w, w+4, w+8)
+// Softmax (+dropout) of the 12 raw score rows of batch row b into LDS pt[S][12] (p~);
+// workgroup slab 0 also stores the undropped p (for the backward) and s_h = sum_j p~.
+DEV void softmax_rows(const float* __restrict__ raw, int S, int b, float p_drop, uint64_t seed, uint64_t offset,
+                      bool write, float* __restrict__ probs, float* __restrict__ psum, float* pt) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   for (int h = wave; h < NH; h += 4) {
+    const float* r = raw + ((long)b * NH + h) * S;
     float mx = -3.0e38f;
-    for (int j = lane; j < S; j += 64) mx = fmaxf(mx, ps[h * S + j]);
+    for (int j = lane; j < S; j += 64) mx = fmaxf(mx, r[j]);
     mx = wave_max(mx);
     float sum = 0.f;
-    for (int j = lane; j < S; j += 64) { const float e = __expf(ps[h * S + j] - mx); ps[h * S + j] = e; sum += e; }
+    for (int j = lane; j < S; j += 64) { const float e = __expf(r[j] - mx); pt[j * NH + h] = e; sum += e; }
     const float inv = 1.0f / wave_sum(sum);
+    float ds = 0.f;
     for (int j = lane; j < S; j += 64) {
-      const float p = ps[h * S + j] * inv;
-      ps[h * S + j] = p;
-      probs[((long)b * NH + h) * S + j] = p;
+      const float p = pt[j * NH + h] * inv;
+      if (write) probs[((long)b * NH + h) * S + j] = p;
+      const float pd = p_drop > 0.f ? p * drop_mask1(seed, offset, ((uint64_t)b * NH + h) * S + j, p_drop) : p;
+      pt[j * NH + h] = pd;
+      ds += pd;
     }
+    ds = wave_sum(ds);
+    if (write && psum && lane == 0) psum[b * NH + h] = ds;
   }
-  __syncthreads();
-  // phase 3: c[h][col] = sum_j p[h][j] M[j][col]; wave w owns columns [192w, 192w+192), 3 per lane
-  float acc[NH][3];
-#pragma unroll
-  for (int h = 0; h < NH; ++h)
-#pragma unroll
-    for (int k = 0; k < 3; ++k) acc[h][k] = 0.f;
-  const int c0 = wave * 192 + lane;
-  for (int j = 0; j < S; ++j) {
-    const T* row = M + (long)j * E + c0;
-    const float m0 = to_f32(row[0]), m1 = to_f32(row[64]), m2 = to_f32(row[128]);
-#pragma unroll
-    for (int h = 0; h < NH; ++h) {
-      const float p = ps[h * S + j];
-      acc[h][0] += p * m0; acc[h][1] += p * m1; acc[h][2] += p * m2;
-    }
-  }
-#pragma unroll
-  for (int h = 0; h < NH; ++h)
-#pragma unroll
-    for (int k = 0; k < 3; ++k) ctx[((long)b * NH + h) * E + c0 + 64 * k] = from_f32<TQ>(acc[h][k]);
 }
 
-// ---- backward ----
-// dp[h][j] = dc[h].M[j];  dsc = p (dp - sum_j p dp);  dq'[h] = sum_j dsc[h][j] M[j];
-// dM[j] (+)= sum_h p[h][j] dc[h] + dsc[h][j] q'[h]
+DEV void lds_row12(const float* base, float (&v)[NH]) {
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float4 x = *(const float4*)(base + 4 * k);
+    v[4 * k] = x.x; v[4 * k + 1] = x.y; v[4 * k + 2] = x.z; v[4 * k + 3] = x.w;
+  }
+}
+
+// grid (E/256, B), 256 threads: lane owns 4 columns of the slab, wave w rows [w*S/4, (w+1)*S/4).
 template <typename T, typename TQ>
-__global__ void __launch_bounds__(256) xattn_bwd_kernel(const T* __restrict__ mem, const TQ* __restrict__ qp,
-                                                        const float* __restrict__ probs, const TQ* __restrict__ dc, int S,
+__global__ void __launch_bounds__(256) xctx_kernel(const T* __restrict__ mem, const float* __restrict__ raw, int S,
+                                                   float p_drop, uint64_t seed, uint64_t offset,
+                                                   float* __restrict__ probs, float* __restrict__ psum,
+                                                   TQ* __restrict__ ctx) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* pt = sm;                       // [S][12]
+  float* red = sm + S * NH;             // [4][12][256]
+  const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  softmax_rows(raw, S, b, p_drop, seed, offset, blockIdx.x == 0, probs, psum, pt);
+  __syncthreads();
+  const int col = blockIdx.x * SLAB + lane * 4;
+  float acc[NH][4];
+#pragma unroll
+  for (int h = 0; h < NH; ++h)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc[h][e] = 0.f;
+  const int per = (S + 3) / 4, j0 = wave * per, j1 = min(S, j0 + per);
+  const T* M = mem + (long)b * S * E + col;
+#pragma unroll 2
+  for (int j = j0; j < j1; ++j) {
+    float m[4], p[NH];
+    load4<T>(M + (long)j * E, m);
+    lds_row12(pt + j * NH, p);
+#pragma unroll
+    for (int h = 0; h < NH; ++h)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[h][e] += p[h] * m[e];
+  }
+#pragma unroll
+  for (int h = 0; h < NH; ++h)
+    *(float4*)(red + (wave * NH + h) * SLAB + lane * 4) = float4{acc[h][0], acc[h][1], acc[h][2], acc[h][3]};
+  __syncthreads();
+  // 12 heads x 256 columns = 3072 outputs, 12 per thread
+  for (int i = tid; i < NH * SLAB; i += 256) {
+    const int h = i / SLAB, c = i % SLAB;
+    const float v = red[(0 * NH + h) * SLAB + c] + red[(1 * NH + h) * SLAB + c] + red[(2 * NH + h) * SLAB + c] +
+                    red[(3 * NH + h) * SLAB + c];
+    ctx[((long)b * NH + h) * E + blockIdx.x * SLAB + c] = from_f32<TQ>(v);
+  }
+}
+
+// Backward, grid (E/256, B), 256 threads.  raw = dc . M_j (xrow_dot); dpsum[b,h] = dL/ds_h.
+//   dp~ = raw + dpsum;  dp = dp~ * mask;  dsc = p (dp - sum_j p dp)
+//   dq'[h,c] = sum_j dsc[h][j] M[j][c];   dM[j][c] (+)= sum_h p~[h][j] dc[h][c] + dsc[h][j] q'[h][c]
+template <typename T, typename TQ>
+__global__ void __launch_bounds__(256) xbwd_cols_kernel(const T* __restrict__ mem, const TQ* __restrict__ qp,
+                                                        const float* __restrict__ probs, const float* __restrict__ raw,
+                                                        const float* __restrict__ dpsum, const TQ* __restrict__ dc, int S,
+                                                        float p_drop, uint64_t seed, uint64_t offset,
                                                         T* __restrict__ dmem, float beta, TQ* __restrict__ dqp) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* qs = sm;                  // [NH][E] q'
-  float* dcs = qs + NH * E;        // [NH][E] dc
-  float* ps = dcs + NH * E;        // [NH][S] p
-  float* dss = ps + NH * S;        // [NH][S] dp -> dsc
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const T* M = mem + (long)b * S * E;
-  for (int i = tid; i < NH * E; i += 256) {
-    qs[i] = to_f32(qp[(long)b * NH * E + i]);
-    dcs[i] = to_f32(dc[(long)b * NH * E + i]);
-  }
-  for (int i = tid; i < NH * S; i += 256) ps[i] = probs[(long)b * NH * S + i];
-  __syncthreads();
-  {
-    float dreg[NH][NCOL];
-#pragma unroll
-    for (int h = 0; h < NH; ++h)
-#pragma unroll
-      for (int k = 0; k < NCOL; ++k) dreg[h][k] = dcs[h * E + col_of(lane, k)];
-    for (int j = wave; j < S; j += 4) {
-      float m[NCOL];
-      load_row12(M + (long)j * E, lane, m);
-#pragma unroll
-      for (int h = 0; h < NH; ++h) {
-        float acc = 0.f;
-#pragma unroll
-        for (int k = 0; k < NCOL; ++k) acc += m[k] * dreg[h][k];
-        acc = wave_sum(acc);
-        if (lane == 0) dss[h * S + j] = acc;
-      }
-    }
-  }
-  __syncthreads();
+  float* pt = sm;                 // [S][12] p~
+  float* st = sm + S * NH;        // [S][12] dsc
+  float* red = st + S * NH;       // [4][12][256]
+  const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   for (int h = wave; h < NH; h += 4) {
+    const float* pr = probs + ((long)b * NH + h) * S;
+    const float* dr = raw + ((long)b * NH + h) * S;
+    const float dsh = dpsum ? dpsum[b * NH + h] : 0.f;
     float dot = 0.f;
-    for (int j = lane; j < S; j += 64) dot += ps[h * S + j] * dss[h * S + j];
+    for (int j = lane; j < S; j += 64) {
+      const float mk = p_drop > 0.f ? drop_mask1(seed, offset, ((uint64_t)b * NH + h) * S + j, p_drop) : 1.f;
+      const float p = pr[j], dp = (dr[j] + dsh) * mk;
+      pt[j * NH + h] = p * mk;
+      st[j * NH + h] = dp;
+      dot += p * dp;
+    }
     dot = wave_sum(dot);
-    for (int j = lane; j < S; j += 64) dss[h * S + j] = ps[h * S + j] * (dss[h * S + j] - dot);
+    for (int j = lane; j < S; j += 64) st[j * NH + h] = pr[j] * (st[j * NH + h] - dot);
   }
   __syncthreads();
-  // dq'[h][col] = sum_j dsc[h][j] M[j][col]  (wave-owned column slices, as the forward context)
-  {
-    float acc[NH][3];
+  const int col = blockIdx.x * SLAB + lane * 4;
+  float qr[NH][4], dcr[NH][4], acc[NH][4];
 #pragma unroll
-    for (int h = 0; h < NH; ++h)
+  for (int h = 0; h < NH; ++h) {
+    load4<TQ>(qp + ((long)b * NH + h) * E + col, qr[h]);
+    load4<TQ>(dc + ((long)b * NH + h) * E + col, dcr[h]);
 #pragma unroll
-      for (int k = 0; k < 3; ++k) acc[h][k] = 0.f;
-    const int c0 = wave * 192 + lane;
-    for (int j = 0; j < S; ++j) {
-      const T* row = M + (long)j * E + c0;
-      const float m0 = to_f32(row[0]), m1 = to_f32(row[64]), m2 = to_f32(row[128]);
-#pragma unroll
-      for (int h = 0; h < NH; ++h) {
-        const float d = dss[h * S + j];
-        acc[h][0] += d * m0; acc[h][1] += d * m1; acc[h][2] += d * m2;
-      }
-    }
-#pragma unroll
-    for (int h = 0; h < NH; ++h)
-#pragma unroll
-      for (int k = 0; k < 3; ++k) dqp[((long)b * NH + h) * E + c0 + 64 * k] = from_f32<TQ>(acc[h][k]);
+    for (int e = 0; e < 4; ++e) acc[h][e] = 0.f;
   }
-  // dM[j][col] = sum_h p[h][j] dc[h][col] + dsc[h][j] q'[h][col]; each thread owns 3 columns
-  {
-    const int c0 = tid;  // columns tid, tid+256, tid+512
-    float dcr[NH][3], qr[NH][3];
+  const int per = (S + 3) / 4, j0 = wave * per, j1 = min(S, j0 + per);
+  const T* M = mem + (long)b * S * E + col;
+  T* dM = dmem + (long)b * S * E + col;
+  for (int j = j0; j < j1; ++j) {
+    float m[4], p[NH], d[NH], o[4] = {0.f, 0.f, 0.f, 0.f};
+    load4<T>(M + (long)j * E, m);
+    lds_row12(pt + j * NH, p);
+    lds_row12(st + j * NH, d);
 #pragma unroll
     for (int h = 0; h < NH; ++h)
 #pragma unroll
-      for (int k = 0; k < 3; ++k) { dcr[h][k] = dcs[h * E + c0 + 256 * k]; qr[h][k] = qs[h * E + c0 + 256 * k]; }
-    T* dM = dmem + (long)b * S * E;
-    for (int j = 0; j < S; ++j) {
-      float o[3] = {0.f, 0.f, 0.f};
-#pragma unroll
-      for (int h = 0; h < NH; ++h) {
-        const float p = ps[h * S + j], d = dss[h * S + j];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) o[k] += p * dcr[h][k] + d * qr[h][k];
+      for (int e = 0; e < 4; ++e) {
+        acc[h][e] += d[h] * m[e];
+        o[e] += p[h] * dcr[h][e] + d[h] * qr[h][e];
       }
+    if (beta != 0.f) {
+      float old[4];
+      load4<T>(dM + (long)j * E, old);
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        T* dst = dM + (long)j * E + c0 + 256 * k;
-        *dst = from_f32<T>(beta != 0.f ? o[k] + beta * to_f32(*dst) : o[k]);
-      }
+      for (int e = 0; e < 4; ++e) o[e] += beta * old[e];
     }
+    store4<T>(dM + (long)j * E, o);
   }
+#pragma unroll
+  for (int h = 0; h < NH; ++h)
+    *(float4*)(red + (wave * NH + h) * SLAB + lane * 4) = float4{acc[h][0], acc[h][1], acc[h][2], acc[h][3]};
+  __syncthreads();
+  for (int i = tid; i < NH * SLAB; i += 256) {
+    const int h = i / SLAB, c = i % SLAB;
+    const float v = red[(0 * NH + h) * SLAB + c] + red[(1 * NH + h) * SLAB + c] + red[(2 * NH + h) * SLAB + c] +
+                    red[(3 * NH + h) * SLAB + c];
+    dqp[((long)b * NH + h) * E + blockIdx.x * SLAB + c] = from_f32<TQ>(v);
+  }
+}
+
+// x[b, c] += bias[c] * s[b, c / group]   (the s_h bv_h term of the dropped-out context)
+__global__ void __launch_bounds__(256) head_bias_fwd_kernel(int B, int W, int group, float* __restrict__ x,
+                                                            const float* __restrict__ bias, const float* __restrict__ s) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)B * W) return;
+  const int b = (int)(i / W), c = (int)(i % W);
+  x[i] += bias[c] * s[(long)b * (W / group) + c / group];
+}
+// ds[b, g] = sum_{c in g} dx[b,c] bias[c];  dbias[c] = beta*dbias[c] + sum_b dx[b,c] s[b, c/group]
+// grid W/64 workgroups of one wave (group == 64: one head per workgroup).
+__global__ void __launch_bounds__(64) head_bias_bwd_kernel(int B, int W, const float* __restrict__ dx,
+                                                           const float* __restrict__ bias, const float* __restrict__ s,
+                                                           float* __restrict__ ds, float* __restrict__ dbias, float beta) {
+  const int g = blockIdx.x, c = g * 64 + threadIdx.x;
+  const float bc = bias[c];
+  float acc = 0.f;
+  for (int b = 0; b < B; ++b) {
+    const float d = dx[(long)b * W + c];
+    acc += d * s[(long)b * (W / 64) + g];
+    const float t = wave_sum(d * bc);
+    if (threadIdx.x == 0) ds[(long)b * (W / 64) + g] = t;
+  }
+  if (dbias) dbias[c] = acc + (beta != 0.f ? beta * dbias[c] : 0.f);
+}
+
+template <typename T, typename TQ>
+int xfwd(int B, int S, const void* mem, const void* qp, const float* kb, float p, uint64_t seed, uint64_t off,
+         float* ws, float* probs, float* psum, void* ctx, hipStream_t st) {
+  hipLaunchKernelGGL((xrow_dot_kernel<T, TQ>), dim3((S + 63) / 64, B), dim3(64), 0, st, (const T*)mem, (const TQ*)qp,
+                     kb, S, ws);
+  const size_t lds = sizeof(float) * ((size_t)S * NH + 4 * NH * SLAB);
+  hipFuncSetAttribute((const void*)xctx_kernel<T, TQ>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL((xctx_kernel<T, TQ>), dim3(E / SLAB, B), dim3(256), lds, st, (const T*)mem, ws, S, p, seed, off,
+                     probs, psum, (TQ*)ctx);
+  return (int)hipGetLastError();
+}
+template <typename T, typename TQ>
+int xbwd(int B, int S, const void* mem, const void* qp, const float* probs, const float* dpsum, const void* dctx,
+         float p, uint64_t seed, uint64_t off, float* ws, void* dmem, float beta, void* dqp, hipStream_t st) {
+  hipLaunchKernelGGL((xrow_dot_kernel<T, TQ>), dim3((S + 63) / 64, B), dim3(64), 0, st, (const T*)mem,
+                     (const TQ*)dctx, (const float*)nullptr, S, ws);
+  const size_t lds = sizeof(float) * ((size_t)2 * S * NH + 4 * NH * SLAB);
+  hipFuncSetAttribute((const void*)xbwd_cols_kernel<T, TQ>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL((xbwd_cols_kernel<T, TQ>), dim3(E / SLAB, B), dim3(256), lds, st, (const T*)mem, (const TQ*)qp,
+                     probs, ws, dpsum, (const TQ*)dctx, S, p, seed, off, (T*)dmem, beta, (TQ*)dqp);
+  return (int)hipGetLastError();
 }
 
 }  // namespace
 
-template <typename T, typename TQ>
-int xfwd(int B, int S, const void* mem, const void* qp, const float* kb, float* probs, void* ctx, hipStream_t st) {
-  const size_t lds = sizeof(float) * (NH * E + NH * S);
-  hipFuncSetAttribute((const void*)xattn_fwd_kernel<T, TQ>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((xattn_fwd_kernel<T, TQ>), dim3(B), dim3(256), lds, st, (const T*)mem, (const TQ*)qp, kb, S, probs,
-                     (TQ*)ctx);
-  return (int)hipGetLastError();
-}
-template <typename T, typename TQ>
-int xbwd(int B, int S, const void* mem, const void* qp, const float* probs, const void* dctx, void* dmem, float beta,
-         void* dqp, hipStream_t st) {
-  const size_t lds = sizeof(float) * (2 * NH * E + 2 * NH * S);
-  hipFuncSetAttribute((const void*)xattn_bwd_kernel<T, TQ>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((xattn_bwd_kernel<T, TQ>), dim3(B), dim3(256), lds, st, (const T*)mem, (const TQ*)qp, probs,
-                     (const TQ*)dctx, S, (T*)dmem, beta, (TQ*)dqp);
-  return (int)hipGetLastError();
-}
-
 extern "C" int eegf_xattn_fwd(int mem_dtype, int q_dtype, int B, int S, const void* mem, const void* qp,
-                              const float* key_bias, float* probs, void* ctx, hipStream_t stream) {
-  if (B <= 0 || S <= 0 || S > 2048 || !mem || !qp || !probs || !ctx) return EEGF_ERR_ARG;
-  if (mem_dtype == EEGF_F32 && q_dtype == EEGF_F32) return xfwd<float, float>(B, S, mem, qp, key_bias, probs, ctx, stream);
-  if (mem_dtype == EEGF_BF16 && q_dtype == EEGF_BF16) return xfwd<bf16, bf16>(B, S, mem, qp, key_bias, probs, ctx, stream);
-  if (mem_dtype == EEGF_BF16 && q_dtype == EEGF_F32) return xfwd<bf16, float>(B, S, mem, qp, key_bias, probs, ctx, stream);
+                              const float* key_bias, float drop_p, unsigned long long seed, unsigned long long offset,
+                              float* ws, float* probs, float* psum, void* ctx, hipStream_t stream) {
+  if (B <= 0 || B > 65535 || S <= 0 || S > 1024 || !mem || !qp || !ws || !probs || !ctx) return EEGF_ERR_ARG;
+  if (drop_p < 0.f || drop_p >= 1.f || (drop_p > 0.f && !psum)) return EEGF_ERR_ARG;
+  if (mem_dtype == EEGF_F32 && q_dtype == EEGF_F32)
+    return xfwd<float, float>(B, S, mem, qp, key_bias, drop_p, seed, offset, ws, probs, psum, ctx, stream);
+  if (mem_dtype == EEGF_BF16 && q_dtype == EEGF_BF16)
+    return xfwd<bf16, bf16>(B, S, mem, qp, key_bias, drop_p, seed, offset, ws, probs, psum, ctx, stream);
+  if (mem_dtype == EEGF_BF16 && q_dtype == EEGF_F32)
+    return xfwd<bf16, float>(B, S, mem, qp, key_bias, drop_p, seed, offset, ws, probs, psum, ctx, stream);
   return EEGF_ERR_ARG;
 }
 
 extern "C" int eegf_xattn_bwd(int mem_dtype, int q_dtype, int B, int S, const void* mem, const void* qp,
-                              const float* probs, const void* dctx, void* dmem, float beta, void* dqp,
-                              hipStream_t stream) {
-  if (B <= 0 || S <= 0 || S > 2048 || !mem || !qp || !probs || !dctx || !dmem || !dqp) return EEGF_ERR_ARG;
+                              const float* probs, const float* dpsum, const void* dctx, float drop_p,
+                              unsigned long long seed, unsigned long long offset, float* ws, void* dmem, float beta,
+                              void* dqp, hipStream_t stream) {
+  if (B <= 0 || B > 65535 || S <= 0 || S > 1024 || !mem || !qp || !probs || !dctx || !ws || !dmem || !dqp)
+    return EEGF_ERR_ARG;
+  if (drop_p < 0.f || drop_p >= 1.f) return EEGF_ERR_ARG;
   if (mem_dtype == EEGF_F32 && q_dtype == EEGF_F32)
-    return xbwd<float, float>(B, S, mem, qp, probs, dctx, dmem, beta, dqp, stream);
+    return xbwd<float, float>(B, S, mem, qp, probs, dpsum, dctx, drop_p, seed, offset, ws, dmem, beta, dqp, stream);
   if (mem_dtype == EEGF_BF16 && q_dtype == EEGF_BF16)
-    return xbwd<bf16, bf16>(B, S, mem, qp, probs, dctx, dmem, beta, dqp, stream);
+    return xbwd<bf16, bf16>(B, S, mem, qp, probs, dpsum, dctx, drop_p, seed, offset, ws, dmem, beta, dqp, stream);
   if (mem_dtype == EEGF_BF16 && q_dtype == EEGF_F32)
-    return xbwd<bf16, float>(B, S, mem, qp, probs, dctx, dmem, beta, dqp, stream);
+    return xbwd<bf16, float>(B, S, mem, qp, probs, dpsum, dctx, drop_p, seed, offset, ws, dmem, beta, dqp, stream);
   return EEGF_ERR_ARG;
+}
+
+extern "C" int eegf_head_bias_fwd(int B, int W, int group, float* x, const float* bias, const float* s,
+                                  hipStream_t stream) {
+  if (B <= 0 || W <= 0 || group <= 0 || W % group != 0 || !x || !bias || !s) return EEGF_ERR_ARG;
+  const long n = (long)B * W;
+  hipLaunchKernelGGL(head_bias_fwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, B, W, group, x,
+                     bias, s);
+  return (int)hipGetLastError();
+}
+
+extern "C" int eegf_head_bias_bwd(int B, int W, int group, const float* dx, const float* bias, const float* s,
+                                  float* ds, float* dbias, float beta, hipStream_t stream) {
+  if (B <= 0 || W <= 0 || group != 64 || W % 64 != 0 || !dx || !bias || !s || !ds) return EEGF_ERR_ARG;
+  hipLaunchKernelGGL(head_bias_bwd_kernel, dim3(W / 64), dim3(64), 0, stream, B, W, dx, bias, s, ds, dbias, beta);
+  return (int)hipGetLastError();
 }

@@ -1,6 +1,9 @@
 // elementwise.hip — small bandwidth-bound helpers between the fused kernels.
 //   eegf_axpby:    y = alpha*x + beta*y          (gradient sums where two paths meet)
 //   eegf_tanh_bwd: dx = dy * (1 - y^2)           (BertPooler tanh, modeling_bert.py:457-462)
+//   eegf_dropout:  x[i] *= mask(i / group)        (in place; group 1 = elementwise dropout, e.g. the
+//                  decoder FFN's inner dropout transformer.py:1197-1199; group 64 = one draw per head, the
+//                  decoder self-attention's dropout of its single attention weight transformer.py:1158-1176)
 #include "common.h"
 #include "eegfusion_internal.h"
 
@@ -16,6 +19,13 @@ template <typename T>
 __global__ void __launch_bounds__(256) tanh_bwd_kernel(long n, const T* __restrict__ dy, const T* __restrict__ y, T* __restrict__ dx) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i < n) { const float t = to_f32(y[i]); dx[i] = from_f32<T>(to_f32(dy[i]) * (1.f - t * t)); }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) dropout_kernel(long n, int group, float p, uint64_t seed, uint64_t offset,
+                                                      T* __restrict__ x) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) x[i] = from_f32<T>(to_f32(x[i]) * drop_mask1(seed, offset, (uint64_t)(i / group), p));
 }
 
 }  // namespace
@@ -34,6 +44,17 @@ extern "C" int eegf_tanh_bwd(int dtype, long n, const void* dy, const void* y, v
   const dim3 grid((unsigned)((n + 255) / 256));
   if (dtype == EEGF_F32) hipLaunchKernelGGL(tanh_bwd_kernel<float>, grid, dim3(256), 0, stream, n, (const float*)dy, (const float*)y, (float*)dx);
   else if (dtype == EEGF_BF16) hipLaunchKernelGGL(tanh_bwd_kernel<bf16>, grid, dim3(256), 0, stream, n, (const bf16*)dy, (const bf16*)y, (bf16*)dx);
+  else return EEGF_ERR_ARG;
+  return (int)hipGetLastError();
+}
+
+extern "C" int eegf_dropout(int dtype, long n, int group, float p, unsigned long long seed, unsigned long long offset,
+                            void* x, hipStream_t stream) {
+  if (n <= 0 || group <= 0 || p < 0.f || p >= 1.f || !x) return EEGF_ERR_ARG;
+  if (p == 0.f) return 0;
+  const dim3 grid((unsigned)((n + 255) / 256));
+  if (dtype == EEGF_F32) hipLaunchKernelGGL(dropout_kernel<float>, grid, dim3(256), 0, stream, n, group, p, seed, offset, (float*)x);
+  else if (dtype == EEGF_BF16) hipLaunchKernelGGL(dropout_kernel<bf16>, grid, dim3(256), 0, stream, n, group, p, seed, offset, (bf16*)x);
   else return EEGF_ERR_ARG;
   return (int)hipGetLastError();
 }

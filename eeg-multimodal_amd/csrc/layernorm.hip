@@ -32,18 +32,6 @@ template <> struct V4<bf16> {
   }
 };
 
-// Dropout keep-mask for 4 consecutive elements starting at element index e4*4.
-DEV void drop_mask4(uint64_t seed, uint64_t offset, uint64_t e4, float p, float (&m)[4]) {
-  const u32x4s r = philox4x32((uint32_t)e4, (uint32_t)(e4 >> 32), (uint32_t)offset, (uint32_t)(offset >> 32),
-                              (uint32_t)seed, (uint32_t)(seed >> 32));
-  const float scale = 1.0f / (1.0f - p);
-  const uint32_t thr = (uint32_t)fminf(p * 4294967296.0f, 4294967295.0f);
-  m[0] = r.x >= thr ? scale : 0.f;
-  m[1] = r.y >= thr ? scale : 0.f;
-  m[2] = r.z >= thr ? scale : 0.f;
-  m[3] = r.w >= thr ? scale : 0.f;
-}
-
 struct LnFwdArgs {
   const void* x; const void* r; const float* table; const float* table2;
   const float* gamma; const float* beta;

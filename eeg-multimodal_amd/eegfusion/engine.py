@@ -50,7 +50,7 @@ class EngineConfig:
     eps: float = 1.0
     eps_mode: str = "newfrac"
     hidden_dropout: float = 0.1    # BertConfig.hidden_dropout_prob
-    attn_dropout: float = 0.1      # attention_probs_dropout_prob (not yet fused)
+    attn_dropout: float = 0.1      # BertConfig.attention_probs_dropout_prob (fused into eegf_attn_*)
     dec_dropout: float = 0.1       # TransformerDecoderLayer(dropout=0.1)
     eeg_channels: int = 64
     act_dim: int = 32
@@ -185,6 +185,10 @@ class FusionEngine:
         call("eegf_colsum", _code(dy), P(dy), ld or width, rows, width, period, P(ws), ws.numel(), P(o), 1.0,
              _stream())
 
+    def dropout(self, x, group, p, rng):
+        if p > 0:
+            call("eegf_dropout", _code(x), x.numel(), group, float(p), self.cfg.seed, rng, P(x), _stream())
+
     def ln_fwd(self, x, r, pre, rows, out, s, mean, rstd, eps, p=0.0, mode=0, rng=0, table=None, period=1,
                table2=None):
         call("eegf_ln_fwd", _code(x), rows, HID, P(x), P(r), P(table), period, P(table2), P(self.F(pre + ".weight")),
@@ -210,6 +214,7 @@ class FusionEngine:
         sv.rng = self.rng_counter
         self.rng_counter += 1 << 12
         pdrop = cfg.hidden_dropout if training else 0.0
+        adrop = cfg.attn_dropout if training else 0.0
         ddrop = cfg.dec_dropout if training else 0.0
 
         # ---------------- EEG front-end + BERT embeddings
@@ -254,7 +259,8 @@ class FusionEngine:
             ctx = self.empty(R, HID)
             lse = torch.empty(B, NH, L, dtype=torch.float32, device=self.a.device)
             ev = self._ev_start("attn_fwd")
-            call("eegf_attn_fwd", self.code, B, NH, L, P(qkv), 3 * HID, P(kbias), scale, P(ctx), HID, P(lse), _stream())
+            call("eegf_attn_fwd", self.code, B, NH, L, P(qkv), 3 * HID, P(kbias), scale, float(adrop), self.cfg.seed,
+                 sv.rng + 12 + 3 * i, P(ctx), HID, P(lse), _stream())
             self._ev_end("attn_fwd", ev)
             ao = self.ws.get("ao", R * HID, self.dt).view(R, HID)
             self.linear(ctx, self.W(pre + "attention.output.dense.weight"), self.F(pre + "attention.output.dense.bias"),
@@ -298,6 +304,8 @@ class FusionEngine:
             in_w, in_b = self.F(pre + "self_attn.in_proj_weight"), self.F(pre + "self_attn.in_proj_bias")
             v = self.eh(B, HID)
             self.linear(x, in_w[2 * HID:], in_b[2 * HID:], v, B)
+            # one query, one key: the attention weight is 1, so dropout of it is a per-(row, head) mask on v
+            self.dropout(v, 64, ddrop, sv.rng + 103 + 8 * d)
             sa = self.eh(B, HID)
             self.linear(v, self.F(pre + "self_attn.out_proj.weight"), self.F(pre + "self_attn.out_proj.bias"), sa, B)
             x1, ln1 = self.eh(B, HID), (self.eh(B, HID), self._f32(B), self._f32(B))
@@ -310,12 +318,18 @@ class FusionEngine:
             self.gemm(q, cw[HID:2 * HID], qp, B, HID, DH, 1, 0, HID, HID, NH * HID, alpha=scale, batch=NH, sA=DH,
                       sB=DH * HID, sC=HID)
             probs = self._f32(B, NH, L)
+            psum = self._f32(B, NH) if ddrop > 0 else None
             cc = self.eh(B, NH, HID)
-            call("eegf_xattn_fwd", _code(h), F32, B, L, P(h), P(qp), P(kbias), P(probs), P(cc), _stream())
+            xws = self.ws.get("xattn", B * NH * L, torch.float32)
+            call("eegf_xattn_fwd", _code(h), F32, B, L, P(h), P(qp), P(kbias), float(ddrop), self.cfg.seed,
+                 sv.rng + 104 + 8 * d, P(xws), P(probs), P(psum), P(cc), _stream())
             ctxd = self.eh(B, HID)
-            # ctx[b, h*64+n] = sum_c cc[b,h,c] Wv[h*64+n, c] + bv[h*64+n]
-            self.gemm(cc, cw[2 * HID:], ctxd, B, DH, HID, 1, 1, NH * HID, HID, HID, epi=_lib.EPI_BIAS,
-                      bias=cb[2 * HID:], batch=NH, sA=HID, sB=DH * HID, sC=DH, sBias=DH)
+            # ctx[b, h*64+n] = sum_c cc[b,h,c] Wv[h*64+n, c] + s[b,h] bv[h*64+n]   (s = sum_j p~_j; 1 w/o dropout)
+            self.gemm(cc, cw[2 * HID:], ctxd, B, DH, HID, 1, 1, NH * HID, HID, HID,
+                      epi=_lib.EPI_BIAS if psum is None else _lib.EPI_NONE,
+                      bias=cb[2 * HID:] if psum is None else None, batch=NH, sA=HID, sB=DH * HID, sC=DH, sBias=DH)
+            if psum is not None:
+                call("eegf_head_bias_fwd", B, HID, DH, P(ctxd), P(cb[2 * HID:]), P(psum), _stream())
             ca = self.eh(B, HID)
             self.linear(ctxd, self.F(pre + "multihead_attn.out_proj.weight"),
                         self.F(pre + "multihead_attn.out_proj.bias"), ca, B)
@@ -323,12 +337,13 @@ class FusionEngine:
             self.ln_fwd(ca, x1, pre + "norm2", B, x2, *ln2, 1e-5, ddrop, 1, sv.rng + 101 + 8 * d)
             f1 = self.eh(B, DEC_FF)
             self.linear(x2, self.F(pre + "linear1.weight"), self.F(pre + "linear1.bias"), f1, B, epi=_lib.EPI_BIAS_RELU)
+            self.dropout(f1, 1, ddrop, sv.rng + 105 + 8 * d)      # _ff_block's inner dropout
             f2 = self.eh(B, HID)
             self.linear(f1, self.F(pre + "linear2.weight"), self.F(pre + "linear2.bias"), f2, B)
             x3, ln3 = self.eh(B, HID), (self.eh(B, HID), self._f32(B), self._f32(B))
             self.ln_fwd(f2, x2, pre + "norm3", B, x3, *ln3, 1e-5, ddrop, 1, sv.rng + 102 + 8 * d)
-            dl.append(dict(x=x, v=v, x1=x1, ln1=ln1, q=q, qp=qp, probs=probs, cc=cc, ctx=ctxd, x2=x2, ln2=ln2, f1=f1,
-                           ln3=ln3))
+            dl.append(dict(x=x, v=v, x1=x1, ln1=ln1, q=q, qp=qp, probs=probs, psum=psum, cc=cc, ctx=ctxd, x2=x2,
+                           ln2=ln2, f1=f1, ln3=ln3))
             x = x3
         t["dec"] = dl
         cross = x
@@ -370,6 +385,7 @@ class FusionEngine:
         B, L = sv.B, sv.L
         R = B * L
         pdrop = cfg.hidden_dropout if sv.training else 0.0
+        adrop = cfg.attn_dropout if sv.training else 0.0
         ddrop = cfg.dec_dropout if sv.training else 0.0
         dlogits = dlogits.float().contiguous()
         hd = t["head"]
@@ -417,7 +433,9 @@ class FusionEngine:
             self.wgrad(df2, s["f1"], pre + "linear2.weight", B)
             self.bgrad(df2, pre + "linear2.bias", B)
             df1 = self.eh(B, DEC_FF)
-            self.dgrad(df2, self.F(pre + "linear2.weight"), df1, B, epi=_lib.EPI_DRELU, aux=s["f1"])
+            # f1 holds dropout(relu(.)): f1 > 0 exactly where both the mask and the ReLU pass
+            self.dgrad(df2, self.F(pre + "linear2.weight"), df1, B, epi=_lib.EPI_DRELU, aux=s["f1"],
+                       scale=1.0 / (1.0 - ddrop))
             self.wgrad(df1, s["x2"], pre + "linear1.weight", B)
             self.bgrad(df1, pre + "linear1.bias", B)
             self.dgrad(df1, self.F(pre + "linear1.weight"), dx2, B, beta=1.0)
@@ -435,15 +453,22 @@ class FusionEngine:
                 # dWv_h[n, c] = sum_b dctx[b, h*64+n] cc[b,h,c]
                 self.gemm(dctx, s["cc"], gw[2 * HID:], DH, HID, B, 0, 0, HID, NH * HID, HID, beta=1.0, batch=NH,
                           sA=DH, sB=HID, sC=DH * HID)
-            if self.need(bname):
+            dpsum = None
+            if s["psum"] is not None:
+                dpsum = self._f32(B, NH)
+                call("eegf_head_bias_bwd", B, HID, DH, P(dctx), P(self.F(bname)[2 * HID:]), P(s["psum"]), P(dpsum),
+                     P(self.G(bname)[2 * HID:]) if self.need(bname) else None, 1.0, _stream())
+            elif self.need(bname):
                 self.bgrad(dctx, bname, B, out=self.G(bname)[2 * HID:])
             dcc = self.eh(B, NH, HID)
             # dcc[b,h,c] = sum_n dctx[b, h*64+n] Wv[h*64+n, c]
             self.gemm(dctx, cw[2 * HID:], dcc, B, HID, DH, 1, 0, HID, HID, NH * HID, batch=NH, sA=DH, sB=DH * HID,
                       sC=HID)
             dqp = self.eh(B, NH, HID)
-            call("eegf_xattn_bwd", _code(mem), F32, B, L, P(mem), P(s["qp"]), P(s["probs"]), P(dcc), P(dmem),
-                 0.0 if d == DEC_L - 1 else 1.0, P(dqp), _stream())
+            xws = self.ws.get("xattn", B * NH * L, torch.float32)
+            call("eegf_xattn_bwd", _code(mem), F32, B, L, P(mem), P(s["qp"]), P(s["probs"]), P(dpsum), P(dcc),
+                 float(ddrop), self.cfg.seed, sv.rng + 104 + 8 * d, P(xws), P(dmem), 0.0 if d == DEC_L - 1 else 1.0,
+                 P(dqp), _stream())
             dq = self.eh(B, HID)
             # dq[b, h*64+i] = sum_c dqp[b,h,c] Wk[h*64+i, c] / 8
             self.gemm(dqp, cw[HID:2 * HID], dq, B, DH, HID, 1, 1, NH * HID, HID, HID, alpha=scale, batch=NH, sA=HID,
@@ -462,6 +487,7 @@ class FusionEngine:
             self.bgrad(dsa, pre + "self_attn.out_proj.bias", B)
             dv = self.eh(B, HID)
             self.dgrad(dsa, self.F(pre + "self_attn.out_proj.weight"), dv, B)
+            self.dropout(dv, 64, ddrop, sv.rng + 103 + 8 * d)
             sw = self.F(pre + "self_attn.in_proj_weight")
             if self.need(pre + "self_attn.in_proj_weight"):
                 self.gemm(dv, s["x"], self.G(pre + "self_attn.in_proj_weight")[2 * HID:], HID, HID, B, 0, 0, HID, HID,
@@ -516,8 +542,9 @@ class FusionEngine:
             self.wgrad(dao, s["ctx"], pre + "attention.output.dense.weight", R)
             self.bgrad(dao, pre + "attention.output.dense.bias", R)
             self.dgrad(dao, self.W(pre + "attention.output.dense.weight"), dctx, R)
-            call("eegf_attn_bwd", self.code, B, NH, L, P(s["qkv"]), 3 * HID, P(t["kbias"]), scale, P(s["ctx"]),
-                 P(dctx), HID, P(s["lse"]), P(dqkv), P(dq_ws), _stream())
+            call("eegf_attn_bwd", self.code, B, NH, L, P(s["qkv"]), 3 * HID, P(t["kbias"]), scale, float(adrop),
+                 self.cfg.seed, sv.rng + 12 + 3 * i, P(s["ctx"]), P(dctx), HID, P(s["lse"]), P(dqkv), P(dq_ws),
+                 _stream())
             qn = pre + "attention.self.query.weight"
             if self.need(qn):
                 gq = self.a.span(qn, 3, self.a.grad).view(3 * HID, HID)

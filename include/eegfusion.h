@@ -88,27 +88,45 @@ int eegf_colsum(int dtype, const void* in, long ld, long rows, int width, int pe
 
 /* Multi-head self-attention (12 x 64) over the fused QKV projection [B, L, ld_qkv>=2304]
  * (BertSelfAttention, modeling_bert.py:139-199).  key_bias [B, L]: 0 or -1e30 (nullable).
- * out [B, L, ld_out>=768]; lse [B, 12, L] saved for the backward.  L % 128 == 0. */
+ * drop_p: dropout of the attention probabilities (modeling_bert.py:131,198; 0 = off), Philox
+ * (seed, offset), element ((b*12+h)*L+q)*L+key.  out [B, L, ld_out>=768]; lse [B, 12, L] saved
+ * for the backward.  L % 128 == 0. */
 int eegf_attn_fwd(int dtype, int B, int H, int L, const void* qkv, long ld_qkv, const float* key_bias,
-                  float scale, void* out, long ld_out, float* lse, hipStream_t stream);
+                  float scale, float drop_p, unsigned long long seed, unsigned long long offset,
+                  void* out, long ld_out, float* lse, hipStream_t stream);
 /* fp32 workspace (elements) eegf_attn_bwd needs for dQ accumulation (0 when L <= 256). */
 long eegf_attn_bwd_workspace(int B, int L);
-/* Attention backward: writes dQ|dK|dV into dqkv [B, L, ld_qkv] (same layout as qkv). L % 256 == 0. */
+/* Attention backward: writes dQ|dK|dV into dqkv [B, L, ld_qkv] (same layout as qkv).  drop_p,
+ * seed, offset as in the forward (the mask is regenerated).  L % 256 == 0. */
 int eegf_attn_bwd(int dtype, int B, int H, int L, const void* qkv, long ld_qkv, const float* key_bias,
-                  float scale, const void* out, const void* dout, long ld_out, const float* lse,
+                  float scale, float drop_p, unsigned long long seed, unsigned long long offset,
+                  const void* out, const void* dout, long ld_out, const float* lse,
                   void* dqkv, float* dq_workspace, hipStream_t stream);
 
 /* Decoder cross-attention over the BERT memory with a single query token
  * (TransformerDecoderLayer._mha_block, transformer.py:1177-1196; model.py:40-43), in the
- * reduced form: qp [B,12,768] = Wk_h^T q_h / 8 (by eegf_gemm); probs [B,12,S] saved;
- * ctx [B,12,768] = sum_j p_j M_j.  key_bias [B,S] nullable.  mem_dtype: the encoder's dtype;
- * q_dtype: the decoder's (bf16 mode runs the decoder in fp32: F32 with a BF16 memory). */
+ * reduced form: qp [B,12,768] = Wk_h^T q_h / 8 (by eegf_gemm); probs [B,12,S] (undropped p)
+ * saved; ctx [B,12,768] = sum_j p~_j M_j with p~ = dropout(p) (drop_p, Philox element
+ * (b*12+h)*S+j); psum [B,12] = sum_j p~_j (required when drop_p > 0; the caller adds
+ * psum_h * bv_h with eegf_head_bias_fwd).  key_bias [B,S] nullable.  ws: B*12*S floats.
+ * mem_dtype: the encoder's dtype; q_dtype: the decoder's (bf16 mode runs the decoder in fp32:
+ * F32 with a BF16 memory).  S <= 1024. */
 int eegf_xattn_fwd(int mem_dtype, int q_dtype, int B, int S, const void* mem, const void* qp,
-                   const float* key_bias, float* probs, void* ctx, hipStream_t stream);
-/* Backward: dmem [B,S,768] (= result + beta*dmem), dqp [B,12,768]. */
+                   const float* key_bias, float drop_p, unsigned long long seed, unsigned long long offset,
+                   float* ws, float* probs, float* psum, void* ctx, hipStream_t stream);
+/* Backward: dctx = dL/dctx [B,12,768]; dpsum [B,12] = dL/dpsum (nullable);
+ * dmem [B,S,768] (= result + beta*dmem), dqp [B,12,768].  ws: B*12*S floats. */
 int eegf_xattn_bwd(int mem_dtype, int q_dtype, int B, int S, const void* mem, const void* qp,
-                   const float* probs, const void* dctx, void* dmem, float beta, void* dqp,
-                   hipStream_t stream);
+                   const float* probs, const float* dpsum, const void* dctx, float drop_p,
+                   unsigned long long seed, unsigned long long offset, float* ws, void* dmem,
+                   float beta, void* dqp, hipStream_t stream);
+/* x[b,c] += bias[c] * s[b, c/group]  (fp32; the psum_h * bv_h term of the cross-attention). */
+int eegf_head_bias_fwd(int B, int W, int group, float* x, const float* bias, const float* s,
+                       hipStream_t stream);
+/* ds[b,g] = sum_{c in g} dx[b,c] bias[c];  dbias[c] = sum_b dx[b,c] s[b,c/group] + beta*dbias[c]
+ * (dbias nullable).  group == 64. */
+int eegf_head_bias_bwd(int B, int W, int group, const float* dx, const float* bias, const float* s,
+                       float* ds, float* dbias, float beta, hipStream_t stream);
 
 /* Fused concat [pooled|img|cross] -> min-max -> privacy stage (variant FUSE_*), one row per
  * workgroup (model.py:46-61, past_acc.py:120-136, main_0430.py:76-85).  noise/gumbels (fp32
@@ -136,6 +154,12 @@ int eegf_cross_entropy(int dtype, int B, int C, const void* logits, const long l
 /* y = alpha*x + beta*y ; dx = dy*(1-y^2) */
 int eegf_axpby(int dtype, long n, float alpha, const void* x, float beta, void* y, hipStream_t stream);
 int eegf_tanh_bwd(int dtype, long n, const void* dy, const void* y, void* dx, hipStream_t stream);
+/* In-place dropout x[i] *= mask(i / group) (Philox element i/group of (seed, offset); kept
+ * elements scale by 1/(1-p)).  group 1: elementwise (decoder FFN inner dropout,
+ * transformer.py:1197-1199); group 64: one draw per head (decoder self-attention weight dropout,
+ * transformer.py:1158-1176).  Applying it to the gradient gives the backward. */
+int eegf_dropout(int dtype, long n, int group, float p, unsigned long long seed, unsigned long long offset,
+                 void* x, hipStream_t stream);
 
 /* torch.optim.Adam step over a contiguous fp32 range (+ optional bf16 shadow refresh). */
 int eegf_adam(long n, float* p, const float* g, float* m, float* v, void* bf16_shadow, float lr,

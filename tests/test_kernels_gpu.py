@@ -108,20 +108,29 @@ def test_colsum(dt, period):
     assert _rel(out, ref) < 1e-5
 
 
-def _attn_ref(qkv, B, L, kbias):
+def _attn_ref(qkv, B, L, kbias, zmask=None):
     q, k, v = qkv.double().view(B, L, 3, 12, 64).unbind(2)
     q, k, v = (t.transpose(1, 2) for t in (q, k, v))
     s = q @ k.transpose(-1, -2) / 8.0
     if kbias is not None:
         s = s + kbias.double()[:, None, None, :]
     p = s.softmax(-1)
+    if zmask is not None:            # dropout(attention_probs) with the kernel's Philox mask
+        p = p * zmask
     return (p @ v).transpose(1, 2).reshape(B, L, 768)
+
+
+def _attn_mask(B, L, p, seed, offset):
+    from philox_ref import attn_mask
+    e = torch.arange(B * 12 * L * L, dtype=torch.int64).numpy()
+    return torch.from_numpy(attn_mask(seed, offset, e, p)).view(B, 12, L, L).cuda()
 
 
 @pytest.mark.parametrize("dt", DT)
 @pytest.mark.parametrize("L", [256, 512])
 @pytest.mark.parametrize("masked", [False, True])
-def test_attention_fwd_bwd(dt, L, masked):
+@pytest.mark.parametrize("pdrop", [0.0, 0.25])
+def test_attention_fwd_bwd(dt, L, masked, pdrop):
     lib = _lib()
     torch.manual_seed(1)
     B = 2
@@ -136,11 +145,15 @@ def test_attention_fwd_bwd(dt, L, masked):
         lib.call("eegf_key_bias", B * L, mask.data_ptr(), kbias.data_ptr(), _s())
     out = torch.empty(B, L, 768, device="cuda", dtype=dt)
     lse = torch.empty(B, 12, L, device="cuda")
+    seed, off = 77, 5
     lib.call("eegf_attn_fwd", _code(dt), B, 12, L, qkv.data_ptr(), 2304, None if kbias is None else kbias.data_ptr(),
-             0.125, out.data_ptr(), 768, lse.data_ptr(), _s())
+             0.125, pdrop, seed, off, out.data_ptr(), 768, lse.data_ptr(), _s())
     torch.cuda.synchronize()
     qr = qkv.double().clone().requires_grad_()
-    ref = _attn_ref(qr, B, L, kbias)
+    z = _attn_mask(B, L, pdrop, seed, off) if pdrop > 0 else None
+    if z is not None:
+        assert abs((z > 0).double().mean().item() - (1 - pdrop)) < 0.01
+    ref = _attn_ref(qr, B, L, kbias, z)
     assert _rel(out, ref) < _tol(dt)
     dout = torch.randn(B, L, 768, device="cuda").to(dt)
     ref.backward(dout.double())
@@ -148,7 +161,7 @@ def test_attention_fwd_bwd(dt, L, masked):
     ws_n = lib.lib().eegf_attn_bwd_workspace(B, L)
     ws = torch.empty(max(ws_n, 1), device="cuda")
     lib.call("eegf_attn_bwd", _code(dt), B, 12, L, qkv.data_ptr(), 2304, None if kbias is None else kbias.data_ptr(),
-             0.125, out.data_ptr(), dout.data_ptr(), 768, lse.data_ptr(), dqkv.data_ptr(), ws.data_ptr(), _s())
+             0.125, pdrop, seed, off, out.data_ptr(), dout.data_ptr(), 768, lse.data_ptr(), dqkv.data_ptr(), ws.data_ptr(), _s())
     torch.cuda.synchronize()
     for sl, name in ((slice(0, 768), "dq"), (slice(768, 1536), "dk"), (slice(1536, 2304), "dv")):
         e = _rel(dqkv[..., sl], qr.grad[..., sl])
@@ -165,40 +178,104 @@ def test_xattn_mixed_dtypes(dt):
     qp = 0.05 * torch.randn(B, 12, 768, device="cuda")
     probs = torch.empty(B, 12, S, device="cuda")
     cc = torch.empty(B, 12, 768, device="cuda")
-    lib.call("eegf_xattn_fwd", 1, 0, B, S, mem.data_ptr(), qp.data_ptr(), None, probs.data_ptr(), cc.data_ptr(), _s())
+    ws = torch.empty(B * 12 * S, device="cuda")
+    lib.call("eegf_xattn_fwd", 1, 0, B, S, mem.data_ptr(), qp.data_ptr(), None, 0.0, 0, 0, ws.data_ptr(),
+             probs.data_ptr(), None, cc.data_ptr(), _s())
     torch.cuda.synchronize()
     p = torch.einsum("bhc,bjc->bhj", qp.double(), mem.double()).softmax(-1)
     assert _rel(cc, torch.einsum("bhj,bjc->bhc", p, mem.double())) < 1e-5
 
 
 @pytest.mark.parametrize("dt", DT)
-def test_xattn_fwd_bwd(dt):
+@pytest.mark.parametrize("S,pdrop,masked", [(256, 0.0, False), (256, 0.3, False), (100, 0.0, True), (300, 0.2, True)])
+def test_xattn_fwd_bwd(dt, S, pdrop, masked):
+    """Reduced cross-attention (scores, softmax, dropout(p), context, s = sum p~) and its backward
+    (dM, dq', with a gradient on s) vs float64 autograd with the replayed Philox mask."""
+    from philox_ref import drop_mask
     lib = _lib()
     torch.manual_seed(2)
-    B, S = 3, 256
+    B = 3
+    seed, off = 1234, 99
     mem = torch.randn(B, S, 768, device="cuda").to(dt)
     qp = (0.05 * torch.randn(B, 12, 768, device="cuda")).to(dt)
+    kbias = None
+    if masked:
+        kbias = torch.zeros(B, S, device="cuda")
+        kbias[0, S // 2:] = -1e30
     probs = torch.empty(B, 12, S, device="cuda")
+    psum = torch.empty(B, 12, device="cuda")
     cc = torch.empty(B, 12, 768, device="cuda", dtype=dt)
-    lib.call("eegf_xattn_fwd", _code(dt), _code(dt), B, S, mem.data_ptr(), qp.data_ptr(), None, probs.data_ptr(),
-             cc.data_ptr(), _s())
+    ws = torch.empty(B * 12 * S, device="cuda")
+    lib.call("eegf_xattn_fwd", _code(dt), _code(dt), B, S, mem.data_ptr(), qp.data_ptr(),
+             None if kbias is None else kbias.data_ptr(), pdrop, seed, off, ws.data_ptr(), probs.data_ptr(),
+             psum.data_ptr(), cc.data_ptr(), _s())
     torch.cuda.synchronize()
     m = mem.double().clone().requires_grad_()
     q = qp.double().clone().requires_grad_()
-    p = torch.einsum("bhc,bjc->bhj", q, m).softmax(-1)
-    c = torch.einsum("bhj,bjc->bhc", p, m)
+    sc = torch.einsum("bhc,bjc->bhj", q, m)
+    if kbias is not None:
+        sc = sc + kbias.double()[:, None, :]
+    p = sc.softmax(-1)
+    z = torch.ones_like(p)
+    if pdrop > 0:
+        z = torch.from_numpy(drop_mask(seed, off, torch.arange(B * 12 * S).numpy(), pdrop)).view(B, 12, S).cuda()
+    pt = p * z
+    c = torch.einsum("bhj,bjc->bhc", pt, m)
+    s = pt.sum(-1)
     assert _rel(probs, p) < _tol(dt)
     assert _rel(cc, c) < _tol(dt)
+    if pdrop > 0:
+        assert _rel(psum, s) < 1e-5
     dc = torch.randn(B, 12, 768, device="cuda").to(dt)
-    c.backward(dc.double())
+    dps = torch.randn(B, 12, device="cuda")
+    (c * dc.double()).sum().add((s * dps.double()).sum() if pdrop > 0 else 0.0).backward()
     dmem = torch.randn_like(mem)
     dmem0 = dmem.double().clone()
     dqp = torch.empty_like(qp)
     lib.call("eegf_xattn_bwd", _code(dt), _code(dt), B, S, mem.data_ptr(), qp.data_ptr(), probs.data_ptr(),
-             dc.data_ptr(), dmem.data_ptr(), 1.0, dqp.data_ptr(), _s())
+             dps.data_ptr() if pdrop > 0 else None, dc.data_ptr(), pdrop, seed, off, ws.data_ptr(), dmem.data_ptr(),
+             1.0, dqp.data_ptr(), _s())
     torch.cuda.synchronize()
     assert _rel(dmem.double() - dmem0, m.grad) < _tol(dt) * 3
     assert _rel(dqp, q.grad) < _tol(dt) * 3
+
+
+def test_head_bias_fwd_bwd():
+    lib = _lib()
+    torch.manual_seed(4)
+    B = 37
+    x = torch.randn(B, 768, device="cuda")
+    bias = torch.randn(768, device="cuda")
+    s = torch.rand(B, 12, device="cuda")
+    ref = x.double() + bias.double() * s.double().repeat_interleave(64, 1)
+    lib.call("eegf_head_bias_fwd", B, 768, 64, x.data_ptr(), bias.data_ptr(), s.data_ptr(), _s())
+    torch.cuda.synchronize()
+    assert _rel(x, ref) < 1e-6
+    dx = torch.randn(B, 768, device="cuda")
+    ds = torch.empty(B, 12, device="cuda")
+    dbias = torch.randn(768, device="cuda")
+    db0 = dbias.double().clone()
+    lib.call("eegf_head_bias_bwd", B, 768, 64, dx.data_ptr(), bias.data_ptr(), s.data_ptr(), ds.data_ptr(),
+             dbias.data_ptr(), 1.0, _s())
+    torch.cuda.synchronize()
+    assert _rel(ds, (dx.double() * bias.double()).view(B, 12, 64).sum(-1)) < 1e-5
+    assert _rel(dbias.double() - db0, (dx.double() * s.double().repeat_interleave(64, 1)).sum(0)) < 1e-5
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("group", [1, 64])
+def test_dropout_grouped(dt, group):
+    from philox_ref import drop_mask
+    lib = _lib()
+    torch.manual_seed(5)
+    n, p, seed, off = 256 * 768, 0.1, 31, 17
+    x = torch.randn(n, device="cuda").to(dt)
+    x0 = x.double().clone()
+    lib.call("eegf_dropout", _code(dt), n, group, p, seed, off, x.data_ptr(), _s())
+    torch.cuda.synchronize()
+    mk = torch.from_numpy(drop_mask(seed, off, (torch.arange(n) // group).numpy(), p)).cuda()
+    assert abs((mk > 0).double().mean().item() - (1 - p)) < 0.02 if group == 1 else True
+    assert _rel(x, x0 * mk) < _tol(dt)
 
 
 @pytest.mark.parametrize("dt", DT)

@@ -1,0 +1,30 @@
+"""Philox4x32 restatement (tests/philox_ref.py, which mirrors csrc/common.h) against the Random123
+known-answer vectors (kat_vectors: philox4x32_10), and the dropout-stream conventions."""
+import numpy as np
+
+from philox_ref import attn_mask, drop_mask, philox4x32
+
+KAT = [  # (counter, key, expected) — Random123 philox4x32_10 KAT
+    ((0, 0, 0, 0), (0, 0), (0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8)),
+    ((0xFFFFFFFF,) * 4, (0xFFFFFFFF, 0xFFFFFFFF), (0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD)),
+    ((0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344), (0xA4093822, 0x299F31D0),
+     (0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1)),
+]
+
+
+def test_philox4x32_10_known_answers():
+    for ctr, key, want in KAT:
+        got = tuple(int(w) for w in philox4x32(*ctr, *key))
+        assert got == want, (ctr, [hex(x) for x in got])
+
+
+def test_dropout_streams_rates():
+    e = np.arange(1 << 18)
+    for p in (0.1, 0.25):
+        for fn in (drop_mask, attn_mask):
+            m = fn(7, 3, e, p)
+            assert abs((m > 0).mean() - (1 - p)) < 0.005
+            assert np.allclose(m[m > 0], 1 / (1 - np.float32(p)))
+    # distinct offsets give independent masks
+    a, b = drop_mask(7, 3, e, 0.5) > 0, drop_mask(7, 4, e, 0.5) > 0
+    assert abs((a == b).mean() - 0.5) < 0.01
