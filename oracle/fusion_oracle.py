@@ -17,8 +17,20 @@ Follows, line by line:
     python/src/custom_models/models.py:56-82.
   * gumbel_softmax: torch/nn/functional.py gumbel_softmax (soft + straight-through hard).
   * Laplace sampling: torch/distributions/laplace.py:83-86 (u ~ U[eps-1, 1); loc - scale*sign(u)*log1p(-|u|)).
-Dropout is p=0 in parity mode (the reference's dropout draws come from torch's RNG and cannot be
-replayed); the HIP path's own dropout is checked separately through its Philox stream.
+Dropout: p=0 against the reference's golden vectors (its draws come from torch's RNG and cannot be
+replayed).  For training-mode parity with dropout on, `set_dropout_replay(fn)` installs a hook called
+at every dropout site of the reference — fn(site, x) -> dropout(x) — through which a test replays the
+HIP path's Philox masks (tests/test_dropout_parity_gpu.py).  Sites, in reference order:
+  ("emb",)               BertEmbeddings.dropout                    modeling_bert.py:107
+  ("attn_probs", i)      dropout(attn_weights)                     modeling_bert.py:131
+  ("attn_out", i)        BertSelfOutput.dropout                    modeling_bert.py:291
+  ("ffn_out", i)         BertOutput.dropout                        modeling_bert.py:349
+  ("dec_sa_w", d)        self-attention weight dropout (SDPA dropout_p)   transformer.py:1158-1176
+  ("dec_sa", d)          dropout1                                  transformer.py:1174
+  ("dec_ca_probs", d)    cross-attention weight dropout            transformer.py:1177-1196
+  ("dec_ca", d)          dropout2                                  transformer.py:1194
+  ("dec_ff_inner", d)    _ff_block's self.dropout                  transformer.py:1198
+  ("dec_ff", d)          dropout3                                  transformer.py:1199
 """
 from __future__ import annotations
 
@@ -44,6 +56,19 @@ class PathConfig:
     honor_dp_mode: bool = False  # PriConcat: apply DP_guarantee('feature_all_lap') (main_0430.py:76-85)
 
 
+_DROP = None
+
+
+def set_dropout_replay(fn) -> None:
+    """fn(site: tuple, x: Tensor) -> Tensor, or None for no dropout (the default)."""
+    global _DROP
+    _DROP = fn
+
+
+def _drop(site, x):
+    return x if _DROP is None else _DROP(site, x)
+
+
 # ------------------------------------------------------------------------------ BERT (a4)
 def _ln(x, w, b, eps):
     return F.layer_norm(x, (x.shape[-1],), w, b, eps)
@@ -60,7 +85,7 @@ def bert_embeddings(p, *, input_ids=None, inputs_embeds=None):
         inputs_embeds = p[pre + "word_embeddings.weight"][input_ids]
     L = inputs_embeds.shape[1]
     x = inputs_embeds + p[pre + "token_type_embeddings.weight"][0] + p[pre + "position_embeddings.weight"][:L]
-    return _ln(x, p[pre + "LayerNorm.weight"], p[pre + "LayerNorm.bias"], LN_BERT)
+    return _drop(("emb",), _ln(x, p[pre + "LayerNorm.weight"], p[pre + "LayerNorm.bias"], LN_BERT))
 
 
 def bert_layer(p, i, h, key_bias):
@@ -75,11 +100,11 @@ def bert_layer(p, i, h, key_bias):
     k = heads(_lin(h, p, pre + "attention.self.key"))
     v = heads(_lin(h, p, pre + "attention.self.value"))
     s = q @ k.transpose(-1, -2) * (DHEAD ** -0.5) + key_bias[:, None, None, :]
-    ctx = (s.softmax(-1) @ v).transpose(1, 2).reshape(B, L, HID)
-    a = _ln(_lin(ctx, p, pre + "attention.output.dense") + h,
+    ctx = (_drop(("attn_probs", i), s.softmax(-1)) @ v).transpose(1, 2).reshape(B, L, HID)
+    a = _ln(_drop(("attn_out", i), _lin(ctx, p, pre + "attention.output.dense")) + h,
             p[pre + "attention.output.LayerNorm.weight"], p[pre + "attention.output.LayerNorm.bias"], LN_BERT)
     f = F.gelu(_lin(a, p, pre + "intermediate.dense"))
-    return _ln(_lin(f, p, pre + "output.dense") + a,
+    return _ln(_drop(("ffn_out", i), _lin(f, p, pre + "output.dense")) + a,
                p[pre + "output.LayerNorm.weight"], p[pre + "output.LayerNorm.bias"], LN_BERT)
 
 
@@ -95,7 +120,7 @@ def bert(p, emb, attention_mask):
 
 
 # -------------------------------------------------------------------------- decoder (a5)
-def mha_literal(x, mem, in_w, in_b, out_w, out_b, key_padding_mask):
+def mha_literal(x, mem, in_w, in_b, out_w, out_b, key_padding_mask, site=None):
     """F.multi_head_attention_forward, batch-major: x [B,Lq,E], mem [B,S,E]; mask True = ignore."""
     B, Lq, E = x.shape
     S = mem.shape[1]
@@ -107,7 +132,10 @@ def mha_literal(x, mem, in_w, in_b, out_w, out_b, key_padding_mask):
     s = (q * DHEAD ** -0.5) @ k.transpose(-1, -2)
     if key_padding_mask is not None:
         s = s.masked_fill(key_padding_mask[:, None, None, :], float("-inf"))
-    ctx = (s.softmax(-1) @ v).transpose(1, 2).reshape(B, Lq, E)
+    w = s.softmax(-1)
+    if site is not None:
+        w = _drop(site, w)
+    ctx = (w @ v).transpose(1, 2).reshape(B, Lq, E)
     return F.linear(ctx, out_w, out_b)
 
 
@@ -115,13 +143,15 @@ def decoder_layer(p, i, x, mem, mem_pad, tgt_pad):
     """TransformerDecoderLayer.forward, norm_first=False (transformer.py:1158-1200)."""
     pre = f"multi_head_decoder.layers.{i}."
     sa = mha_literal(x, x, p[pre + "self_attn.in_proj_weight"], p[pre + "self_attn.in_proj_bias"],
-                     p[pre + "self_attn.out_proj.weight"], p[pre + "self_attn.out_proj.bias"], tgt_pad)
-    x = _ln(x + sa, p[pre + "norm1.weight"], p[pre + "norm1.bias"], LN_DEC)
+                     p[pre + "self_attn.out_proj.weight"], p[pre + "self_attn.out_proj.bias"], tgt_pad,
+                     site=("dec_sa_w", i))
+    x = _ln(x + _drop(("dec_sa", i), sa), p[pre + "norm1.weight"], p[pre + "norm1.bias"], LN_DEC)
     ca = mha_literal(x, mem, p[pre + "multihead_attn.in_proj_weight"], p[pre + "multihead_attn.in_proj_bias"],
-                     p[pre + "multihead_attn.out_proj.weight"], p[pre + "multihead_attn.out_proj.bias"], mem_pad)
-    x = _ln(x + ca, p[pre + "norm2.weight"], p[pre + "norm2.bias"], LN_DEC)
-    ff = _lin(F.relu(_lin(x, p, pre + "linear1")), p, pre + "linear2")
-    return _ln(x + ff, p[pre + "norm3.weight"], p[pre + "norm3.bias"], LN_DEC)
+                     p[pre + "multihead_attn.out_proj.weight"], p[pre + "multihead_attn.out_proj.bias"], mem_pad,
+                     site=("dec_ca_probs", i))
+    x = _ln(x + _drop(("dec_ca", i), ca), p[pre + "norm2.weight"], p[pre + "norm2.bias"], LN_DEC)
+    ff = _lin(_drop(("dec_ff_inner", i), F.relu(_lin(x, p, pre + "linear1"))), p, pre + "linear2")
+    return _ln(x + _drop(("dec_ff", i), ff), p[pre + "norm3.weight"], p[pre + "norm3.bias"], LN_DEC)
 
 
 def decoder(p, tgt, mem, mem_mask, tgt_mask):
