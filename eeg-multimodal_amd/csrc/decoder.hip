@@ -41,30 +41,51 @@ template <> DEV void store4<bf16>(bf16* p, const float (&v)[4]) {
   *(bf16x4*)p = o;
 }
 
-// out[b,h,j] = vec[b,h,:] . M[b,j,:] (+ kbias[b,j]); grid (ceil(S/64), B), 64 threads.
+// out[b,h,j] = vec[b,h,:] . M[b,j,:] (+ kbias[b,j]); grid (ceil(S/64), B), 256 threads:
+// lane = row j, wave w = column quarter [192w, 192w+192) (8 columns per 16-B step, next step's
+// row chunk prefetched), partial dot products reduced across the 4 waves through LDS.
 template <typename T, typename TV>
-__global__ void __launch_bounds__(64) xrow_dot_kernel(const T* __restrict__ mem, const TV* __restrict__ vec,
-                                                      const float* __restrict__ kbias, int S, float* __restrict__ out) {
-  const int b = blockIdx.y, j = blockIdx.x * 64 + threadIdx.x;
+__global__ void __launch_bounds__(256) xrow_dot_kernel(const T* __restrict__ mem, const TV* __restrict__ vec,
+                                                       const float* __restrict__ kbias, int S, float* __restrict__ out) {
+  constexpr int QW = E / 4;                       // 192 columns per wave
+  __shared__ float red[4][NH][64];
+  const int b = blockIdx.y, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + lane;
   const int jr = j < S ? j : S - 1;
-  const T* row = mem + ((long)b * S + jr) * E;
-  const TV* v = vec + (long)b * NH * E;
+  const int c0 = wave * QW;
+  const T* row = mem + ((long)b * S + jr) * E + c0;
+  const TV* v = vec + (long)b * NH * E + c0;
   float acc[NH];
 #pragma unroll
   for (int h = 0; h < NH; ++h) acc[h] = 0.f;
+  float nx[8];
+  load4<T>(row, *(float(*)[4])nx);
+  load4<T>(row + 4, *(float(*)[4])(nx + 4));
 #pragma unroll 1
-  for (int c = 0; c < E; c += 4) {       // 4 columns x 12 heads of v per step: 48 scalar registers
-    float m[4];
-    load4<T>(row + c, m);
+  for (int c = 0; c < QW; c += 8) {
+    float m[8];
 #pragma unroll
-    for (int h = 0; h < NH; ++h)
+    for (int e = 0; e < 8; ++e) m[e] = nx[e];
+    if (c + 8 < QW) {
+      load4<T>(row + c + 8, *(float(*)[4])nx);
+      load4<T>(row + c + 12, *(float(*)[4])(nx + 4));
+    }
 #pragma unroll
-      for (int e = 0; e < 4; ++e) acc[h] += m[e] * to_f32(v[h * E + c + e]);
+    for (int hf = 0; hf < 2; ++hf)                // 4 columns x 12 heads of v (scalar) per half-step
+#pragma unroll
+      for (int h = 0; h < NH; ++h)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[h] += m[4 * hf + e] * to_f32(v[h * E + c + 4 * hf + e]);
   }
-  if (j < S) {
-    const float kb = kbias ? kbias[(long)b * S + j] : 0.f;
 #pragma unroll
-    for (int h = 0; h < NH; ++h) out[((long)b * NH + h) * S + j] = acc[h] + kb;
+  for (int h = 0; h < NH; ++h) red[wave][h][lane] = acc[h];
+  __syncthreads();
+  for (int i = threadIdx.x; i < NH * 64; i += 256) {
+    const int h = i >> 6, l = i & 63, jj = blockIdx.x * 64 + l;
+    if (jj < S) {
+      const float kb = kbias ? kbias[(long)b * S + jj] : 0.f;
+      out[((long)b * NH + h) * S + jj] = red[0][h][l] + red[1][h][l] + red[2][h][l] + red[3][h][l] + kb;
+    }
   }
 }
 
@@ -72,8 +93,8 @@ __global__ void __launch_bounds__(64) xrow_dot_kernel(const T* __restrict__ mem,
 // workgroup slab 0 also stores the undropped p (for the backward) and s_h = sum_j p~.
 DEV void softmax_rows(const float* __restrict__ raw, int S, int b, float p_drop, uint64_t seed, uint64_t offset,
                       bool write, float* __restrict__ probs, float* __restrict__ psum, float* pt) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int h = wave; h < NH; h += 4) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int h = wave; h < NH; h += nw) {
     const float* r = raw + ((long)b * NH + h) * S;
     float mx = -3.0e38f;
     for (int j = lane; j < S; j += 64) mx = fmaxf(mx, r[j]);
@@ -102,9 +123,34 @@ DEV void lds_row12(const float* base, float (&v)[NH]) {
   }
 }
 
-// grid (E/256, B), 256 threads: lane owns 4 columns of the slab, wave w rows [w*S/4, (w+1)*S/4).
+// Sum of the 8 waves' [12][4-column] partials in red[4][12][256]: waves 4-7 park theirs, waves 0-3
+// add their own in place; the caller then sums the 4 slices (fixed order: deterministic).
+DEV void reduce8_waves(const float (&acc)[NH][4], float* red, int wave, int lane) {
+  if (wave >= 4) {
+#pragma unroll
+    for (int h = 0; h < NH; ++h)
+      *(float4*)(red + ((wave - 4) * NH + h) * SLAB + lane * 4) = float4{acc[h][0], acc[h][1], acc[h][2], acc[h][3]};
+  }
+  __syncthreads();
+  if (wave < 4) {
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+      float4* q = (float4*)(red + (wave * NH + h) * SLAB + lane * 4);
+      const float4 o = *q;
+      *q = float4{o.x + acc[h][0], o.y + acc[h][1], o.z + acc[h][2], o.w + acc[h][3]};
+    }
+  }
+  __syncthreads();
+}
+DEV float red4(const float* red, int h, int c) {
+  return red[(0 * NH + h) * SLAB + c] + red[(1 * NH + h) * SLAB + c] + red[(2 * NH + h) * SLAB + c] +
+         red[(3 * NH + h) * SLAB + c];
+}
+
+// grid (E/256, B), 512 threads: lane owns 4 columns of the slab, wave w rows [w*S/8, (w+1)*S/8);
+// the 8 per-wave partial contexts are summed in two rounds through a [4][12][256] LDS buffer.
 template <typename T, typename TQ>
-__global__ void __launch_bounds__(256) xctx_kernel(const T* __restrict__ mem, const float* __restrict__ raw, int S,
+__global__ void __launch_bounds__(512) xctx_kernel(const T* __restrict__ mem, const float* __restrict__ raw, int S,
                                                    float p_drop, uint64_t seed, uint64_t offset,
                                                    float* __restrict__ probs, float* __restrict__ psum,
                                                    TQ* __restrict__ ctx) {
@@ -120,9 +166,9 @@ __global__ void __launch_bounds__(256) xctx_kernel(const T* __restrict__ mem, co
   for (int h = 0; h < NH; ++h)
 #pragma unroll
     for (int e = 0; e < 4; ++e) acc[h][e] = 0.f;
-  const int per = (S + 3) / 4, j0 = wave * per, j1 = min(S, j0 + per);
+  const int per = (S + 7) / 8, j0 = wave * per, j1 = min(S, j0 + per);
   const T* M = mem + (long)b * S * E + col;
-#pragma unroll 2
+#pragma unroll 4
   for (int j = j0; j < j1; ++j) {
     float m[4], p[NH];
     load4<T>(M + (long)j * E, m);
@@ -132,16 +178,10 @@ __global__ void __launch_bounds__(256) xctx_kernel(const T* __restrict__ mem, co
 #pragma unroll
       for (int e = 0; e < 4; ++e) acc[h][e] += p[h] * m[e];
   }
-#pragma unroll
-  for (int h = 0; h < NH; ++h)
-    *(float4*)(red + (wave * NH + h) * SLAB + lane * 4) = float4{acc[h][0], acc[h][1], acc[h][2], acc[h][3]};
-  __syncthreads();
-  // 12 heads x 256 columns = 3072 outputs, 12 per thread
-  for (int i = tid; i < NH * SLAB; i += 256) {
+  reduce8_waves(acc, red, wave, lane);
+  for (int i = tid; i < NH * SLAB; i += 512) {
     const int h = i / SLAB, c = i % SLAB;
-    const float v = red[(0 * NH + h) * SLAB + c] + red[(1 * NH + h) * SLAB + c] + red[(2 * NH + h) * SLAB + c] +
-                    red[(3 * NH + h) * SLAB + c];
-    ctx[((long)b * NH + h) * E + blockIdx.x * SLAB + c] = from_f32<TQ>(v);
+    ctx[((long)b * NH + h) * E + blockIdx.x * SLAB + c] = from_f32<TQ>(red4(red, h, c));
   }
 }
 
@@ -149,7 +189,7 @@ __global__ void __launch_bounds__(256) xctx_kernel(const T* __restrict__ mem, co
 //   dp~ = raw + dpsum;  dp = dp~ * mask;  dsc = p (dp - sum_j p dp)
 //   dq'[h,c] = sum_j dsc[h][j] M[j][c];   dM[j][c] (+)= sum_h p~[h][j] dc[h][c] + dsc[h][j] q'[h][c]
 template <typename T, typename TQ>
-__global__ void __launch_bounds__(256) xbwd_cols_kernel(const T* __restrict__ mem, const TQ* __restrict__ qp,
+__global__ void __launch_bounds__(512) xbwd_cols_kernel(const T* __restrict__ mem, const TQ* __restrict__ qp,
                                                         const float* __restrict__ probs, const float* __restrict__ raw,
                                                         const float* __restrict__ dpsum, const TQ* __restrict__ dc, int S,
                                                         float p_drop, uint64_t seed, uint64_t offset,
@@ -159,7 +199,7 @@ __global__ void __launch_bounds__(256) xbwd_cols_kernel(const T* __restrict__ me
   float* st = sm + S * NH;        // [S][12] dsc
   float* red = st + S * NH;       // [4][12][256]
   const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int h = wave; h < NH; h += 4) {
+  for (int h = wave; h < NH; h += 8) {
     const float* pr = probs + ((long)b * NH + h) * S;
     const float* dr = raw + ((long)b * NH + h) * S;
     const float dsh = dpsum ? dpsum[b * NH + h] : 0.f;
@@ -184,9 +224,10 @@ __global__ void __launch_bounds__(256) xbwd_cols_kernel(const T* __restrict__ me
 #pragma unroll
     for (int e = 0; e < 4; ++e) acc[h][e] = 0.f;
   }
-  const int per = (S + 3) / 4, j0 = wave * per, j1 = min(S, j0 + per);
+  const int per = (S + 7) / 8, j0 = wave * per, j1 = min(S, j0 + per);
   const T* M = mem + (long)b * S * E + col;
   T* dM = dmem + (long)b * S * E + col;
+#pragma unroll 2
   for (int j = j0; j < j1; ++j) {
     float m[4], p[NH], d[NH], o[4] = {0.f, 0.f, 0.f, 0.f};
     load4<T>(M + (long)j * E, m);
@@ -207,15 +248,10 @@ __global__ void __launch_bounds__(256) xbwd_cols_kernel(const T* __restrict__ me
     }
     store4<T>(dM + (long)j * E, o);
   }
-#pragma unroll
-  for (int h = 0; h < NH; ++h)
-    *(float4*)(red + (wave * NH + h) * SLAB + lane * 4) = float4{acc[h][0], acc[h][1], acc[h][2], acc[h][3]};
-  __syncthreads();
-  for (int i = tid; i < NH * SLAB; i += 256) {
+  reduce8_waves(acc, red, wave, lane);
+  for (int i = tid; i < NH * SLAB; i += 512) {
     const int h = i / SLAB, c = i % SLAB;
-    const float v = red[(0 * NH + h) * SLAB + c] + red[(1 * NH + h) * SLAB + c] + red[(2 * NH + h) * SLAB + c] +
-                    red[(3 * NH + h) * SLAB + c];
-    dqp[((long)b * NH + h) * E + blockIdx.x * SLAB + c] = from_f32<TQ>(v);
+    dqp[((long)b * NH + h) * E + blockIdx.x * SLAB + c] = from_f32<TQ>(red4(red, h, c));
   }
 }
 
@@ -227,42 +263,53 @@ __global__ void __launch_bounds__(256) head_bias_fwd_kernel(int B, int W, int gr
   const int b = (int)(i / W), c = (int)(i % W);
   x[i] += bias[c] * s[(long)b * (W / group) + c / group];
 }
-// ds[b, g] = sum_{c in g} dx[b,c] bias[c];  dbias[c] = beta*dbias[c] + sum_b dx[b,c] s[b, c/group]
-// grid W/64 workgroups of one wave (group == 64: one head per workgroup).
-__global__ void __launch_bounds__(64) head_bias_bwd_kernel(int B, int W, const float* __restrict__ dx,
-                                                           const float* __restrict__ bias, const float* __restrict__ s,
-                                                           float* __restrict__ ds, float* __restrict__ dbias, float beta) {
-  const int g = blockIdx.x, c = g * 64 + threadIdx.x;
-  const float bc = bias[c];
-  float acc = 0.f;
-  for (int b = 0; b < B; ++b) {
-    const float d = dx[(long)b * W + c];
-    acc += d * s[(long)b * (W / 64) + g];
-    const float t = wave_sum(d * bc);
-    if (threadIdx.x == 0) ds[(long)b * (W / 64) + g] = t;
+// ds[b, g] = sum_{c in g} dx[b,c] bias[c]: grid B, 256 threads (thread t: columns t, t+256, t+512;
+// wave w reduces heads w, w+4, w+8).
+__global__ void __launch_bounds__(256) head_bias_ds_kernel(int W, const float* __restrict__ dx,
+                                                           const float* __restrict__ bias, float* __restrict__ ds) {
+  const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  for (int k = 0; k < W / 256; ++k) {
+    const int c = t + 256 * k;
+    const float v = wave_sum(dx[(long)b * W + c] * bias[c]);
+    if (lane == 0) ds[(long)b * (W / 64) + 4 * k + wave] = v;
   }
-  if (dbias) dbias[c] = acc + (beta != 0.f ? beta * dbias[c] : 0.f);
+}
+// dbias[c] = beta*dbias[c] + sum_b dx[b,c] s[b, c/64]: grid W/64, 256 threads (wave w: rows w, w+4, ..).
+__global__ void __launch_bounds__(256) head_bias_db_kernel(int B, int W, const float* __restrict__ dx,
+                                                           const float* __restrict__ s, float* __restrict__ dbias,
+                                                           float beta) {
+  __shared__ float red[4][64];
+  const int g = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = g * 64 + lane;
+  float acc = 0.f;
+#pragma unroll 8
+  for (int b = wave; b < B; b += 4) acc += dx[(long)b * W + c] * s[(long)b * (W / 64) + g];
+  red[wave][lane] = acc;
+  __syncthreads();
+  if (wave == 0) {
+    const float v = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    dbias[c] = v + (beta != 0.f ? beta * dbias[c] : 0.f);
+  }
 }
 
 template <typename T, typename TQ>
 int xfwd(int B, int S, const void* mem, const void* qp, const float* kb, float p, uint64_t seed, uint64_t off,
          float* ws, float* probs, float* psum, void* ctx, hipStream_t st) {
-  hipLaunchKernelGGL((xrow_dot_kernel<T, TQ>), dim3((S + 63) / 64, B), dim3(64), 0, st, (const T*)mem, (const TQ*)qp,
+  hipLaunchKernelGGL((xrow_dot_kernel<T, TQ>), dim3((S + 63) / 64, B), dim3(256), 0, st, (const T*)mem, (const TQ*)qp,
                      kb, S, ws);
   const size_t lds = sizeof(float) * ((size_t)S * NH + 4 * NH * SLAB);
   hipFuncSetAttribute((const void*)xctx_kernel<T, TQ>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((xctx_kernel<T, TQ>), dim3(E / SLAB, B), dim3(256), lds, st, (const T*)mem, ws, S, p, seed, off,
+  hipLaunchKernelGGL((xctx_kernel<T, TQ>), dim3(E / SLAB, B), dim3(512), lds, st, (const T*)mem, ws, S, p, seed, off,
                      probs, psum, (TQ*)ctx);
   return (int)hipGetLastError();
 }
 template <typename T, typename TQ>
 int xbwd(int B, int S, const void* mem, const void* qp, const float* probs, const float* dpsum, const void* dctx,
          float p, uint64_t seed, uint64_t off, float* ws, void* dmem, float beta, void* dqp, hipStream_t st) {
-  hipLaunchKernelGGL((xrow_dot_kernel<T, TQ>), dim3((S + 63) / 64, B), dim3(64), 0, st, (const T*)mem,
+  hipLaunchKernelGGL((xrow_dot_kernel<T, TQ>), dim3((S + 63) / 64, B), dim3(256), 0, st, (const T*)mem,
                      (const TQ*)dctx, (const float*)nullptr, S, ws);
   const size_t lds = sizeof(float) * ((size_t)2 * S * NH + 4 * NH * SLAB);
   hipFuncSetAttribute((const void*)xbwd_cols_kernel<T, TQ>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((xbwd_cols_kernel<T, TQ>), dim3(E / SLAB, B), dim3(256), lds, st, (const T*)mem, (const TQ*)qp,
+  hipLaunchKernelGGL((xbwd_cols_kernel<T, TQ>), dim3(E / SLAB, B), dim3(512), lds, st, (const T*)mem, (const TQ*)qp,
                      probs, ws, dpsum, (const TQ*)dctx, S, p, seed, off, (T*)dmem, beta, (TQ*)dqp);
   return (int)hipGetLastError();
 }
@@ -310,7 +357,8 @@ extern "C" int eegf_head_bias_fwd(int B, int W, int group, float* x, const float
 
 extern "C" int eegf_head_bias_bwd(int B, int W, int group, const float* dx, const float* bias, const float* s,
                                   float* ds, float* dbias, float beta, hipStream_t stream) {
-  if (B <= 0 || W <= 0 || group != 64 || W % 64 != 0 || !dx || !bias || !s || !ds) return EEGF_ERR_ARG;
-  hipLaunchKernelGGL(head_bias_bwd_kernel, dim3(W / 64), dim3(64), 0, stream, B, W, dx, bias, s, ds, dbias, beta);
+  if (B <= 0 || W <= 0 || group != 64 || W % 256 != 0 || !dx || !bias || !s || !ds) return EEGF_ERR_ARG;
+  hipLaunchKernelGGL(head_bias_ds_kernel, dim3(B), dim3(256), 0, stream, W, dx, bias, ds);
+  if (dbias) hipLaunchKernelGGL(head_bias_db_kernel, dim3(W / 64), dim3(256), 0, stream, B, W, dx, s, dbias, beta);
   return (int)hipGetLastError();
 }

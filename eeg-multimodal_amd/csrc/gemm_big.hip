@@ -11,7 +11,11 @@
 //   * XOR-swizzled LDS images written lane-linearly (swizzle applied to the SOURCE address):
 //     row-major [256][64] operands use chunk ^= (row>>1)&7 (conflict-free ds_read_b128); k-major
 //     [64][256] operands use chunk ^= 2*((k&3) | ((k>>3)&1)<<2) (spread ds_read_b64_tr_b16);
-//   * XCD-aware tile order; LDS-staged coalesced epilogue (bias, GELU / act' from aux).
+//   * XCD-aware tile order; LDS-staged coalesced epilogue (bias, GELU / act' from aux);
+//   * optional fused column sums of a K-contiguous A (the bias gradient of an input-gradient
+//     GEMM, colsum over the token rows of dY): workgroups of tile column 0 sum each staged A tile
+//     (in-wave shuffles, then 8 waves through 4 KB of LDS left free by the operand buffers) and
+//     write one fp32 partial row per 256-row tile: colsum_part[tile_m][K].
 // Edges: rows/cols beyond M/N are clamped to valid memory and never stored; K % 64 == 0.
 #include "common.h"
 #include "eegfusion_internal.h"
@@ -29,6 +33,7 @@ struct BigArgs {
   int M, N, K;
   float alpha, beta, epi_scale;
   int ksplit;            // >0: split-K slice length; C = fp32 slabs [blockIdx.y][M][N]
+  float* colsum_part;    // AKC only: [tiles_m][K] partial column sums of A (nullable)
 };
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -118,65 +123,11 @@ DEV void tile_io(bf16* lds, bf16* gp, long ld, int m0, int n0, int M, int N, int
 DEV void ld4(const bf16* p, float (&v)[4]) { const bf16x4 x = *(const bf16x4*)p; v[0] = (float)x[0]; v[1] = (float)x[1]; v[2] = (float)x[2]; v[3] = (float)x[3]; }
 DEV void st4(bf16* p, const float (&v)[4]) { bf16x4 x; x[0] = (bf16)v[0]; x[1] = (bf16)v[1]; x[2] = (bf16)v[2]; x[3] = (bf16)v[3]; *(bf16x4*)p = x; }
 
-template <bool AKC, bool BKC, int EPI, typename TO>
-__global__ void __launch_bounds__(NT, 1) gemm_big_kernel(BigArgs g) {
-  __shared__ __attribute__((aligned(16))) bf16 lds[LDS_ELEMS];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 2, wn = wave & 3;
-  const int tiles_n = (g.N + TN - 1) / TN, tiles_m = (g.M + TM - 1) / TM;
-  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int tm = t / tiles_n, tn = t % tiles_n;
-  const int m0 = tm * TM, n0 = tn * TN;
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  int kbeg = 0, kend = g.K;
-  if (g.ksplit > 0) { kbeg = blockIdx.y * g.ksplit; kend = min(g.K, kbeg + g.ksplit); }
-  const int nk = (kend - kbeg) / BK;
-  if (AKC) stage_rowmajor(lds, g.A, g.lda, m0, g.M, kbeg, wave, lane);
-  else stage_kmajor(lds, g.A, g.lda, m0, g.M, kbeg, wave, lane);
-  if (BKC) stage_rowmajor(lds + TILE, g.B, g.ldb, n0, g.N, kbeg, wave, lane);
-  else stage_kmajor(lds + TILE, g.B, g.ldb, n0, g.N, kbeg, wave, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = (kt & 1) * 2 * TILE, nxt = 2 * TILE - cur;
-    if (kt + 1 < nk) {
-      const int kn = kbeg + (kt + 1) * BK;
-      if (AKC) stage_rowmajor(lds + nxt, g.A, g.lda, m0, g.M, kn, wave, lane);
-      else stage_kmajor(lds + nxt, g.A, g.lda, m0, g.M, kn, wave, lane);
-      if (BKC) stage_rowmajor(lds + nxt + TILE, g.B, g.ldb, n0, g.N, kn, wave, lane);
-      else stage_kmajor(lds + nxt + TILE, g.B, g.ldb, n0, g.N, kn, wave, lane);
-    }
-    const bf16* As = lds + cur;
-    const bf16* Bs = lds + cur + TILE;
-#pragma unroll
-    for (int kc = 0; kc < 2; ++kc) {
-      bf16x8 b[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c = wn * 64 + j * 16;
-        if (BKC) b[j] = rd_row(Bs, c + (lane & 15), 4 * kc + (lane >> 4));
-        else b[j] = rd_col(Bs, 32 * kc + 8 * (lane >> 4), c, lane);
-      }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const bf16x8 a = AKC ? rd_row(As, wm * 128 + i * 16 + (lane & 15), 4 * kc + (lane >> 4))
-                             : rd_col(As, 32 * kc + 8 * (lane >> 4), wm * 128 + i * 16, lane);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mma16(b[j], a, acc[i][j]);
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-
-  // ---- epilogue ----
+// Shared epilogue of the 256x256 kernels: acc[i][j] holds rows wm*128 + 16i + (lane&15), columns
+// wn*64 + 16j + 4*(lane>>4) + 0..3 of the block tile (m0, n0).
+template <int EPI, typename TO>
+DEV void big_epilogue(const BigArgs& g, f32x4 (&acc)[8][4], bf16* lds, int m0, int n0, int tid, int lane, int wm,
+                      int wn) {
   constexpr bool HAS_BIAS = EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_TANH;
   constexpr bool AUX_IN = EPI == EPI_DGELU || EPI == EPI_DRELU || EPI == EPI_DTANH;
   if constexpr (sizeof(TO) == 4) {
@@ -259,9 +210,275 @@ __global__ void __launch_bounds__(NT, 1) gemm_big_kernel(BigArgs g) {
   }
 }
 
+template <bool AKC, bool BKC, int EPI, typename TO, bool CS = false>
+__global__ void __launch_bounds__(NT, 1) gemm_big_kernel(BigArgs g) {
+  __shared__ __attribute__((aligned(16))) bf16 lds[LDS_ELEMS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int tiles_n = (g.N + TN - 1) / TN, tiles_m = (g.M + TM - 1) / TM;
+  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int tm = t / tiles_n, tn = t % tiles_n;
+  const int m0 = tm * TM, n0 = tn * TN;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  int kbeg = 0, kend = g.K;
+  if (g.ksplit > 0) { kbeg = blockIdx.y * g.ksplit; kend = min(g.K, kbeg + g.ksplit); }
+  const int nk = (kend - kbeg) / BK;
+  if (AKC) stage_rowmajor(lds, g.A, g.lda, m0, g.M, kbeg, wave, lane);
+  else stage_kmajor(lds, g.A, g.lda, m0, g.M, kbeg, wave, lane);
+  if (BKC) stage_rowmajor(lds + TILE, g.B, g.ldb, n0, g.N, kbeg, wave, lane);
+  else stage_kmajor(lds + TILE, g.B, g.ldb, n0, g.N, kbeg, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // fused A column sums (tile column 0 only): red[parity][wave][64] in the LDS tail
+  const bool do_cs = CS && AKC && tn == 0;
+  float* red = (float*)(lds + 4 * TILE);
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = (kt & 1) * 2 * TILE, nxt = 2 * TILE - cur;
+    if (kt + 1 < nk) {
+      const int kn = kbeg + (kt + 1) * BK;
+      if (AKC) stage_rowmajor(lds + nxt, g.A, g.lda, m0, g.M, kn, wave, lane);
+      else stage_kmajor(lds + nxt, g.A, g.lda, m0, g.M, kn, wave, lane);
+      if (BKC) stage_rowmajor(lds + nxt + TILE, g.B, g.ldb, n0, g.N, kn, wave, lane);
+      else stage_kmajor(lds + nxt + TILE, g.B, g.ldb, n0, g.N, kn, wave, lane);
+    }
+    const bf16* As = lds + cur;
+    const bf16* Bs = lds + cur + TILE;
+#pragma unroll
+    for (int kc = 0; kc < 2; ++kc) {
+      bf16x8 b[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = wn * 64 + j * 16;
+        if (BKC) b[j] = rd_row(Bs, c + (lane & 15), 4 * kc + (lane >> 4));
+        else b[j] = rd_col(Bs, 32 * kc + 8 * (lane >> 4), c, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const bf16x8 a = AKC ? rd_row(As, wm * 128 + i * 16 + (lane & 15), 4 * kc + (lane >> 4))
+                             : rd_col(As, 32 * kc + 8 * (lane >> 4), wm * 128 + i * 16, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mma16(b[j], a, acc[i][j]);
+      }
+    }
+    if (CS) __builtin_amdgcn_sched_barrier(0);     // keep the sums out of the MFMA schedule
+    if (CS && do_cs) {
+      if (kt > 0 && tid < 64) {      // previous k-step's 8 wave partials (ordered by the barrier)
+        const float* rp = red + ((kt - 1) & 1) * 8 * 64;
+        float v = 0.f;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) v += rp[w * 64 + tid];
+        g.colsum_part[(long)tm * g.K + kbeg + (kt - 1) * BK + tid] = v;
+      }
+      const int kc = lane & 7, rg = tid >> 3;          // 8-k chunk, 4-row group
+#pragma unroll 1
+      for (int hf = 0; hf < 2; ++hf) {                 // 4 k-values at a time (register budget)
+        float s[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int r = rg * 4 + q;
+          if (m0 + r < g.M) {
+            const bf16x8 v = rd_row(As, r, kc);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) s[e] += (float)v[4 * hf + e];
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          s[e] += __shfl_xor(s[e], 8, 64);
+          s[e] += __shfl_xor(s[e], 16, 64);
+          s[e] += __shfl_xor(s[e], 32, 64);
+        }
+        if (lane < 8) *(f32x4*)(red + (kt & 1) * 8 * 64 + wave * 64 + kc * 8 + 4 * hf) = f32x4{s[0], s[1], s[2], s[3]};
+      }
+    }
+    if (CS) __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (CS && do_cs && tid < 64) {
+    const float* rp = red + ((nk - 1) & 1) * 8 * 64;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) v += rp[w * 64 + tid];
+    g.colsum_part[(long)tm * g.K + kbeg + (nk - 1) * BK + tid] = v;
+  }
+  if (CS) __syncthreads();         // the epilogue reuses the LDS tail
+
+  big_epilogue<EPI, TO>(g, acc, lds, m0, n0, tid, lane, wm, wn);
+}
+
+// ---------------------------------------------------------------------------------------------
+// 8-phase schedule for A and B both K-contiguous (the forward x W^T GEMMs), after the structure of
+// cdna_hip_programming.md §5 "The 256² 8-phase template": the two wave groups (wm = 0 / 1, one wave
+// of each per SIMD) run staggered by one barrier, so one group's MFMAs overlap the other's LDS
+// reads and staging; operands are staged in 16 KB half-tiles, one per phase, and retired with a
+// counted vmcnt (never 0 in the loop) under raw s_barriers.
+//   Half-tiles of K-tile t (buffer t&1): A_h0 = rows {0..63, 128..191}, A_h1 = rows {64..127,
+//   192..255} (the wave's m-quadrant 0 / 1), B_h0 / B_h1 = the wave's n-quadrant 0 / 1 (columns
+//   64w + 32h + 0..31).  Phase p of tile t computes quadrant (mh, nh) = (0,0) (0,1) (1,1) (1,0):
+//     reads  P0: A_h0 + B_h0    P1: B_h1    P2: A_h1    P3: -        (64 fragment VGPRs)
+//     stages P0: B_h1(t+1)  P1: A_h1(t+1)  P2: A_h0(t+2)  P3: B_h0(t+2)
+//   Every stage lands >= 2 phases after the last read of the half it overwrites (WAR with the
+//   stagger); each phase's vmcnt retires the half staged 4 phases earlier, read >= 1 phase later.
+constexpr int HALF = 128 * BK;                // elements per half-tile (16 KB)
+int g_gemm8 = [] { const char* e = getenv("EEGF_GEMM8"); return e ? atoi(e) : 0; }();
+
+DEV void stage_half(bf16* dst, const bf16* src, long ld, int base, int sh, int stride, int off, int rmax, int k0,
+                    int wave, int lane) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int R0 = (wave * 2 + j) * 8;
+    const int l = R0 + (lane >> 3);
+    const int c = (lane & 7) ^ swz_row(l);
+    const int gr = min(base + (l >> sh) * stride + off + (l & ((1 << sh) - 1)), rmax - 1);
+    glds16(src + (long)gr * ld + k0 + c * 8, dst + R0 * BK);
+  }
+}
+
+DEV void vm_wait(int n) {      // s_waitcnt vmcnt(2n), n = younger half-tiles in flight (0..4)
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+  }
+}
+DEV void raw_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int EPI, typename TO, int MODE>      // MODE 1: staggered groups; 2: lockstep; 3: staggered, no setprio
+__global__ void __launch_bounds__(NT, 1) gemm8_kernel(BigArgs g) {
+  constexpr bool STAG = MODE != 2, PRIO = MODE != 3;
+  __shared__ __attribute__((aligned(16))) bf16 lds[LDS_ELEMS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int tiles_n = (g.N + TN - 1) / TN, tiles_m = (g.M + TM - 1) / TM;
+  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int tm = t / tiles_n, tn = t % tiles_n;
+  const int m0 = tm * TM, n0 = tn * TN;
+  const int nk = g.K / BK;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // half-tile slots: buffer b at b*4*HALF: [A_h0][A_h1][B_h0][B_h1]
+  auto stageA = [&](int tile, int h) {
+    stage_half(lds + (tile & 1) * 4 * HALF + h * HALF, g.A, g.lda, m0, 6, 128, 64 * h, g.M, tile * BK, wave, lane);
+  };
+  auto stageB = [&](int tile, int h) {
+    stage_half(lds + (tile & 1) * 4 * HALF + (2 + h) * HALF, g.B, g.ldb, n0, 5, 64, 32 * h, g.N, tile * BK, wave,
+               lane);
+  };
+  // global phase phi = 4t + p stages: p0 B_h1(t+1), p1 A_h1(t+1), p2 A_h0(t+2), p3 B_h0(t+2)
+  auto stage_tile_of = [&](int phi) { const int tt = phi >> 2, p = phi & 3; return tt + (p <= 1 ? 1 : 2); };
+  auto stage_phase = [&](int phi) {
+    const int tt = stage_tile_of(phi), p = phi & 3;
+    if (tt >= nk) return;
+    if (p == 0) stageB(tt, 1);
+    else if (p == 1) stageA(tt, 1);
+    else if (p == 2) stageA(tt, 0);
+    else stageB(tt, 0);
+  };
+  auto younger = [&](int phi) {       // real stages among phases phi-3 .. phi
+    int n = 0;
+#pragma unroll
+    for (int x = 0; x < 4; ++x) n += stage_tile_of(phi - x) < nk ? 1 : 0;
+    return n;
+  };
+
+  // prologue = the stages of phases -6 .. -1
+  for (int phi = -6; phi < 0; ++phi) stage_phase(phi);
+  vm_wait(younger(-1));               // retires phases -6, -5 (A_h0(0), B_h0(0))
+  raw_barrier();
+  if (STAG && wm == 1) raw_barrier();  // stagger group 1 by one barrier
+
+  bf16x8 ar[4][2], br0[2][2], br1[2][2];
+  for (int kt = 0; kt < nk; ++kt) {
+    const bf16* Ab = lds + (kt & 1) * 4 * HALF;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int phi = 4 * kt + p;
+      // (a) fragment reads of this phase's quadrant
+      if (p == 0) {
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+          for (int kc = 0; kc < 2; ++kc) br0[jj][kc] = rd_row(Ab + 2 * HALF, wn * 32 + jj * 16 + (lane & 15), 4 * kc + (lane >> 4));
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (p == 1) {
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+          for (int kc = 0; kc < 2; ++kc) br1[jj][kc] = rd_row(Ab + 3 * HALF, wn * 32 + jj * 16 + (lane & 15), 4 * kc + (lane >> 4));
+      }
+      if (p == 0 || p == 2) {
+        const bf16* Ah = Ab + (p == 0 ? 0 : HALF);
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+          for (int kc = 0; kc < 2; ++kc) ar[ii][kc] = rd_row(Ah, wm * 64 + ii * 16 + (lane & 15), 4 * kc + (lane >> 4));
+      }
+      // (b) stage one half-tile, (c) retire the one staged 4 phases ago
+      stage_phase(phi);
+      vm_wait(younger(phi));
+      raw_barrier();
+      // (e) the quadrant's 16 MFMAs
+      const int mh = (p == 0 || p == 1) ? 0 : 1, nh = (p == 1 || p == 2) ? 1 : 0;
+      if (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+          for (int kc = 0; kc < 2; ++kc) {
+            const bf16x8 bv = nh == 0 ? br0[jj][kc] : br1[jj][kc];
+            acc[mh * 4 + ii][nh * 2 + jj] = mma16(bv, ar[ii][kc], acc[mh * 4 + ii][nh * 2 + jj]);
+          }
+      if (PRIO) __builtin_amdgcn_s_setprio(0);
+      if (STAG) raw_barrier();
+    }
+  }
+  if (STAG && wm == 0) raw_barrier();  // re-align the groups
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // acc[i][j]: i = 4*mh + ii -> rows wm*128 + 64*mh + 16*ii = wm*128 + 16*i (same map as gemm_big)
+  big_epilogue<EPI, TO>(g, acc, lds, m0, n0, tid, lane, wm, wn);
+}
+
 template <bool AKC, bool BKC, int EPI, typename TO>
 int launch_big(const BigArgs& a, int splits, hipStream_t s) {
   const int tiles = ((a.M + TM - 1) / TM) * ((a.N + TN - 1) / TN);
+  if constexpr (AKC && BKC && sizeof(TO) == 2) {
+    if (g_gemm8 && !a.colsum_part && splits == 1) {
+      if (g_gemm8 == 2) hipLaunchKernelGGL((gemm8_kernel<EPI, TO, 2>), dim3(tiles), dim3(NT), 0, s, a);
+      else if (g_gemm8 == 3) hipLaunchKernelGGL((gemm8_kernel<EPI, TO, 3>), dim3(tiles), dim3(NT), 0, s, a);
+      else hipLaunchKernelGGL((gemm8_kernel<EPI, TO, 1>), dim3(tiles), dim3(NT), 0, s, a);
+      return (int)hipGetLastError();
+    }
+  }
+  if constexpr (AKC && !BKC && sizeof(TO) == 2) {
+    if (a.colsum_part) {
+      hipLaunchKernelGGL((gemm_big_kernel<AKC, BKC, EPI, TO, true>), dim3(tiles, splits), dim3(NT), 0, s, a);
+      return (int)hipGetLastError();
+    }
+  }
+  if (a.colsum_part) return EEGF_ERR_ARG;
   hipLaunchKernelGGL((gemm_big_kernel<AKC, BKC, EPI, TO>), dim3(tiles, splits), dim3(NT), 0, s, a);
   return (int)hipGetLastError();
 }
@@ -286,12 +503,13 @@ __global__ void __launch_bounds__(256) big_splitk_reduce(const float* __restrict
 //             in `workspace` reduced in a fixed order (bitwise reproducible), beta applied once.
 int eegf_gemm_big(int a_kc, int b_kc, int epi, int out_f32, int M, int N, int K, const void* A, long lda,
                   const void* B, long ldb, void* C, long ldc, const float* bias, void* aux, long ldaux, float alpha,
-                  float beta, float epi_scale, void* workspace, long ws_bytes, hipStream_t stream) {
+                  float beta, float epi_scale, void* workspace, long ws_bytes, float* a_colsum, hipStream_t stream) {
   if (K % BK != 0 || M % 8 != 0 || N % 8 != 0) return 1;
   if (lda % 8 || ldb % 8 || ldc % 8 || (aux && ldaux % 8)) return 1;
   if ((((uintptr_t)A | (uintptr_t)B | (uintptr_t)C | (uintptr_t)aux) & 15) != 0) return 1;
   BigArgs a{(const bf16*)A, (const bf16*)B, C, bias, (bf16*)aux, lda, ldb, ldc, ldaux, M, N, K, alpha, beta,
-            epi_scale, 0};
+            epi_scale, 0, a_colsum};
+  if (a_colsum && (!a_kc || out_f32)) return 1;
   if (out_f32) {
     if (a_kc || b_kc || epi != EPI_NONE || M < 256 || N < 256 || K < 4096 || ldc % 4) return 1;
     const int tiles = ((M + TM - 1) / TM) * ((N + TN - 1) / TN);
@@ -335,4 +553,17 @@ int eegf_gemm_big(int a_kc, int b_kc, int epi, int out_f32, int M, int N, int K,
     }
   }
   return 1;
+}
+
+// Row-tile count of the fused A column sums (rows of the a_colsum partial buffer) when eegf_gemm
+// would take the 256x256 path for this shape with a K-contiguous A and bf16 output, else 0.
+int eegf_gemm_big_colsum_tiles(int M, int N, int K) {
+  if (K % BK != 0 || M % 8 != 0 || N % 8 != 0 || M < 2048 || N < 256) return 0;
+  return (M + TM - 1) / TM;
+}
+
+// Tuning/A-B hook: key 1 = 8-phase schedule for the forward GEMMs (1 on, 0 off).  Returns the old value.
+extern "C" int eegf_tune(int key, int value) {
+  if (key == 1) { const int o = g_gemm8; g_gemm8 = value; return o; }
+  return EEGF_ERR_ARG;
 }

@@ -164,10 +164,30 @@ class FusionEngine:
             e2.record()
             self.probe[tag].append((ev, e2))
 
-    def dgrad(self, dy, w, out, M, ldd=None, ldo=None, epi=_lib.EPI_NONE, aux=None, scale=1.0, beta=0.0):
+    def dgrad(self, dy, w, out, M, ldd=None, ldo=None, epi=_lib.EPI_NONE, aux=None, scale=1.0, beta=0.0,
+              bias_grad=None):
+        """out = dy W (* act'(aux)) (+ beta out).  bias_grad: fp32 tensor that receives += dy.sum(0) —
+        fused into the GEMM (per-256-row-tile column sums of dy, eegf_gemm_acs) when the shape takes
+        the 256x256 path, else a separate column reduction."""
         N, K = w.shape
-        return self.gemm(dy, w, out, M, K, N, 1, 0, ldd or N, K, ldo or K, epi=epi, aux=aux,
-                         ldaux=(aux.shape[-1] if aux is not None else 0), scale=scale, beta=beta)
+        ldaux = aux.shape[-1] if aux is not None else 0
+        if bias_grad is not None:
+            tiles = _lib.lib().eegf_gemm_colsum_tiles(_code(dy), _code(out), 1, M, K, N)
+            if tiles > 0 and (ldd or N) == N:
+                part = self.ws.get("acs", tiles * N, torch.float32)
+                call("eegf_gemm_acs", _code(dy), _code(out), 1, 0, epi, M, K, N, P(dy), N, P(w), K, P(out), ldo or K,
+                     None, P(aux), ldaux, 1.0, float(beta), float(scale), P(part), _stream())
+                ws = self.ws.get("colsum", 1 << 24, torch.float32)
+                call("eegf_colsum", F32, P(part), N, tiles, N, 1, P(ws), ws.numel(), P(bias_grad), 1.0, _stream())
+                return out
+            ws = self.ws.get("colsum", 1 << 24, torch.float32)
+            call("eegf_colsum", _code(dy), P(dy), ldd or N, M, N, 1, P(ws), ws.numel(), P(bias_grad), 1.0, _stream())
+        return self.gemm(dy, w, out, M, K, N, 1, 0, ldd or N, K, ldo or K, epi=epi, aux=aux, ldaux=ldaux,
+                         scale=scale, beta=beta)
+
+    def gbias(self, name):
+        """gradient view to accumulate a bias gradient into, or None when not needed"""
+        return self.G(name) if self.need(name) else None
 
     def wgrad(self, dy, x, name, M, ldd=None, ldx=None):
         if not self.need(name):
@@ -533,15 +553,15 @@ class FusionEngine:
             dhn = self.ws.get(f"b_dh{i % 2}", R * HID, self.dt).view(R, HID)
             self.ln_bwd(dh, *s["ln2"], pre + "output.LayerNorm", R, dfo, da, pdrop, 1, sv.rng + 11 + 3 * i)
             self.wgrad(dfo, s["ffact"], pre + "output.dense.weight", R)
-            self.bgrad(dfo, pre + "output.dense.bias", R)
-            self.dgrad(dfo, self.W(pre + "output.dense.weight"), dffp, R, epi=_lib.EPI_DGELU, aux=s["ffpre"])
+            self.dgrad(dfo, self.W(pre + "output.dense.weight"), dffp, R, epi=_lib.EPI_DGELU, aux=s["ffpre"],
+                       bias_grad=self.gbias(pre + "output.dense.bias"))
             self.wgrad(dffp, s["a1"], pre + "intermediate.dense.weight", R)
-            self.bgrad(dffp, pre + "intermediate.dense.bias", R)
-            self.dgrad(dffp, self.W(pre + "intermediate.dense.weight"), da, R, beta=1.0)
+            self.dgrad(dffp, self.W(pre + "intermediate.dense.weight"), da, R, beta=1.0,
+                       bias_grad=self.gbias(pre + "intermediate.dense.bias"))
             self.ln_bwd(da, *s["ln1"], pre + "attention.output.LayerNorm", R, dao, dhn, pdrop, 1, sv.rng + 10 + 3 * i)
             self.wgrad(dao, s["ctx"], pre + "attention.output.dense.weight", R)
-            self.bgrad(dao, pre + "attention.output.dense.bias", R)
-            self.dgrad(dao, self.W(pre + "attention.output.dense.weight"), dctx, R)
+            self.dgrad(dao, self.W(pre + "attention.output.dense.weight"), dctx, R,
+                       bias_grad=self.gbias(pre + "attention.output.dense.bias"))
             call("eegf_attn_bwd", self.code, B, NH, L, P(s["qkv"]), 3 * HID, P(t["kbias"]), scale, float(adrop),
                  self.cfg.seed, sv.rng + 12 + 3 * i, P(s["ctx"]), P(dctx), HID, P(s["lse"]), P(dqkv), P(dq_ws),
                  _stream())
@@ -550,10 +570,11 @@ class FusionEngine:
                 gq = self.a.span(qn, 3, self.a.grad).view(3 * HID, HID)
                 self.gemm(dqkv, s["h"], gq, 3 * HID, HID, R, 0, 0, 3 * HID, HID, HID, beta=1.0)
             bn = pre + "attention.self.query.bias"
-            if self.need(bn):
-                self.bgrad(dqkv, bn, R, width=3 * HID, out=self.a.span(bn, 3, self.a.grad))
+            gb = self.a.span(bn, 3, self.a.grad) if self.need(bn) else None
             if i > lowest or lowest == 0:
-                self.dgrad(dqkv, self.Wspan(qn, 3).view(3 * HID, HID), dhn, R, beta=1.0)
+                self.dgrad(dqkv, self.Wspan(qn, 3).view(3 * HID, HID), dhn, R, beta=1.0, bias_grad=gb)
+            elif gb is not None:
+                self.bgrad(dqkv, bn, R, width=3 * HID, out=gb)
             dh = dhn
         if lowest > 0:
             return

@@ -56,6 +56,20 @@ int eegf_gemm(int dtype, int out_dtype, int a_kcontig, int b_kcontig, int epi,
               const float* bias, long strideBias, void* aux, long ldaux, long strideAux,
               float alpha, float beta, float epi_scale, void* workspace, long ws_bytes,
               hipStream_t stream);
+/* Tuning / A-B hook (benchmarks): key 1 = schedule of the forward 256x256 GEMMs (0 = 2-stage, the
+ * default; 1..3 = experimental 8-phase variants).  Returns the previous value, or EEGF_ERR_ARG. */
+int eegf_tune(int key, int value);
+/* Rows of the a_colsum partial buffer eegf_gemm_acs writes for this shape (ceil(M/256)), or 0 when
+ * the fused column sums are unavailable (needs bf16 in/out, K-contiguous A, M >= 2048, N >= 256,
+ * K % 64 == 0, 8-aligned dims). */
+int eegf_gemm_colsum_tiles(int dtype, int out_dtype, int a_kcontig, int M, int N, int K);
+/* eegf_gemm (batch 1, no split-K) that also writes the column sums of A over each 256-row tile:
+ * a_colsum [ceil(M/256)][K] fp32.  For an input-gradient GEMM (A = dY) these are the partial bias
+ * gradients (nn.Linear bias.grad = dY.sum(0)), reduced with eegf_colsum over ceil(M/256) rows. */
+int eegf_gemm_acs(int dtype, int out_dtype, int a_kcontig, int b_kcontig, int epi, int M, int N, int K,
+                  const void* A, long lda, const void* B, long ldb, void* C, long ldc, const float* bias,
+                  void* aux, long ldaux, float alpha, float beta, float epi_scale, float* a_colsum,
+                  hipStream_t stream);
 
 /* fusion variants (eegf_fusion_fwd/bwd) */
 #define FUSE_CONCAT 0        /* model.py ConcatModel.feature: minmax(cat)            model.py:46-50      */

@@ -251,3 +251,32 @@ def test_gemm_big_dgrad_beta(M, N, K):
     k.linear_dgrad(dy, w, out=c, beta=1.0)
     torch.cuda.synchronize()
     _check(c, ref, torch.bfloat16)
+
+
+@pytest.mark.parametrize("epi", ["none", "dgelu"])
+@pytest.mark.parametrize("M,N,K,beta", [(4352, 808, 768, 0.0), (2056, 768, 3072, 1.0), (4096, 768, 2304, 1.0)])
+def test_gemm_acs_fused_bias_grad(epi, M, N, K, beta):
+    if epi == "dgelu":
+        beta = 0.0          # activation-derivative epilogues read aux in place of C (beta must be 0)
+    """eegf_gemm_acs: the input-gradient GEMM plus per-256-row-tile column sums of dY (the fused
+    bias gradient); ragged M (tiles past M excluded), beta accumulate, epilogue."""
+    from eegfusion import _lib
+    torch.manual_seed(13)
+    dy = torch.randn(M, K, device="cuda").to(torch.bfloat16)          # [M, N_out=K]
+    w = (torch.randn(K, N, device="cuda") * 0.1).to(torch.bfloat16)   # [N_out, N_in]
+    c = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+    aux = torch.randn(M, N, device="cuda").to(torch.bfloat16) if epi == "dgelu" else None
+    c0 = c.double().clone()
+    tiles = _lib.lib().eegf_gemm_colsum_tiles(1, 1, 1, M, N, K)
+    assert tiles == (M + 255) // 256
+    part = torch.full((tiles, K), float("nan"), device="cuda")
+    _lib.call("eegf_gemm_acs", 1, 1, 1, 0, _lib.EPI_DGELU if epi == "dgelu" else _lib.EPI_NONE, M, N, K,
+              dy.data_ptr(), K, w.data_ptr(), N, c.data_ptr(), N, None,
+              aux.data_ptr() if aux is not None else None, N if aux is not None else 0, 1.0, beta, 1.0,
+              part.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    ref, _ = _ref_epi(dy.double() @ w.double(), epi, None, aux, 1.0)
+    _check(c, ref + beta * c0, torch.bfloat16)
+    pref = torch.nn.functional.pad(dy.double(), (0, 0, 0, tiles * 256 - M)).view(tiles, 256, K).sum(1)
+    assert ((part.double() - pref).abs().max() / pref.abs().max()).item() < 1e-5
+    assert _lib.lib().eegf_gemm_colsum_tiles(0, 0, 1, M, N, K) == 0      # fp32: not fused

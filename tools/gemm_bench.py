@@ -57,25 +57,55 @@ def run(name, M, N, Kd, layout, epi, iters=20):
         C = torch.zeros(M, N, device=dev, dtype=torch.float32)
         f = lambda: K.gemm(A, B, C, M=M, N=N, K=Kd, a_kc=0, b_kc=0, lda=M, ldb=N, ldc=N, beta=1.0, workspace=ws)
         tf = lambda: A.t() @ B
+    from eegfusion import _lib
+    lib = _lib.lib()
+    lib.eegf_tune.argtypes = [_lib.i32, _lib.i32]
+
+    def timed(fn, n):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(n):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        return s.elapsed_time(e) / n
+
+    def tf_(ms):
+        return 2.0 * M * N * Kd / ms / 1e9
+
+    if AB:   # interleaved rounds of the two schedules in one process (key 1: 8-phase forward)
+        for fn in (f, tf):
+            fn()
+        torch.cuda.synchronize()
+        r = {0: [], 1: [], 2: [], 3: []}
+        for _ in range(5):
+            for v in (0, 1, 2, 3):
+                lib.eegf_tune(1, v)
+                f()
+                torch.cuda.synchronize()
+                r[v].append(timed(f, iters))
+        lib.eegf_tune(1, 1)
+        med = {v: sorted(x)[len(x) // 2] for v, x in r.items()}
+        tt = timed(tf, iters)
+        print(f"{name:16s} {M}x{N}x{Kd} " + " | ".join(f"v{v} {tf_(med[v]):6.1f}" for v in med)
+              + f" | torch {tf_(tt):6.1f} TF", flush=True)
+        return
     res = []
     for fn in (f, tf):
         for _ in range(3):
             fn()
         torch.cuda.synchronize()
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        for _ in range(iters):
-            fn()
-        e.record()
-        torch.cuda.synchronize()
-        ms = s.elapsed_time(e) / iters
-        res.append((ms, 2.0 * M * N * Kd / ms / 1e9))
+        ms = timed(fn, iters)
+        res.append((ms, tf_(ms)))
     print(f"{name:20s} M={M:6d} N={N:5d} K={Kd:6d}  eegf {res[0][0]*1e3:8.1f} us {res[0][1]:7.1f} TF | "
           f"torch {res[1][0]*1e3:8.1f} us {res[1][1]:7.1f} TF", flush=True)
 
 
+AB = "--ab" in sys.argv
+
+
 if __name__ == "__main__":
-    only = sys.argv[1:]
+    only = [a for a in sys.argv[1:] if not a.startswith("--")]
     for s in SHAPES:
         if not only or s[0] in only:
             run(*s)
