@@ -90,6 +90,22 @@ DEV bf16x8 rd_col(const bf16* t, int k0, int c0, int lane) {
   return r;
 }
 
+// rd_col on a row-major [256][64] tile: 8 rows r0..r0+7 (lane group) of column c0 + (lane&15)
+DEV bf16x8 rd_col_rm(const bf16* t, int r0, int c0, int lane) {
+  const int i = lane & 15, q = i >> 2, p = i & 3;
+  const int col = c0 + 4 * p;
+  const int ch = col >> 3, off = col & 7;
+  const int ra = r0 + q, rb = r0 + 4 + q;
+  const bf16* a0 = t + ra * BK + (((ch ^ swz_row(ra)) << 3) | off);
+  const bf16* a1 = t + rb * BK + (((ch ^ swz_row(rb)) << 3) | off);
+  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)a0);
+  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)a1);
+  bf16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
 DEV float erf_half(float x, float e) {
   const float z = fabsf(x) * 0.70710678118654752f;
   const float t = __frcp_rn(1.0f + 0.3275911f * z);
@@ -210,9 +226,12 @@ DEV void big_epilogue(const BigArgs& g, f32x4 (&acc)[8][4], bf16* lds, int m0, i
   }
 }
 
+constexpr int CS_KMAX = 3072;                 // fused column sums: K <= 3072 (sums parked in LDS)
+
 template <bool AKC, bool BKC, int EPI, typename TO, bool CS = false>
 __global__ void __launch_bounds__(NT, 1) gemm_big_kernel(BigArgs g) {
-  __shared__ __attribute__((aligned(16))) bf16 lds[LDS_ELEMS];
+  // CS: operand ring 128 KB | red[2][8][64] 4 KB | ks[K] fp32 12 KB  (the epilogue reuses the front)
+  __shared__ __attribute__((aligned(16))) bf16 lds[CS ? (4 * TILE + 1024 * 2 + CS_KMAX * 2) : LDS_ELEMS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
   const int tiles_n = (g.N + TN - 1) / TN, tiles_m = (g.M + TM - 1) / TM;
@@ -239,6 +258,8 @@ __global__ void __launch_bounds__(NT, 1) gemm_big_kernel(BigArgs g) {
   // fused A column sums (tile column 0 only): red[parity][wave][64] in the LDS tail
   const bool do_cs = CS && AKC && tn == 0;
   float* red = (float*)(lds + 4 * TILE);
+  float* ks = red + 2 * 8 * 64;
+  const int cs_rows = g.M - m0 - 32 * wave - 8 * (lane >> 4);   // rows of this lane's 8-row group below M
 
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = (kt & 1) * 2 * TILE, nxt = 2 * TILE - cur;
@@ -251,6 +272,25 @@ __global__ void __launch_bounds__(NT, 1) gemm_big_kernel(BigArgs g) {
     }
     const bf16* As = lds + cur;
     const bf16* Bs = lds + cur + TILE;
+    // fused column sums of this A tile on the MFMA: ones[16 x 256] . A[256 x 64] (rows past M masked in
+    // the ones operand); wave w contracts rows [32w, 32w+32), its 64 partial sums go through LDS
+    if (CS && do_cs) {
+      if (kt > 0 && tid < 64) {      // previous k-step's 8 wave partials (ordered by the barrier)
+        const float* rp = red + ((kt - 1) & 1) * 8 * 64;
+        float v = 0.f;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) v += rp[w * 64 + tid];
+        ks[(kt - 1) * BK + tid] = v;
+      }
+      bf16x8 ones;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ones[e] = (bf16)(e < cs_rows ? 1.0f : 0.0f);
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        const f32x4 c = mma16(ones, rd_col_rm(As, 32 * wave + 8 * (lane >> 4), 16 * f, lane), f32x4{0.f, 0.f, 0.f, 0.f});
+        if (lane < 16) red[(kt & 1) * 8 * 64 + wave * 64 + 16 * f + lane] = c[0];
+      }
+    }
 #pragma unroll
     for (int kc = 0; kc < 2; ++kc) {
       bf16x8 b[4];
@@ -268,38 +308,6 @@ __global__ void __launch_bounds__(NT, 1) gemm_big_kernel(BigArgs g) {
         for (int j = 0; j < 4; ++j) acc[i][j] = mma16(b[j], a, acc[i][j]);
       }
     }
-    if (CS) __builtin_amdgcn_sched_barrier(0);     // keep the sums out of the MFMA schedule
-    if (CS && do_cs) {
-      if (kt > 0 && tid < 64) {      // previous k-step's 8 wave partials (ordered by the barrier)
-        const float* rp = red + ((kt - 1) & 1) * 8 * 64;
-        float v = 0.f;
-#pragma unroll
-        for (int w = 0; w < 8; ++w) v += rp[w * 64 + tid];
-        g.colsum_part[(long)tm * g.K + kbeg + (kt - 1) * BK + tid] = v;
-      }
-      const int kc = lane & 7, rg = tid >> 3;          // 8-k chunk, 4-row group
-#pragma unroll 1
-      for (int hf = 0; hf < 2; ++hf) {                 // 4 k-values at a time (register budget)
-        float s[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int r = rg * 4 + q;
-          if (m0 + r < g.M) {
-            const bf16x8 v = rd_row(As, r, kc);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) s[e] += (float)v[4 * hf + e];
-          }
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          s[e] += __shfl_xor(s[e], 8, 64);
-          s[e] += __shfl_xor(s[e], 16, 64);
-          s[e] += __shfl_xor(s[e], 32, 64);
-        }
-        if (lane < 8) *(f32x4*)(red + (kt & 1) * 8 * 64 + wave * 64 + kc * 8 + 4 * hf) = f32x4{s[0], s[1], s[2], s[3]};
-      }
-    }
-    if (CS) __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
@@ -308,9 +316,14 @@ __global__ void __launch_bounds__(NT, 1) gemm_big_kernel(BigArgs g) {
     float v = 0.f;
 #pragma unroll
     for (int w = 0; w < 8; ++w) v += rp[w * 64 + tid];
-    g.colsum_part[(long)tm * g.K + kbeg + (nk - 1) * BK + tid] = v;
+    ks[(nk - 1) * BK + tid] = v;
   }
-  if (CS) __syncthreads();         // the epilogue reuses the LDS tail
+  if (CS) {
+    __syncthreads();
+    if (do_cs)
+      for (int k = tid; k < g.K; k += NT) g.colsum_part[(long)tm * g.K + k] = ks[k];
+    __syncthreads();               // the epilogue reuses the front of the LDS
+  }
 
   big_epilogue<EPI, TO>(g, acc, lds, m0, n0, tid, lane, wm, wn);
 }
@@ -536,6 +549,7 @@ int eegf_gemm_big(int a_kc, int b_kc, int epi, int out_f32, int M, int N, int K,
     return (int)hipGetLastError();
   }
   if (!a_kc || M < 2048 || N < 256) return 1;
+  if (a_colsum && K > CS_KMAX) return 1;
   if (b_kc) {
     switch (epi) {
       case EPI_NONE: return launch_big<true, true, EPI_NONE, bf16>(a, 1, stream);
@@ -558,7 +572,7 @@ int eegf_gemm_big(int a_kc, int b_kc, int epi, int out_f32, int M, int N, int K,
 // Row-tile count of the fused A column sums (rows of the a_colsum partial buffer) when eegf_gemm
 // would take the 256x256 path for this shape with a K-contiguous A and bf16 output, else 0.
 int eegf_gemm_big_colsum_tiles(int M, int N, int K) {
-  if (K % BK != 0 || M % 8 != 0 || N % 8 != 0 || M < 2048 || N < 256) return 0;
+  if (K % BK != 0 || M % 8 != 0 || N % 8 != 0 || M < 2048 || N < 256 || K > CS_KMAX) return 0;
   return (M + TM - 1) / TM;
 }
 
