@@ -145,6 +145,30 @@ DEV int xcd_remap(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
 }
 
+// erf(x/sqrt 2) by Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7), sharing exp(-x^2/2) with the
+// GELU derivative: one v_exp + one v_rcp instead of the library erff's branchy polynomial.
+DEV float erf_half(float x, float e) {            // e = exp(-x*x/2)
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __frcp_rn(1.0f + 0.3275911f * z);
+  const float poly = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
+  return copysignf(1.0f - poly * e, x);
+}
+DEV float gelu_f(float x) {
+  const float e = __expf(-0.5f * x * x);
+  return 0.5f * x * (1.0f + erf_half(x, e));
+}
+DEV float gelu_grad(float x) {
+  const float e = __expf(-0.5f * x * x);
+  return 0.5f * (1.0f + erf_half(x, e)) + x * 0.39894228040143268f * e;
+}
+// gelu(x) and gelu'(x) together (one exp, one erf): the forward stores gelu' for the backward
+DEV void gelu_fg(float x, float& gl, float& gd) {
+  const float e = __expf(-0.5f * x * x);
+  const float h = 0.5f * (1.0f + erf_half(x, e));
+  gl = x * h;
+  gd = h + x * 0.39894228040143268f * e;
+}
+
 // ---------------------------------------------------------------------------------------
 // Counter-based RNG: Philox4x32-10 (Salmon et al., SC'11).  Every random draw in the path
 // (dropout masks, Laplace noise, Gumbel noise) is a pure function of (seed, stream, counter),

@@ -29,23 +29,6 @@ struct GemmArgs {
   int lds_epi;         // LDS-staged coalesced epilogue (bf16 out, beta == 0)
 };
 
-// erf(x/sqrt 2) by Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7), sharing exp(-x^2/2) with the
-// GELU derivative: one v_exp + one v_rcp instead of the library erff's branchy polynomial.
-DEV float erf_half(float x, float e) {            // e = exp(-x*x/2)
-  const float z = fabsf(x) * 0.70710678118654752f;
-  const float t = __frcp_rn(1.0f + 0.3275911f * z);
-  const float poly = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
-  return copysignf(1.0f - poly * e, x);
-}
-DEV float gelu_f(float x) {
-  const float e = __expf(-0.5f * x * x);
-  return 0.5f * x * (1.0f + erf_half(x, e));
-}
-DEV float gelu_grad(float x) {
-  const float e = __expf(-0.5f * x * x);
-  return 0.5f * (1.0f + erf_half(x, e)) + x * 0.39894228040143268f * e;
-}
-
 DEV void load4(const float* p, float (&v)[4]) { const f32x4 x = *(const f32x4*)p; v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3]; }
 DEV void load4(const bf16* p, float (&v)[4]) { const bf16x4 x = *(const bf16x4*)p; v[0] = (float)x[0]; v[1] = (float)x[1]; v[2] = (float)x[2]; v[3] = (float)x[3]; }
 DEV void store4(float* p, const float (&v)[4]) { *(f32x4*)p = f32x4{v[0], v[1], v[2], v[3]}; }
@@ -221,9 +204,12 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmArgs g) {
   TO* Cp = (TO*)g.C + (long)z * g.sC;
   TO* aux = (TO*)g.aux + (long)z * g.sAux;
   const float* biasp = g.bias ? g.bias + (long)z * g.sBias : nullptr;
-  constexpr bool HAS_BIAS = EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_TANH;
-  constexpr bool HAS_AUX = EPI == EPI_BIAS_GELU || EPI == EPI_DGELU || EPI == EPI_DRELU || EPI == EPI_DTANH;
-  constexpr bool AUX_IN = EPI == EPI_DGELU || EPI == EPI_DRELU || EPI == EPI_DTANH;
+  constexpr bool HAS_BIAS = EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_TANH ||
+                            EPI == EPI_BIAS_GELU_D;
+  constexpr bool HAS_AUX = EPI == EPI_BIAS_GELU || EPI == EPI_DGELU || EPI == EPI_DRELU || EPI == EPI_DTANH ||
+                           EPI == EPI_BIAS_GELU_D || EPI == EPI_MUL_AUX;
+  constexpr bool AUX_IN = EPI == EPI_DGELU || EPI == EPI_DRELU || EPI == EPI_DTANH || EPI == EPI_MUL_AUX;
+  constexpr bool TWO_OUT = EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_D;   // C and aux both written
   if constexpr (sizeof(TO) == 2 && sizeof(T) == 2) {
     if (g.beta == 0.f && g.lds_epi) {
       // LDS-staged epilogue: the 128x128 bf16 tile goes through LDS so every global access is a
@@ -252,20 +238,29 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmArgs g) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             float v = g.alpha * acc[i][j][r];
-            if (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) v += bias[r];
+            if (EPI == EPI_BIAS) v += bias[r];
+            else if (EPI == EPI_BIAS_GELU) v = g.aux ? v + bias[r] : gelu_f(v + bias[r]);
             else if (EPI == EPI_BIAS_RELU) v = fmaxf(v + bias[r], 0.f);
             else if (EPI == EPI_BIAS_TANH) v = tanhf(v + bias[r]);
             else if (EPI == EPI_DGELU) v *= gelu_grad(av[r]);
             else if (EPI == EPI_DRELU) v = av[r] > 0.f ? v * g.epi_scale : 0.f;
             else if (EPI == EPI_DTANH) v *= (1.f - av[r] * av[r]);
-            acc[i][j][r] = v;                 // BIAS_GELU keeps the pre-activation
-            o[r] = v;
+            else if (EPI == EPI_MUL_AUX) v *= av[r];
+            if (EPI == EPI_BIAS_GELU_D) {     // aux round first: gelu'; acc keeps gelu for the C round
+              float gl, gd;
+              gelu_fg(v + bias[r], gl, gd);
+              acc[i][j][r] = gl;
+              o[r] = gd;
+            } else {
+              acc[i][j][r] = v;               // BIAS_GELU keeps the pre-activation
+              o[r] = v;
+            }
           }
           store4(lp, o);
         }
       }
       __syncthreads();
-      if (EPI == EPI_BIAS_GELU) {
+      if ((EPI == EPI_BIAS_GELU && g.aux) || EPI == EPI_BIAS_GELU_D) {
         tile_io<false>(ct, LDC, (bf16*)aux, g.ldaux, m0, n0, g.M, g.N, tid);
         __syncthreads();
 #pragma unroll
@@ -274,7 +269,7 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmArgs g) {
           for (int i = 0; i < 4; ++i) {
             float o[4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = gelu_f(acc[i][j][r]);
+            for (int r = 0; r < 4; ++r) o[r] = EPI == EPI_BIAS_GELU_D ? acc[i][j][r] : gelu_f(acc[i][j][r]);
             store4(ct + (wm * 64 + i * 16 + (lane & 15)) * LDC + wn * 64 + j * 16 + 4 * (lane >> 4), o);
           }
         __syncthreads();
@@ -302,17 +297,17 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmArgs g) {
       const int m = m0 + wm * 64 + i * 16 + (lane & 15);
       if (m >= g.M) continue;
       TO* cp = Cp + (long)m * g.ldc + n;
-      TO* ap = HAS_AUX ? aux + (long)m * g.ldaux + n : nullptr;
+      TO* ap = HAS_AUX && g.aux ? aux + (long)m * g.ldaux + n : nullptr;
       const bool vec = nfull && ((uintptr_t)cp & (4 * sizeof(TO) - 1)) == 0 &&
-                       (!HAS_AUX || ((uintptr_t)ap & (4 * sizeof(TO) - 1)) == 0);
+                       (!ap || ((uintptr_t)ap & (4 * sizeof(TO) - 1)) == 0);
       float av[4] = {0.f, 0.f, 0.f, 0.f}, cv[4] = {0.f, 0.f, 0.f, 0.f};
       if (vec) {
-        if (EPI == EPI_DGELU || EPI == EPI_DRELU || EPI == EPI_DTANH) load4(ap, av);
+        if (AUX_IN) load4(ap, av);
         if (g.beta != 0.f) load4(cp, cv);
       } else {
         for (int r = 0; r < 4; ++r)
           if (n + r < g.N) {
-            if (EPI == EPI_DGELU || EPI == EPI_DRELU || EPI == EPI_DTANH) av[r] = to_f32(ap[r]);
+            if (AUX_IN) av[r] = to_f32(ap[r]);
             if (g.beta != 0.f) cv[r] = to_f32(cp[r]);
           }
       }
@@ -322,6 +317,8 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmArgs g) {
         float v = g.alpha * acc[i][j][r];
         if (EPI == EPI_BIAS) v += bias[r];
         else if (EPI == EPI_BIAS_GELU) { v += bias[r]; pre[r] = v; v = gelu_f(v); }
+        else if (EPI == EPI_BIAS_GELU_D) { float gl; gelu_fg(v + bias[r], gl, pre[r]); v = gl; }
+        else if (EPI == EPI_MUL_AUX) v *= av[r];
         else if (EPI == EPI_BIAS_RELU) v = fmaxf(v + bias[r], 0.f);
         else if (EPI == EPI_BIAS_TANH) v = tanhf(v + bias[r]);
         else if (EPI == EPI_DGELU) v *= gelu_grad(av[r]);
@@ -332,12 +329,12 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmArgs g) {
       }
       if (vec) {
         store4(cp, o);
-        if (EPI == EPI_BIAS_GELU) store4(ap, pre);
+        if (TWO_OUT && ap) store4(ap, pre);
       } else {
         for (int r = 0; r < 4; ++r)
           if (n + r < g.N) {
             cp[r] = from_f32<TO>(o[r]);
-            if (EPI == EPI_BIAS_GELU) ap[r] = from_f32<TO>(pre[r]);
+            if (TWO_OUT && ap) ap[r] = from_f32<TO>(pre[r]);
           }
       }
     }
@@ -357,8 +354,12 @@ __global__ void __launch_bounds__(256) gemm_splitk_reduce(const float* __restric
   for (int s = 0; s < splits; ++s) v += slabs[(long)s * total + e];
   const long m = e / N, n = e % N;
   TO* c = C + m * ldc + n;
-  if (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_TANH) v += bias[n];
-  if (EPI == EPI_BIAS_GELU) { aux[m * ldaux + n] = from_f32<TO>(v); v = gelu_f(v); }
+  if (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_TANH ||
+      EPI == EPI_BIAS_GELU_D)
+    v += bias[n];
+  if (EPI == EPI_BIAS_GELU) { if (aux) aux[m * ldaux + n] = from_f32<TO>(v); v = gelu_f(v); }
+  else if (EPI == EPI_BIAS_GELU_D) { float gl, gd; gelu_fg(v, gl, gd); aux[m * ldaux + n] = from_f32<TO>(gd); v = gl; }
+  else if (EPI == EPI_MUL_AUX) v *= to_f32(aux[m * ldaux + n]);
   else if (EPI == EPI_BIAS_RELU) v = fmaxf(v, 0.f);
   else if (EPI == EPI_BIAS_TANH) v = tanhf(v);
   else if (EPI == EPI_DGELU) v *= gelu_grad(to_f32(aux[m * ldaux + n]));
@@ -383,6 +384,8 @@ int splitk_reduce_t(int epi, const float* ws, int splits, int M, int N, void* C,
     case EPI_DGELU: RED(EPI_DGELU); break;
     case EPI_DRELU: RED(EPI_DRELU); break;
     case EPI_DTANH: RED(EPI_DTANH); break;
+    case EPI_BIAS_GELU_D: RED(EPI_BIAS_GELU_D); break;
+    case EPI_MUL_AUX: RED(EPI_MUL_AUX); break;
     default: return EEGF_ERR_ARG;
   }
 #undef RED
@@ -431,6 +434,8 @@ int dispatch_epi(int epi, int akc, int bkc, const GemmArgs& a, int batch, hipStr
     case EPI_DGELU: return launch<T, true, false, TO, EPI_DGELU>(a, batch, s);
     case EPI_DRELU: return launch<T, true, false, TO, EPI_DRELU>(a, batch, s);
     case EPI_DTANH: return launch<T, true, false, TO, EPI_DTANH>(a, batch, s);
+    case EPI_BIAS_GELU_D: return launch<T, true, true, TO, EPI_BIAS_GELU_D>(a, batch, s);
+    case EPI_MUL_AUX: return launch<T, true, false, TO, EPI_MUL_AUX>(a, batch, s);
   }
   return EEGF_ERR_ARG;
 }
@@ -459,12 +464,15 @@ static int gemm_impl(int dtype, int out_dtype, int a_kcontig, int b_kcontig, int
                      hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0 || batch <= 0 || !A || !B || !C) return EEGF_ERR_ARG;
   if (batch > 65535) return EEGF_ERR_ARG;
-  const bool has_bias = epi == EPI_BIAS || epi == EPI_BIAS_GELU || epi == EPI_BIAS_RELU || epi == EPI_BIAS_TANH;
+  if (epi < EPI_NONE || epi > EPI_MUL_AUX) return EEGF_ERR_ARG;
+  const bool has_bias = epi == EPI_BIAS || epi == EPI_BIAS_GELU || epi == EPI_BIAS_RELU || epi == EPI_BIAS_TANH ||
+                        epi == EPI_BIAS_GELU_D;
+  const bool aux_in = epi == EPI_DGELU || epi == EPI_DRELU || epi == EPI_DTANH || epi == EPI_MUL_AUX;
   if (has_bias && !bias) return EEGF_ERR_ARG;
-  if ((epi == EPI_BIAS_GELU || epi == EPI_DGELU || epi == EPI_DRELU || epi == EPI_DTANH) && !aux) return EEGF_ERR_ARG;
-  if ((epi == EPI_DGELU || epi == EPI_DRELU || epi == EPI_DTANH) && beta != 0.f) return EEGF_ERR_ARG;  // aux replaces C
+  if ((aux_in || epi == EPI_BIAS_GELU_D) && !aux) return EEGF_ERR_ARG;    // BIAS_GELU: aux optional
+  if (aux_in && beta != 0.f) return EEGF_ERR_ARG;                           // aux replaces C
   if (epi != EPI_NONE) {
-    const bool fwd = epi <= EPI_BIAS_TANH;
+    const bool fwd = epi <= EPI_BIAS_TANH || epi == EPI_BIAS_GELU_D;
     if (fwd && !(a_kcontig && b_kcontig)) return EEGF_ERR_ARG;
     if (!fwd && !(a_kcontig && !b_kcontig)) return EEGF_ERR_ARG;
   }

@@ -106,18 +106,6 @@ DEV bf16x8 rd_col_rm(const bf16* t, int r0, int c0, int lane) {
   return r;
 }
 
-DEV float erf_half(float x, float e) {
-  const float z = fabsf(x) * 0.70710678118654752f;
-  const float t = __frcp_rn(1.0f + 0.3275911f * z);
-  const float poly = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
-  return copysignf(1.0f - poly * e, x);
-}
-DEV float gelu_f(float x) { const float e = __expf(-0.5f * x * x); return 0.5f * x * (1.0f + erf_half(x, e)); }
-DEV float gelu_grad(float x) {
-  const float e = __expf(-0.5f * x * x);
-  return 0.5f * (1.0f + erf_half(x, e)) + x * 0.39894228040143268f * e;
-}
-
 template <bool LOAD>
 DEV void tile_io(bf16* lds, bf16* gp, long ld, int m0, int n0, int M, int N, int tid) {
 #pragma unroll 4
@@ -144,8 +132,9 @@ DEV void st4(bf16* p, const float (&v)[4]) { bf16x4 x; x[0] = (bf16)v[0]; x[1] =
 template <int EPI, typename TO>
 DEV void big_epilogue(const BigArgs& g, f32x4 (&acc)[8][4], bf16* lds, int m0, int n0, int tid, int lane, int wm,
                       int wn) {
-  constexpr bool HAS_BIAS = EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_TANH;
-  constexpr bool AUX_IN = EPI == EPI_DGELU || EPI == EPI_DRELU || EPI == EPI_DTANH;
+  constexpr bool HAS_BIAS = EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_TANH ||
+                            EPI == EPI_BIAS_GELU_D;
+  constexpr bool AUX_IN = EPI == EPI_DGELU || EPI == EPI_DRELU || EPI == EPI_DTANH || EPI == EPI_MUL_AUX;
   if constexpr (sizeof(TO) == 4) {
     // fp32 output (weight gradients): direct 16-B stores of 4 consecutive columns; split-K slabs
     float* Cf = (float*)g.C + (g.ksplit > 0 ? (long)blockIdx.y * g.M * g.N : 0);
@@ -194,33 +183,49 @@ DEV void big_epilogue(const BigArgs& g, f32x4 (&acc)[8][4], bf16* lds, int m0, i
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float v = g.alpha * acc[i][j][r];
-        if (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) v += bias[r];
+        if (EPI == EPI_BIAS) v += bias[r];
+        else if (EPI == EPI_BIAS_GELU) v = g.aux ? v + bias[r] : gelu_f(v + bias[r]);  // no aux: act only
         else if (EPI == EPI_BIAS_RELU) v = fmaxf(v + bias[r], 0.f);
         else if (EPI == EPI_BIAS_TANH) v = tanhf(v + bias[r]);
         else if (EPI == EPI_DGELU) v *= gelu_grad(av[r]);
         else if (EPI == EPI_DRELU) v = av[r] > 0.f ? v * g.epi_scale : 0.f;
         else if (EPI == EPI_DTANH) v *= (1.f - av[r] * av[r]);
+        else if (EPI == EPI_MUL_AUX) v *= av[r];
         else if (g.beta != 0.f) v += g.beta * av[r];         // EPI_NONE accumulate (beta * C)
-        acc[i][j][r] = v;
-        o[r] = v;
+        if (EPI == EPI_BIAS_GELU_D) {                        // aux round first: gelu'; acc keeps gelu
+          float gl, gd;
+          gelu_fg(v + bias[r], gl, gd);
+          acc[i][j][r] = gl;
+          o[r] = gd;
+        } else {
+          acc[i][j][r] = v;
+          o[r] = v;
+        }
       }
       st4(lp, o);
     }
   }
   __syncthreads();
-  if (EPI == EPI_BIAS_GELU) {
+  if ((EPI == EPI_BIAS_GELU && g.aux) || EPI == EPI_BIAS_GELU_D) {
+    // store the pre-activation tile, then compute GELU while those stores drain (raw barriers: a
+    // __syncthreads() here would wait for the stores); LDS reads of the tile are complete per
+    // thread once its stores have issued
     tile_io<false>(ct, g.aux, g.ldaux, m0, n0, g.M, g.N, tid);
-    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = EPI == EPI_BIAS_GELU_D ? acc[i][j][r] : gelu_f(acc[i][j][r]);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        float o[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = gelu_f(acc[i][j][r]);
+        float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
         st4(ct + (wm * 128 + i * 16 + (lane & 15)) * LDC + wn * 64 + j * 16 + 4 * (lane >> 4), o);
       }
-    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
   tile_io<false>(ct, Cb, g.ldc, m0, n0, g.M, g.N, tid);
   }
@@ -557,6 +562,7 @@ int eegf_gemm_big(int a_kc, int b_kc, int epi, int out_f32, int M, int N, int K,
       case EPI_BIAS_GELU: return launch_big<true, true, EPI_BIAS_GELU, bf16>(a, 1, stream);
       case EPI_BIAS_RELU: return launch_big<true, true, EPI_BIAS_RELU, bf16>(a, 1, stream);
       case EPI_BIAS_TANH: return launch_big<true, true, EPI_BIAS_TANH, bf16>(a, 1, stream);
+      case EPI_BIAS_GELU_D: return launch_big<true, true, EPI_BIAS_GELU_D, bf16>(a, 1, stream);
     }
   } else {
     switch (epi) {
@@ -564,6 +570,7 @@ int eegf_gemm_big(int a_kc, int b_kc, int epi, int out_f32, int M, int N, int K,
       case EPI_DGELU: return launch_big<true, false, EPI_DGELU, bf16>(a, 1, stream);
       case EPI_DRELU: return launch_big<true, false, EPI_DRELU, bf16>(a, 1, stream);
       case EPI_DTANH: return launch_big<true, false, EPI_DTANH, bf16>(a, 1, stream);
+      case EPI_MUL_AUX: return launch_big<true, false, EPI_MUL_AUX, bf16>(a, 1, stream);
     }
   }
   return 1;

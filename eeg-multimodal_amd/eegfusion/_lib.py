@@ -16,6 +16,7 @@ F32, BF16 = 0, 1
 ERR_ARG = -1
 
 EPI_NONE, EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_RELU, EPI_BIAS_TANH, EPI_DGELU, EPI_DRELU, EPI_DTANH = range(8)
+EPI_BIAS_GELU_D, EPI_MUL_AUX = 8, 9
 FUSE_CONCAT, FUSE_PRICONCAT, FUSE_PRICONCAT_LAP, FUSE_PRIGUMBEL = range(4)
 
 i32, i64, f32, u64, vp = C.c_int, C.c_long, C.c_float, C.c_uint64, C.c_void_p

@@ -262,7 +262,9 @@ class FusionEngine:
         t["kbias"] = kbias
         e = "bert.embeddings."
         h = self.empty(R, HID)
-        s0, m0, r0 = self.empty(R, HID), self._f32(R), self._f32(R)
+        # without save (the PriGumbel DP pass: no full backward) the LN residual sums / statistics and
+        # the FFN pre-activations are not stored
+        s0, m0, r0 = (self.empty(R, HID), self._f32(R), self._f32(R)) if save else (None, None, None)
         self.ln_fwd(x, None, e + "LayerNorm", R, h, s0, m0, r0, 1e-12, pdrop, 2, sv.rng + 1,
                     table=self.F(e + "position_embeddings.weight"), period=L,
                     table2=self.F(e + "token_type_embeddings.weight"))
@@ -286,20 +288,22 @@ class FusionEngine:
             self.linear(ctx, self.W(pre + "attention.output.dense.weight"), self.F(pre + "attention.output.dense.bias"),
                         ao, R)
             a1 = self.empty(R, HID)
-            s1, m1, r1 = self.empty(R, HID), self._f32(R), self._f32(R)
+            s1, m1, r1 = (self.empty(R, HID), self._f32(R), self._f32(R)) if save else (None, None, None)
             self.ln_fwd(ao, h, pre + "attention.output.LayerNorm", R, a1, s1, m1, r1, 1e-12, pdrop, 1,
                         sv.rng + 10 + 3 * i)
-            ffpre, ffact = self.empty(R, FFN), self.empty(R, FFN)
+            # saved for the backward: gelu'(pre) (the DGELU epilogue becomes a multiply)
+            ffgd = self.empty(R, FFN) if save else None
+            ffact = self.empty(R, FFN) if save else self.ws.get("ffact", R * FFN, self.dt).view(R, FFN)
             self.linear(a1, self.W(pre + "intermediate.dense.weight"), self.F(pre + "intermediate.dense.bias"), ffact,
-                        R, epi=_lib.EPI_BIAS_GELU, aux=ffpre, tag="ffn1_fwd")
+                        R, epi=_lib.EPI_BIAS_GELU_D if save else _lib.EPI_BIAS_GELU, aux=ffgd, tag="ffn1_fwd")
             fo = self.ws.get("fo", R * HID, self.dt).view(R, HID)
             self.linear(ffact, self.W(pre + "output.dense.weight"), self.F(pre + "output.dense.bias"), fo, R,
                         tag="ffn2_fwd")
             h2 = self.empty(R, HID)
-            s2, m2, r2 = self.empty(R, HID), self._f32(R), self._f32(R)
+            s2, m2, r2 = (self.empty(R, HID), self._f32(R), self._f32(R)) if save else (None, None, None)
             self.ln_fwd(fo, a1, pre + "output.LayerNorm", R, h2, s2, m2, r2, 1e-12, pdrop, 1, sv.rng + 11 + 3 * i)
             if save:
-                layers.append(dict(h=h, qkv=qkv, ctx=ctx, lse=lse, a1=a1, ln1=(s1, m1, r1), ffpre=ffpre, ffact=ffact,
+                layers.append(dict(h=h, qkv=qkv, ctx=ctx, lse=lse, a1=a1, ln1=(s1, m1, r1), ffgd=ffgd, ffact=ffact,
                                    ln2=(s2, m2, r2)))
             h = h2
         t["layers"] = layers
@@ -553,7 +557,7 @@ class FusionEngine:
             dhn = self.ws.get(f"b_dh{i % 2}", R * HID, self.dt).view(R, HID)
             self.ln_bwd(dh, *s["ln2"], pre + "output.LayerNorm", R, dfo, da, pdrop, 1, sv.rng + 11 + 3 * i)
             self.wgrad(dfo, s["ffact"], pre + "output.dense.weight", R)
-            self.dgrad(dfo, self.W(pre + "output.dense.weight"), dffp, R, epi=_lib.EPI_DGELU, aux=s["ffpre"],
+            self.dgrad(dfo, self.W(pre + "output.dense.weight"), dffp, R, epi=_lib.EPI_MUL_AUX, aux=s["ffgd"],
                        bias_grad=self.gbias(pre + "output.dense.bias"))
             self.wgrad(dffp, s["a1"], pre + "intermediate.dense.weight", R)
             self.dgrad(dffp, self.W(pre + "intermediate.dense.weight"), da, R, beta=1.0,

@@ -13,7 +13,8 @@ from ._lib import BF16, F32, call
 
 EPI = dict(none=_lib.EPI_NONE, bias=_lib.EPI_BIAS, bias_gelu=_lib.EPI_BIAS_GELU,
            bias_relu=_lib.EPI_BIAS_RELU, bias_tanh=_lib.EPI_BIAS_TANH, dgelu=_lib.EPI_DGELU,
-           drelu=_lib.EPI_DRELU, dtanh=_lib.EPI_DTANH)
+           drelu=_lib.EPI_DRELU, dtanh=_lib.EPI_DTANH, bias_gelu_d=_lib.EPI_BIAS_GELU_D,
+           mul_aux=_lib.EPI_MUL_AUX)
 
 
 def code(t: torch.Tensor) -> int:

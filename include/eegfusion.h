@@ -32,12 +32,14 @@ extern "C" {
 /* GEMM epilogues */
 #define EPI_NONE 0       /* C = alpha*AB (+ beta*C)                                   */
 #define EPI_BIAS 1       /* + bias[n]                           nn.Linear forward        */
-#define EPI_BIAS_GELU 2  /* aux = AB+bias; C = gelu_erf(aux)    BertIntermediate         */
+#define EPI_BIAS_GELU 2  /* aux = AB+bias (NULL: not stored); C = gelu_erf(AB+bias)  BertIntermediate */
 #define EPI_BIAS_RELU 3  /* C = relu(AB+bias)                   fc_layers[0..1]          */
 #define EPI_BIAS_TANH 4  /* C = tanh(AB+bias)                   fc_layers[2..3], pooler  */
 #define EPI_DGELU 5      /* C = AB * gelu'(aux)                 backward of EPI_BIAS_GELU */
 #define EPI_DRELU 6      /* C = AB * (aux>0) * epi_scale        backward of relu(+dropout) */
 #define EPI_DTANH 7      /* C = AB * (1-aux^2)                  backward of tanh         */
+#define EPI_BIAS_GELU_D 8 /* C = gelu_erf(AB+bias); aux = gelu_erf'(AB+bias)  (saves the derivative) */
+#define EPI_MUL_AUX 9    /* C = AB * aux                        backward of EPI_BIAS_GELU_D */
 
 /* Every dense projection of the path: BERT Q/K/V/out/FFN (transformers modeling_bert.py:139-351),
  * pooler (modeling_bert.py:451-462), visual_encoder (model.py:18,36), decoder in_proj/out_proj/

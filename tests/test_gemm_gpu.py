@@ -14,11 +14,19 @@ def _k():
     return kernels
 
 
+def _gelu_grad(x):
+    return 0.5 * (1 + torch.erf(x / 2 ** 0.5)) + x * torch.exp(-0.5 * x * x) / (2 * torch.pi) ** 0.5
+
+
 def _ref_epi(v, epi, bias, aux, scale):
-    if epi in ("bias", "bias_gelu", "bias_relu", "bias_tanh"):
+    if epi in ("bias", "bias_gelu", "bias_relu", "bias_tanh", "bias_gelu_d"):
         v = v + bias.double()
     if epi == "bias_gelu":
         return torch.nn.functional.gelu(v), v
+    if epi == "bias_gelu_d":
+        return torch.nn.functional.gelu(v), _gelu_grad(v)
+    if epi == "mul_aux":
+        return v * aux.double(), None
     if epi == "bias_relu":
         return torch.relu(v), None
     if epi == "bias_tanh":
@@ -74,7 +82,7 @@ def test_gemm_layouts(dt, M, N, K, layout):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("epi", ["bias", "bias_gelu", "bias_relu", "bias_tanh"])
+@pytest.mark.parametrize("epi", ["bias", "bias_gelu", "bias_relu", "bias_tanh", "bias_gelu_d"])
 def test_gemm_fwd_epilogues(dt, epi):
     k = _k()
     torch.manual_seed(1)
@@ -82,7 +90,7 @@ def test_gemm_fwd_epilogues(dt, epi):
     x = (torch.randn(M, K, device="cuda") * 0.3).to(dt)
     w = (torch.randn(N, K, device="cuda") * 0.3).to(dt)
     b = torch.randn(N, device="cuda")
-    aux = torch.empty(M, N, device="cuda", dtype=dt) if epi == "bias_gelu" else None
+    aux = torch.empty(M, N, device="cuda", dtype=dt) if epi in ("bias_gelu", "bias_gelu_d") else None
     out = k.linear(x, w, b, epi=epi, aux=aux)
     torch.cuda.synchronize()
     ref, pre = _ref_epi(x.double() @ w.double().t(), epi, b, None, 1.0)
@@ -92,7 +100,7 @@ def test_gemm_fwd_epilogues(dt, epi):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("epi", ["dgelu", "drelu", "dtanh"])
+@pytest.mark.parametrize("epi", ["dgelu", "drelu", "dtanh", "mul_aux"])
 def test_gemm_dgrad_epilogues(dt, epi):
     k = _k()
     torch.manual_seed(2)
@@ -155,7 +163,7 @@ def test_gemm_wgrad_splitk(dt, M, N, K):
     assert torch.equal(dw2, dw3)          # deterministic
 
 
-@pytest.mark.parametrize("epi", ["none", "bias", "bias_gelu", "bias_relu", "bias_tanh"])
+@pytest.mark.parametrize("epi", ["none", "bias", "bias_gelu", "bias_relu", "bias_tanh", "bias_gelu_d", "gelu_noaux"])
 @pytest.mark.parametrize("M,N,K", [(4352, 808, 768), (2048, 2304, 256)])
 def test_gemm_big_fwd(epi, M, N, K):
     """256x256 glds-pipelined bf16 kernel (M >= 2048), including M/N edge tiles."""
@@ -164,7 +172,13 @@ def test_gemm_big_fwd(epi, M, N, K):
     x = (torch.randn(M, K, device="cuda") * 0.3).to(torch.bfloat16)
     w = (torch.randn(N, K, device="cuda") * 0.3).to(torch.bfloat16)
     b = torch.randn(N, device="cuda") if epi != "none" else None
-    aux = torch.empty(M, N, device="cuda", dtype=torch.bfloat16) if epi == "bias_gelu" else None
+    aux = torch.empty(M, N, device="cuda", dtype=torch.bfloat16) if epi in ("bias_gelu", "bias_gelu_d") else None
+    if epi == "gelu_noaux":      # BIAS_GELU without the pre-activation output (forward-only passes)
+        epi = "bias_gelu"
+        out = k.linear(x, w, b, epi=epi, aux=None)
+        torch.cuda.synchronize()
+        _check(out, _ref_epi(x.double() @ w.double().t(), epi, b, None, 1.0)[0], torch.bfloat16)
+        return
     out = k.linear(x, w, b, epi=epi, aux=aux)
     torch.cuda.synchronize()
     ref, pre = _ref_epi(x.double() @ w.double().t(), epi, b, None, 1.0)
@@ -173,7 +187,7 @@ def test_gemm_big_fwd(epi, M, N, K):
         _check(aux, pre, torch.bfloat16)
 
 
-@pytest.mark.parametrize("epi", ["none", "dgelu", "drelu", "dtanh"])
+@pytest.mark.parametrize("epi", ["none", "dgelu", "drelu", "dtanh", "mul_aux"])
 @pytest.mark.parametrize("M,N,K", [(4352, 808, 768), (2048, 3072, 320)])
 def test_gemm_big_dgrad(epi, M, N, K):
     k = _k()
@@ -189,7 +203,8 @@ def test_gemm_big_dgrad(epi, M, N, K):
     _check(out, ref, torch.bfloat16)
 
 
-@pytest.mark.parametrize("epi", ["bias", "bias_gelu", "bias_relu", "bias_tanh", "dgelu", "drelu", "dtanh", "none"])
+@pytest.mark.parametrize("epi", ["bias", "bias_gelu", "bias_relu", "bias_tanh", "dgelu", "drelu", "dtanh", "none",
+                                 "bias_gelu_d", "mul_aux"])
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_gemm_small_m_splitk_epilogues(dt, epi):
     """Batch-row GEMMs (M = B) take split-K with the epilogue applied in the slab reduction."""
@@ -201,7 +216,7 @@ def test_gemm_small_m_splitk_epilogues(dt, epi):
     if epi.startswith("bias") or epi == "none":
         w = (torch.randn(N, K, device="cuda") * 0.2).to(dt)
         b = torch.randn(N, device="cuda")
-        aux = torch.empty(M, N, device="cuda", dtype=dt) if epi == "bias_gelu" else None
+        aux = torch.empty(M, N, device="cuda", dtype=dt) if epi in ("bias_gelu", "bias_gelu_d") else None
         out = torch.empty(M, N, device="cuda", dtype=dt)
         k.gemm(x, w, out, M=M, N=N, K=K, a_kc=1, b_kc=1, lda=K, ldb=K, ldc=N, epi=epi, bias=b if epi != "none" else None,
                aux=aux, ldaux=N, workspace=ws)
