@@ -184,7 +184,7 @@ DEV void big_epilogue(const BigArgs& g, f32x4 (&acc)[8][4], bf16* lds, int m0, i
       for (int r = 0; r < 4; ++r) {
         float v = g.alpha * acc[i][j][r];
         if (EPI == EPI_BIAS) v += bias[r];
-        else if (EPI == EPI_BIAS_GELU) v = g.aux ? v + bias[r] : gelu_f(v + bias[r]);  // no aux: act only
+        else if (EPI == EPI_BIAS_GELU) v = g.aux ? v + bias[r] : v;      // no aux: GELU below (packed)
         else if (EPI == EPI_BIAS_RELU) v = fmaxf(v + bias[r], 0.f);
         else if (EPI == EPI_BIAS_TANH) v = tanhf(v + bias[r]);
         else if (EPI == EPI_DGELU) v *= gelu_grad(av[r]);
@@ -192,14 +192,20 @@ DEV void big_epilogue(const BigArgs& g, f32x4 (&acc)[8][4], bf16* lds, int m0, i
         else if (EPI == EPI_DTANH) v *= (1.f - av[r] * av[r]);
         else if (EPI == EPI_MUL_AUX) v *= av[r];
         else if (g.beta != 0.f) v += g.beta * av[r];         // EPI_NONE accumulate (beta * C)
-        if (EPI == EPI_BIAS_GELU_D) {                        // aux round first: gelu'; acc keeps gelu
-          float gl, gd;
-          gelu_fg(v + bias[r], gl, gd);
-          acc[i][j][r] = gl;
-          o[r] = gd;
-        } else {
-          acc[i][j][r] = v;
-          o[r] = v;
+        acc[i][j][r] = v;
+        o[r] = v;
+      }
+      if (EPI == EPI_BIAS_GELU_D || (EPI == EPI_BIAS_GELU && !g.aux)) {
+        // packed GELU on the 4 values: _D stores gelu' in this (aux) round and keeps gelu in acc
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          const f32x2 x = {acc[i][j][2 * h2] + bias[2 * h2], acc[i][j][2 * h2 + 1] + bias[2 * h2 + 1]};
+          f32x2 gl, gd;
+          gelu2(x, gl, EPI == EPI_BIAS_GELU_D ? &gd : nullptr);
+          acc[i][j][2 * h2] = gl.x;
+          acc[i][j][2 * h2 + 1] = gl.y;
+          o[2 * h2] = EPI == EPI_BIAS_GELU_D ? gd.x : gl.x;
+          o[2 * h2 + 1] = EPI == EPI_BIAS_GELU_D ? gd.y : gl.y;
         }
       }
       st4(lp, o);
@@ -215,8 +221,15 @@ DEV void big_epilogue(const BigArgs& g, f32x4 (&acc)[8][4], bf16* lds, int m0, i
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int i = 0; i < 8; ++i)
+        if (EPI == EPI_BIAS_GELU) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][j][r] = EPI == EPI_BIAS_GELU_D ? acc[i][j][r] : gelu_f(acc[i][j][r]);
+          for (int h2 = 0; h2 < 2; ++h2) {
+            f32x2 gl;
+            gelu2(f32x2{acc[i][j][2 * h2], acc[i][j][2 * h2 + 1]}, gl, nullptr);
+            acc[i][j][2 * h2] = gl.x;
+            acc[i][j][2 * h2 + 1] = gl.y;
+          }
+        }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #pragma unroll
     for (int j = 0; j < 4; ++j)
