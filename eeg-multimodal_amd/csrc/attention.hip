@@ -29,6 +29,7 @@ struct AttnArgs {
   const void* o; const void* dout; void* dqkv; float* dq_acc;
   int B, H, L; long ld_qkv, ld_out; float scale;
   float p; uint64_t seed, offset;   // attention-probability dropout (p = 0: off)
+  uint32_t* bits;                   // dropout keep bits: written by the forward, read by the backward
 };
 
 // Dropout mask of the probabilities P[q][key] of head (b,h): element ((b*H+h)*L + q)*L + key of
@@ -68,6 +69,30 @@ DEV void attn_mask_bwd(const AttnArgs& a, int b, int h, long q0, long kb, int la
     const uint32_t rt = (uint32_t)__shfl((int)row, (lane & ~7) | t, 64);
     m8 |= ((rt >> s) & 1u) << t;               // bit t <-> (qf = t>>2, r = t&3)
   }
+}
+
+// Keep bits of the attention-probability dropout, row-major per (b, h): word (q, j) of L/32 words per
+// query row, bit t <-> key 32 j + t.  The forward stores them (a.bits non-null) so the backward reads
+// them instead of regenerating the Philox stream.  Forward lane (g, li) of query q holds nib[f]
+// (bit r <-> key k0 + 16 f + 4 g + r, f = 0..3, k0 % 64 == 0): the group's two words are OR-reduced
+// over the 4 lanes g (all lanes must call this) and stored by lanes g = 0.
+DEV void store_bits_fwd(const AttnArgs& a, int b, int h, long q, long k0, int g, const uint32_t (&nib)[4]) {
+  uint32_t w0 = (nib[0] << (4 * g)) | (nib[1] << (16 + 4 * g));
+  uint32_t w1 = (nib[2] << (4 * g)) | (nib[3] << (16 + 4 * g));
+  w0 |= (uint32_t)__shfl_xor((int)w0, 16, 64);
+  w1 |= (uint32_t)__shfl_xor((int)w1, 16, 64);
+  w0 |= (uint32_t)__shfl_xor((int)w0, 32, 64);
+  w1 |= (uint32_t)__shfl_xor((int)w1, 32, 64);
+  if (g == 0) *(uint2*)(a.bits + (((long)b * a.H + h) * a.L + q) * (a.L / 32) + k0 / 32) = make_uint2(w0, w1);
+}
+// Backward layout of the same bits (as attn_mask_bwd): bit t8 <-> row 16 (t8 >> 2) + 4 g + (t8 & 3) of the
+// rows starting at rowbits (wpr words per row), key kb + li.
+DEV uint32_t load_bits_bwd(const uint32_t* rowbits, int wpr, long kb, int g, int li) {
+  const int j = (int)((kb + li) >> 5), t = (int)((kb + li) & 31);
+  uint32_t m = 0;
+#pragma unroll
+  for (int t8 = 0; t8 < 8; ++t8) m |= ((rowbits[(16 * (t8 >> 2) + 4 * g + (t8 & 3)) * wpr + j] >> t) & 1u) << t8;
+  return m;
 }
 
 // Cooperative copy of `rows` x 64 elements (row stride `ld` in global) into LDS [rows][64+pad].
@@ -147,6 +172,7 @@ __global__ void __launch_bounds__(512) attn_fwd_kernel(AttnArgs a) {
     if (a.p > 0.f) {   // O accumulates dropout(P) V; the normaliser l stays the undropped sum
       uint32_t nib[4];
       attn_mask_fwd(a, b, h, q, k0, g, thr, nib);
+      if (a.bits) store_bits_fwd(a, b, h, q, k0, g, nib);
 #pragma unroll
       for (int f = 0; f < 4; ++f)
 #pragma unroll
@@ -245,7 +271,10 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(AttnArgs a) {
     uint32_t m8[2] = {0xFFu, 0xFFu};
     if (a.p > 0.f) {
 #pragma unroll
-      for (int f = 0; f < 2; ++f) attn_mask_bwd(a, b, h, q0, kw0 + 16 * f, lane, thr, m8[f]);
+      for (int f = 0; f < 2; ++f) {
+        if (a.bits) m8[f] = load_bits_bwd(a.bits + (((long)b * a.H + h) * a.L + q0) * (a.L / 32), a.L / 32, kw0 + 16 * f, g, li);
+        else attn_mask_bwd(a, b, h, q0, kw0 + 16 * f, lane, thr, m8[f]);
+      }
     }
 #pragma unroll
     for (int qf = 0; qf < 2; ++qf) {
@@ -336,16 +365,52 @@ __global__ void dq_convert_kernel(const float* dq_acc, void* dqkv, int is_bf16, 
   else ((float*)dqkv)[r * ld + c] = dq_acc[i];
 }
 
+#include "attention256.inc"
+
+// persistent L = 256 kernels: one workgroup per CU (capped by the item count)
+int l256_grid(int items) {
+  static const int cus = [] {
+    int dev = 0, n = 256;
+    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    return n > 0 ? n : 256;
+  }();
+  return items < cus ? items : cus;
+}
+}  // namespace
+
+// Which directions take the L = 256 kernels: bit 0 forward, bit 1 backward (eegf_tune key 2,
+// initial value from EEGF_ATTN256 = 0 / fwd / bwd / all).  Default forward only: the persistent
+// backward (attn_bwd256_kernel) measures slower than attn_bwd_kernel with dropout on.
+int g_attn256_mode = [] {
+  const char* e = getenv("EEGF_ATTN256");
+  if (!e) return 1;
+  if (e[0] == '0') return 0;
+  if (e[0] == 'b') return 2;
+  if (e[0] == 'a') return 3;
+  return 1;
+}();
+
+namespace {
+bool l256_path(int dtype, int L, const float* key_bias, bool bwd) {
+  return (g_attn256_mode & (bwd ? 2 : 1)) && dtype == EEGF_BF16 && L == LF && !key_bias;
+}
+
 }  // namespace
 
 extern "C" int eegf_attn_fwd(int dtype, int B, int H, int L, const void* qkv, long ld_qkv, const float* key_bias,
                              float scale, float drop_p, unsigned long long seed, unsigned long long offset,
-                             void* out, long ld_out, float* lse, hipStream_t stream) {
+                             void* out, long ld_out, float* lse, unsigned int* drop_bits, hipStream_t stream) {
   if (B <= 0 || H != 12 || L <= 0 || L % 128 != 0 || !qkv || !out || !lse || ld_qkv < 2304 || ld_out < 768)
     return EEGF_ERR_ARG;
   if (B > 65535 || drop_p < 0.f || drop_p >= 1.f) return EEGF_ERR_ARG;
   AttnArgs a{qkv, out, lse, key_bias, nullptr, nullptr, nullptr, nullptr, B, H, L, ld_qkv, ld_out, scale,
-             drop_p, seed, offset};
+             drop_p, seed, offset, drop_p > 0.f ? drop_bits : nullptr};
+  if (l256_path(dtype, L, key_bias, false) && !a.bits) {
+    const dim3 g1(l256_grid(B * H));
+    if (drop_p > 0.f) hipLaunchKernelGGL(attn_fwd256_kernel<true>, g1, dim3(512), 0, stream, a);
+    else hipLaunchKernelGGL(attn_fwd256_kernel<false>, g1, dim3(512), 0, stream, a);
+    return (int)hipGetLastError();
+  }
   const dim3 grid(L / 128, H, B);
   if (dtype == EEGF_F32) hipLaunchKernelGGL(attn_fwd_kernel<float>, grid, dim3(512), 0, stream, a);
   else if (dtype == EEGF_BF16) hipLaunchKernelGGL(attn_fwd_kernel<bf16>, grid, dim3(512), 0, stream, a);
@@ -358,13 +423,19 @@ extern "C" long eegf_attn_bwd_workspace(int B, int L) { return L > 256 ? (long)B
 extern "C" int eegf_attn_bwd(int dtype, int B, int H, int L, const void* qkv, long ld_qkv, const float* key_bias,
                              float scale, float drop_p, unsigned long long seed, unsigned long long offset,
                              const void* out, const void* dout, long ld_out, const float* lse,
-                             void* dqkv, float* dq_workspace, hipStream_t stream) {
+                             const unsigned int* drop_bits, void* dqkv, float* dq_workspace, hipStream_t stream) {
   if (B <= 0 || H != 12 || L <= 0 || L % 256 != 0 || !qkv || !out || !dout || !lse || !dqkv) return EEGF_ERR_ARG;
   if (ld_qkv < 2304 || ld_out < 768 || B > 65535 || drop_p < 0.f || drop_p >= 1.f) return EEGF_ERR_ARG;
   if (L > 256 && !dq_workspace) return EEGF_ERR_ARG;
   if (L > 256) hipMemsetAsync(dq_workspace, 0, sizeof(float) * (size_t)B * L * 768, stream);
   AttnArgs a{qkv, nullptr, const_cast<float*>(lse), key_bias, out, dout, dqkv, dq_workspace, B, H, L, ld_qkv, ld_out,
-             scale, drop_p, seed, offset};
+             scale, drop_p, seed, offset, drop_p > 0.f ? const_cast<uint32_t*>(drop_bits) : nullptr};
+  if (l256_path(dtype, L, key_bias, true)) {
+    const dim3 g1(l256_grid(B * H));
+    if (drop_p > 0.f) hipLaunchKernelGGL(attn_bwd256_kernel<true>, g1, dim3(512), 0, stream, a);
+    else hipLaunchKernelGGL(attn_bwd256_kernel<false>, g1, dim3(512), 0, stream, a);
+    return (int)hipGetLastError();
+  }
   const dim3 grid(L / 256, H, B);
   if (dtype == EEGF_F32) hipLaunchKernelGGL(attn_bwd_kernel<float>, grid, dim3(512), 0, stream, a);
   else if (dtype == EEGF_BF16) hipLaunchKernelGGL(attn_bwd_kernel<bf16>, grid, dim3(512), 0, stream, a);

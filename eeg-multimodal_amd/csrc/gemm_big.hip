@@ -374,6 +374,38 @@ DEV void stage_half(bf16* dst, const bf16* src, long ld, int base, int sh, int s
   }
 }
 
+// k-major half-tile image [64 k][128 local columns] (weight-gradient A and B, input-gradient B):
+// 2 glds per wave, each 4 k-rows x 256 B; local column lc maps to tile column
+// (lc >> sh) * stride + off + (lc & (2^sh - 1)) (the same half split as stage_half); the 16-B
+// chunk index is XOR-swizzled with swz_k(k) on the source side (conflict-free tr reads).
+DEV void stage_half_km(bf16* dst, const bf16* src, long ld, int base, int sh, int stride, int off, int cmax,
+                       int k0, int wave, int lane) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int K0 = (wave * 2 + j) * 4;
+    const int k = K0 + (lane >> 4);
+    const int lc = ((lane & 15) ^ swz_k(k)) * 8;
+    const int col = min(base + (lc >> sh) * stride + off + (lc & ((1 << sh) - 1)), cmax - 8);
+    glds16(src + (long)(k0 + k) * ld + col, dst + K0 * 128);
+  }
+}
+
+// rd_col on a k-major half image [64][128]: k-values k0..k0+7 of local column c0 + (lane&15)
+DEV bf16x8 rd_colh(const bf16* t, int k0, int c0, int lane) {
+  const int i = lane & 15, q = i >> 2, p = i & 3;
+  const int col = c0 + 4 * p;
+  const int ch = col >> 3, off = col & 7;
+  const int ka = k0 + q, kb = k0 + 4 + q;
+  const bf16* a0 = t + ka * 128 + (((ch ^ swz_k(ka)) << 3) | off);
+  const bf16* a1 = t + kb * 128 + (((ch ^ swz_k(kb)) << 3) | off);
+  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)a0);
+  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)a1);
+  bf16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
 DEV void vm_wait(int n) {      // s_waitcnt vmcnt(2n), n = younger half-tiles in flight (0..4)
   switch (n) {
     case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
@@ -389,7 +421,9 @@ DEV void raw_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int EPI, typename TO, int MODE>      // MODE 1: staggered groups; 2: lockstep; 3: staggered, no setprio
+// Layouts: AKC/BKC as gemm_big_kernel (row-major half images read with ds_read_b128, k-major ones
+// with ds_read_b64_tr_b16); fp32 output = split-K slabs over blockIdx.y as gemm_big_kernel.
+template <bool AKC, bool BKC, int EPI, typename TO, int MODE>   // MODE 1: staggered; 2: lockstep; 3: staggered, no setprio
 __global__ void __launch_bounds__(NT, 1) gemm8_kernel(BigArgs g) {
   constexpr bool STAG = MODE != 2, PRIO = MODE != 3;
   __shared__ __attribute__((aligned(16))) bf16 lds[LDS_ELEMS];
@@ -399,7 +433,9 @@ __global__ void __launch_bounds__(NT, 1) gemm8_kernel(BigArgs g) {
   const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
   const int tm = t / tiles_n, tn = t % tiles_n;
   const int m0 = tm * TM, n0 = tn * TN;
-  const int nk = g.K / BK;
+  int kbeg = 0, kend = g.K;
+  if (g.ksplit > 0) { kbeg = blockIdx.y * g.ksplit; kend = min(g.K, kbeg + g.ksplit); }
+  const int nk = (kend - kbeg) / BK;
 
   f32x4 acc[8][4];
 #pragma unroll
@@ -409,11 +445,22 @@ __global__ void __launch_bounds__(NT, 1) gemm8_kernel(BigArgs g) {
 
   // half-tile slots: buffer b at b*4*HALF: [A_h0][A_h1][B_h0][B_h1]
   auto stageA = [&](int tile, int h) {
-    stage_half(lds + (tile & 1) * 4 * HALF + h * HALF, g.A, g.lda, m0, 6, 128, 64 * h, g.M, tile * BK, wave, lane);
+    bf16* d = lds + (tile & 1) * 4 * HALF + h * HALF;
+    if (AKC) stage_half(d, g.A, g.lda, m0, 6, 128, 64 * h, g.M, kbeg + tile * BK, wave, lane);
+    else stage_half_km(d, g.A, g.lda, m0, 6, 128, 64 * h, g.M, kbeg + tile * BK, wave, lane);
   };
   auto stageB = [&](int tile, int h) {
-    stage_half(lds + (tile & 1) * 4 * HALF + (2 + h) * HALF, g.B, g.ldb, n0, 5, 64, 32 * h, g.N, tile * BK, wave,
-               lane);
+    bf16* d = lds + (tile & 1) * 4 * HALF + (2 + h) * HALF;
+    if (BKC) stage_half(d, g.B, g.ldb, n0, 5, 64, 32 * h, g.N, kbeg + tile * BK, wave, lane);
+    else stage_half_km(d, g.B, g.ldb, n0, 5, 64, 32 * h, g.N, kbeg + tile * BK, wave, lane);
+  };
+  auto rdB = [&](const bf16* Bh, int jj, int kc) {
+    return BKC ? rd_row(Bh, wn * 32 + jj * 16 + (lane & 15), 4 * kc + (lane >> 4))
+               : rd_colh(Bh, 32 * kc + 8 * (lane >> 4), wn * 32 + jj * 16, lane);
+  };
+  auto rdA = [&](const bf16* Ah, int ii, int kc) {
+    return AKC ? rd_row(Ah, wm * 64 + ii * 16 + (lane & 15), 4 * kc + (lane >> 4))
+               : rd_colh(Ah, 32 * kc + 8 * (lane >> 4), wm * 64 + ii * 16, lane);
   };
   // global phase phi = 4t + p stages: p0 B_h1(t+1), p1 A_h1(t+1), p2 A_h0(t+2), p3 B_h0(t+2)
   auto stage_tile_of = [&](int phi) { const int tt = phi >> 2, p = phi & 3; return tt + (p <= 1 ? 1 : 2); };
@@ -449,21 +496,21 @@ __global__ void __launch_bounds__(NT, 1) gemm8_kernel(BigArgs g) {
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj)
 #pragma unroll
-          for (int kc = 0; kc < 2; ++kc) br0[jj][kc] = rd_row(Ab + 2 * HALF, wn * 32 + jj * 16 + (lane & 15), 4 * kc + (lane >> 4));
+          for (int kc = 0; kc < 2; ++kc) br0[jj][kc] = rdB(Ab + 2 * HALF, jj, kc);
         __builtin_amdgcn_sched_barrier(0);
       }
       if (p == 1) {
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj)
 #pragma unroll
-          for (int kc = 0; kc < 2; ++kc) br1[jj][kc] = rd_row(Ab + 3 * HALF, wn * 32 + jj * 16 + (lane & 15), 4 * kc + (lane >> 4));
+          for (int kc = 0; kc < 2; ++kc) br1[jj][kc] = rdB(Ab + 3 * HALF, jj, kc);
       }
       if (p == 0 || p == 2) {
         const bf16* Ah = Ab + (p == 0 ? 0 : HALF);
 #pragma unroll
         for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
-          for (int kc = 0; kc < 2; ++kc) ar[ii][kc] = rd_row(Ah, wm * 64 + ii * 16 + (lane & 15), 4 * kc + (lane >> 4));
+          for (int kc = 0; kc < 2; ++kc) ar[ii][kc] = rdA(Ah, ii, kc);
       }
       // (b) stage one half-tile, (c) retire the one staged 4 phases ago
       stage_phase(phi);
@@ -495,13 +542,12 @@ __global__ void __launch_bounds__(NT, 1) gemm8_kernel(BigArgs g) {
 template <bool AKC, bool BKC, int EPI, typename TO>
 int launch_big(const BigArgs& a, int splits, hipStream_t s) {
   const int tiles = ((a.M + TM - 1) / TM) * ((a.N + TN - 1) / TN);
-  if constexpr (AKC && BKC && sizeof(TO) == 2) {
-    if (g_gemm8 && !a.colsum_part && splits == 1) {
-      if (g_gemm8 == 2) hipLaunchKernelGGL((gemm8_kernel<EPI, TO, 2>), dim3(tiles), dim3(NT), 0, s, a);
-      else if (g_gemm8 == 3) hipLaunchKernelGGL((gemm8_kernel<EPI, TO, 3>), dim3(tiles), dim3(NT), 0, s, a);
-      else hipLaunchKernelGGL((gemm8_kernel<EPI, TO, 1>), dim3(tiles), dim3(NT), 0, s, a);
-      return (int)hipGetLastError();
-    }
+  if (g_gemm8 && !a.colsum_part) {
+    const dim3 grid(tiles, splits);
+    if (g_gemm8 == 2) hipLaunchKernelGGL((gemm8_kernel<AKC, BKC, EPI, TO, 2>), grid, dim3(NT), 0, s, a);
+    else if (g_gemm8 == 3) hipLaunchKernelGGL((gemm8_kernel<AKC, BKC, EPI, TO, 3>), grid, dim3(NT), 0, s, a);
+    else hipLaunchKernelGGL((gemm8_kernel<AKC, BKC, EPI, TO, 1>), grid, dim3(NT), 0, s, a);
+    return (int)hipGetLastError();
   }
   if constexpr (AKC && !BKC && sizeof(TO) == 2) {
     if (a.colsum_part) {
@@ -596,8 +642,13 @@ int eegf_gemm_big_colsum_tiles(int M, int N, int K) {
   return (M + TM - 1) / TM;
 }
 
-// Tuning/A-B hook: key 1 = 8-phase schedule for the forward GEMMs (1 on, 0 off).  Returns the old value.
+extern int g_attn256_mode;     // attention.hip
+
+// Tuning / A-B hook (returns the old value): key 1 = 8-phase GEMM schedule (0 off, 1 staggered,
+// 2 lockstep, 3 staggered without setprio); key 2 = L = 256 attention kernels (bit 0 forward,
+// bit 1 backward).
 extern "C" int eegf_tune(int key, int value) {
   if (key == 1) { const int o = g_gemm8; g_gemm8 = value; return o; }
+  if (key == 2) { const int o = g_attn256_mode; g_attn256_mode = value; return o; }
   return EEGF_ERR_ARG;
 }

@@ -26,7 +26,7 @@ CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract
 
 
 def _headers() -> list[Path]:
-    return sorted(CSRC.glob("*.h")) + sorted(INCLUDE.glob("*.h"))
+    return sorted(CSRC.glob("*.h")) + sorted(CSRC.glob("*.inc")) + sorted(INCLUDE.glob("*.h"))
 
 
 def _needs(target: Path, deps: list[Path]) -> bool:

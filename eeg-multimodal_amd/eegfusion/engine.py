@@ -280,9 +280,12 @@ class FusionEngine:
                         self.a.span(pre + "attention.self.query.bias", 3), qkv, R, tag="qkv_fwd")
             ctx = self.empty(R, HID)
             lse = torch.empty(B, NH, L, dtype=torch.float32, device=self.a.device)
+            # the backward regenerates the dropout mask from the Philox stream (measured faster than
+            # storing the keep bits in the forward and reading them back)
+            bits = None
             ev = self._ev_start("attn_fwd")
             call("eegf_attn_fwd", self.code, B, NH, L, P(qkv), 3 * HID, P(kbias), scale, float(adrop), self.cfg.seed,
-                 sv.rng + 12 + 3 * i, P(ctx), HID, P(lse), _stream())
+                 sv.rng + 12 + 3 * i, P(ctx), HID, P(lse), P(bits), _stream())
             self._ev_end("attn_fwd", ev)
             ao = self.ws.get("ao", R * HID, self.dt).view(R, HID)
             self.linear(ctx, self.W(pre + "attention.output.dense.weight"), self.F(pre + "attention.output.dense.bias"),
@@ -303,7 +306,7 @@ class FusionEngine:
             s2, m2, r2 = (self.empty(R, HID), self._f32(R), self._f32(R)) if save else (None, None, None)
             self.ln_fwd(fo, a1, pre + "output.LayerNorm", R, h2, s2, m2, r2, 1e-12, pdrop, 1, sv.rng + 11 + 3 * i)
             if save:
-                layers.append(dict(h=h, qkv=qkv, ctx=ctx, lse=lse, a1=a1, ln1=(s1, m1, r1), ffgd=ffgd, ffact=ffact,
+                layers.append(dict(h=h, qkv=qkv, ctx=ctx, lse=lse, bits=bits, a1=a1, ln1=(s1, m1, r1), ffgd=ffgd, ffact=ffact,
                                    ln2=(s2, m2, r2)))
             h = h2
         t["layers"] = layers
@@ -567,8 +570,8 @@ class FusionEngine:
             self.dgrad(dao, self.W(pre + "attention.output.dense.weight"), dctx, R,
                        bias_grad=self.gbias(pre + "attention.output.dense.bias"))
             call("eegf_attn_bwd", self.code, B, NH, L, P(s["qkv"]), 3 * HID, P(t["kbias"]), scale, float(adrop),
-                 self.cfg.seed, sv.rng + 12 + 3 * i, P(s["ctx"]), P(dctx), HID, P(s["lse"]), P(dqkv), P(dq_ws),
-                 _stream())
+                 self.cfg.seed, sv.rng + 12 + 3 * i, P(s["ctx"]), P(dctx), HID, P(s["lse"]), P(s["bits"]), P(dqkv),
+                 P(dq_ws), _stream())
             qn = pre + "attention.self.query.weight"
             if self.need(qn):
                 gq = self.a.span(qn, 3, self.a.grad).view(3 * HID, HID)

@@ -106,18 +106,20 @@ int eegf_colsum(int dtype, const void* in, long ld, long rows, int width, int pe
  * (BertSelfAttention, modeling_bert.py:139-199).  key_bias [B, L]: 0 or -1e30 (nullable).
  * drop_p: dropout of the attention probabilities (modeling_bert.py:131,198; 0 = off), Philox
  * (seed, offset), element ((b*12+h)*L+q)*L+key.  out [B, L, ld_out>=768]; lse [B, 12, L] saved
- * for the backward.  L % 128 == 0. */
+ * for the backward.  drop_bits (nullable, used when drop_p > 0): receives the keep mask, one bit per
+ * probability, [B*12][L][L/32] u32, bit t of word j <-> key 32j+t, for eegf_attn_bwd.  L % 128 == 0. */
 int eegf_attn_fwd(int dtype, int B, int H, int L, const void* qkv, long ld_qkv, const float* key_bias,
                   float scale, float drop_p, unsigned long long seed, unsigned long long offset,
-                  void* out, long ld_out, float* lse, hipStream_t stream);
+                  void* out, long ld_out, float* lse, unsigned int* drop_bits, hipStream_t stream);
 /* fp32 workspace (elements) eegf_attn_bwd needs for dQ accumulation (0 when L <= 256). */
 long eegf_attn_bwd_workspace(int B, int L);
 /* Attention backward: writes dQ|dK|dV into dqkv [B, L, ld_qkv] (same layout as qkv).  drop_p,
- * seed, offset as in the forward (the mask is regenerated).  L % 256 == 0. */
+ * seed, offset as in the forward; drop_bits: the forward's keep mask (nullable: the mask is
+ * regenerated from the Philox stream).  L % 256 == 0. */
 int eegf_attn_bwd(int dtype, int B, int H, int L, const void* qkv, long ld_qkv, const float* key_bias,
                   float scale, float drop_p, unsigned long long seed, unsigned long long offset,
                   const void* out, const void* dout, long ld_out, const float* lse,
-                  void* dqkv, float* dq_workspace, hipStream_t stream);
+                  const unsigned int* drop_bits, void* dqkv, float* dq_workspace, hipStream_t stream);
 
 /* Decoder cross-attention over the BERT memory with a single query token
  * (TransformerDecoderLayer._mha_block, transformer.py:1177-1196; model.py:40-43), in the

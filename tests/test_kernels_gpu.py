@@ -120,6 +120,14 @@ def _attn_ref(qkv, B, L, kbias, zmask=None):
     return (p @ v).transpose(1, 2).reshape(B, L, 768)
 
 
+def _check_bits(bits, z, B, L):
+    """keep bits [B*12][L][L/32] (bit t of word j <-> key 32j+t) == the replayed Philox keep mask"""
+    w = bits.view(B, 12, L, L // 32).to(torch.int64) & 0xFFFFFFFF
+    t = torch.arange(32, device=w.device)
+    keep = ((w[..., None] >> t) & 1).view(B, 12, L, L)
+    assert torch.equal(keep.bool(), z > 0)
+
+
 def _attn_mask(B, L, p, seed, offset):
     from philox_ref import attn_mask
     e = torch.arange(B * 12 * L * L, dtype=torch.int64).numpy()
@@ -130,7 +138,8 @@ def _attn_mask(B, L, p, seed, offset):
 @pytest.mark.parametrize("L", [256, 512])
 @pytest.mark.parametrize("masked", [False, True])
 @pytest.mark.parametrize("pdrop", [0.0, 0.25])
-def test_attention_fwd_bwd(dt, L, masked, pdrop):
+@pytest.mark.parametrize("use_bits", [False, True])
+def test_attention_fwd_bwd(dt, L, masked, pdrop, use_bits):
     lib = _lib()
     torch.manual_seed(1)
     B = 2
@@ -145,12 +154,15 @@ def test_attention_fwd_bwd(dt, L, masked, pdrop):
         lib.call("eegf_key_bias", B * L, mask.data_ptr(), kbias.data_ptr(), _s())
     out = torch.empty(B, L, 768, device="cuda", dtype=dt)
     lse = torch.empty(B, 12, L, device="cuda")
+    bits = torch.zeros(B * 12 * L * L // 32, device="cuda", dtype=torch.int32)
     seed, off = 77, 5
     lib.call("eegf_attn_fwd", _code(dt), B, 12, L, qkv.data_ptr(), 2304, None if kbias is None else kbias.data_ptr(),
-             0.125, pdrop, seed, off, out.data_ptr(), 768, lse.data_ptr(), _s())
+             0.125, pdrop, seed, off, out.data_ptr(), 768, lse.data_ptr(), bits.data_ptr() if use_bits else None, _s())
     torch.cuda.synchronize()
     qr = qkv.double().clone().requires_grad_()
     z = _attn_mask(B, L, pdrop, seed, off) if pdrop > 0 else None
+    if z is not None and use_bits:     # the stored keep bits are the Philox mask
+        _check_bits(bits, z, B, L)
     if z is not None:
         assert abs((z > 0).double().mean().item() - (1 - pdrop)) < 0.01
     ref = _attn_ref(qr, B, L, kbias, z)
@@ -161,7 +173,8 @@ def test_attention_fwd_bwd(dt, L, masked, pdrop):
     ws_n = lib.lib().eegf_attn_bwd_workspace(B, L)
     ws = torch.empty(max(ws_n, 1), device="cuda")
     lib.call("eegf_attn_bwd", _code(dt), B, 12, L, qkv.data_ptr(), 2304, None if kbias is None else kbias.data_ptr(),
-             0.125, pdrop, seed, off, out.data_ptr(), dout.data_ptr(), 768, lse.data_ptr(), dqkv.data_ptr(), ws.data_ptr(), _s())
+             0.125, pdrop, seed, off, out.data_ptr(), dout.data_ptr(), 768, lse.data_ptr(),
+             bits.data_ptr() if use_bits else None, dqkv.data_ptr(), ws.data_ptr(), _s())
     torch.cuda.synchronize()
     for sl, name in ((slice(0, 768), "dq"), (slice(768, 1536), "dk"), (slice(1536, 2304), "dv")):
         e = _rel(dqkv[..., sl], qr.grad[..., sl])
@@ -394,3 +407,46 @@ def test_window_tokens(dt):
     lib.call("eegf_window_tokens", _code(dt), 3, 64, 256, eeg.data_ptr(), tok.data_ptr(), _s())
     torch.cuda.synchronize()
     assert torch.equal(tok, eeg.transpose(1, 2).reshape(-1, 64).to(dt))
+
+
+@pytest.mark.parametrize("pdrop", [0.0, 0.1])
+@pytest.mark.parametrize("mode", [1, 3])
+def test_attention_l256_persistent(pdrop, mode):
+    """L = 256 bf16 path with more (b, h) items than workgroups: every persistent workgroup runs
+    several items (next-item K/V/Q prefetch, chunk stream across items).  mode (eegf_tune key 2):
+    1 = persistent forward (default), 3 = persistent forward and backward."""
+    lib = _lib()
+    lib.lib().eegf_tune.argtypes = [lib.i32, lib.i32]
+    old = lib.lib().eegf_tune(2, mode)
+    try:
+        _attention_l256(lib, pdrop)
+    finally:
+        lib.lib().eegf_tune(2, old)
+
+
+def _attention_l256(lib, pdrop):
+    torch.manual_seed(4)
+    B, L, dt = 24, 256, torch.bfloat16
+    qkv = torch.randn(B, L, 2304, device="cuda").to(dt)
+    out = torch.empty(B, L, 768, device="cuda", dtype=dt)
+    lse = torch.empty(B, 12, L, device="cuda")
+    seed, off = 123, 9
+    lib.call("eegf_attn_fwd", _code(dt), B, 12, L, qkv.data_ptr(), 2304, None, 0.125, pdrop, seed, off,
+             out.data_ptr(), 768, lse.data_ptr(), None, _s())
+    torch.cuda.synchronize()
+    qr = qkv.double().clone().requires_grad_()
+    z = _attn_mask(B, L, pdrop, seed, off) if pdrop > 0 else None
+    ref = _attn_ref(qr, B, L, None, z)
+    assert _rel(out, ref) < _tol(dt)
+    q, k, _ = qkv.double().view(B, L, 3, 12, 64).unbind(2)
+    s = (q.transpose(1, 2) @ k.transpose(1, 2).transpose(-1, -2)) / 8.0
+    assert (lse.double() - torch.logsumexp(s, -1)).abs().max().item() < 1e-2
+    dout = torch.randn(B, L, 768, device="cuda").to(dt)
+    ref.backward(dout.double())
+    dqkv = torch.full_like(qkv, float("nan"))
+    lib.call("eegf_attn_bwd", _code(dt), B, 12, L, qkv.data_ptr(), 2304, None, 0.125, pdrop, seed, off,
+             out.data_ptr(), dout.data_ptr(), 768, lse.data_ptr(), None, dqkv.data_ptr(), None, _s())
+    torch.cuda.synchronize()
+    for sl, name in ((slice(0, 768), "dq"), (slice(768, 1536), "dk"), (slice(1536, 2304), "dv")):
+        e = _rel(dqkv[..., sl], qr.grad[..., sl])
+        assert e < _tol(dt) * 3, (name, e)

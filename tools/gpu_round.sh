@@ -1,0 +1,23 @@
+#!/bin/bash
+# One GPU session: parity tests, GEMM schedule A/B, bench line, rocprofv3 kernel stats.
+# usage (on the box, from the repo root): bash tools/gpu_round.sh <tag> [steps...]
+set -o pipefail
+TAG=${1:-r1}
+O=gpurun_out
+mkdir -p $O
+export PYTHONUNBUFFERED=1
+step() { local name=$1; shift; echo "[gpu_round] $name" ; "$@"; local rc=$?; echo "[gpu_round] $name rc=$rc"; return $rc; }
+for s in "${@:2}"; do
+  case $s in
+    tests) step tests timeout -k 10 420 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/${TAG}_gpu_tests.log 2>&1 || exit 1 ;;
+    gemm8tests) EEGF_GEMM8=1 step gemm8tests timeout -k 10 300 python -u -m pytest tests/test_gemm_gpu.py -x -q --timeout 120 --timeout-method thread > $O/${TAG}_gemm8_tests.log 2>&1 || exit 1 ;;
+    gemmab) step gemmab timeout -k 10 300 python -u tools/gemm_bench.py --ab > $O/${TAG}_gemm_ab.log 2>&1 || exit 1 ;;
+    attn) step attn timeout -k 10 120 python -u tools/attn_bench.py > $O/${TAG}_attn.log 2>&1 && EEGF_ATTN256=0 step attn0 timeout -k 10 120 python -u tools/attn_bench.py >> $O/${TAG}_attn.log 2>&1 || exit 1 ;;
+    attntests) step attntests timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread -k "attention" > $O/${TAG}_attn_tests.log 2>&1 || exit 1 ;;
+    gemm) step gemm timeout -k 10 300 python -u tools/gemm_bench.py > $O/${TAG}_gemm.log 2>&1 || exit 1 ;;
+    bench) step bench timeout -k 10 400 python -u bench.py > $O/${TAG}_bench.json 2> $O/${TAG}_bench.err || exit 1 ;;
+    prof) (cd /tmp && export TMPDIR=/tmp && step prof timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$O/${TAG}_prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 4 --warmup 2 --no-cpu-baseline > $GRAFT_REPO_ROOT/$O/${TAG}_prof.log 2>&1) || exit 1 ;;
+    smoke) step smoke timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/${TAG}_smoke.log 2>&1 || exit 1 ;;
+  esac
+done
+echo "[gpu_round] done"
