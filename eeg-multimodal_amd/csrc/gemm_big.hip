@@ -34,7 +34,9 @@ struct BigArgs {
   float alpha, beta, epi_scale;
   int ksplit;            // >0: split-K slice length; C = fp32 slabs [blockIdx.y][M][N]
   float* colsum_part;    // AKC only: [tiles_m][K] partial column sums of A (nullable)
+  int prio;              // 1: waves 4-7 run at s_setprio 1 for the whole kernel (eegf_tune key 3)
 };
+int g_big_prio = [] { const char* e = getenv("EEGF_GEMM_PRIO"); return e ? atoi(e) : 0; }();
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) const void glb_void;
@@ -256,6 +258,7 @@ __global__ void __launch_bounds__(NT, 1) gemm_big_kernel(BigArgs g) {
   const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
   const int tm = t / tiles_n, tn = t % tiles_n;
   const int m0 = tm * TM, n0 = tn * TN;
+  if (g.prio && wave >= 4) __builtin_amdgcn_s_setprio(1);   // static priority for the younger half
 
   f32x4 acc[8][4];
 #pragma unroll
@@ -360,7 +363,7 @@ __global__ void __launch_bounds__(NT, 1) gemm_big_kernel(BigArgs g) {
 //   Every stage lands >= 2 phases after the last read of the half it overwrites (WAR with the
 //   stagger); each phase's vmcnt retires the half staged 4 phases earlier, read >= 1 phase later.
 constexpr int HALF = 128 * BK;                // elements per half-tile (16 KB)
-int g_gemm8 = [] { const char* e = getenv("EEGF_GEMM8"); return e ? atoi(e) : 0; }();
+int g_gemm8 = [] { const char* e = getenv("EEGF_GEMM8"); return e ? atoi(e) : -1; }();   // -1: auto
 
 DEV void stage_half(bf16* dst, const bf16* src, long ld, int base, int sh, int stride, int off, int rmax, int k0,
                     int wave, int lane) {
@@ -423,10 +426,18 @@ DEV void raw_barrier() {
 
 // Layouts: AKC/BKC as gemm_big_kernel (row-major half images read with ds_read_b128, k-major ones
 // with ds_read_b64_tr_b16); fp32 output = split-K slabs over blockIdx.y as gemm_big_kernel.
-template <bool AKC, bool BKC, int EPI, typename TO, int MODE>   // MODE 1: staggered; 2: lockstep; 3: staggered, no setprio
+// MODE 1: staggered groups, per-phase vmcnt; 2: lockstep, per-phase vmcnt; 3: as 1 without setprio;
+// 4: lockstep with one vmcnt per K-tile (phase 3: every half staged up to phase 1 of this tile retired,
+//    the two younger ones stay in flight across the barrier).
+// CS: fused column sums of A (as gemm_big_kernel's): in workgroups of tile column 0, waves 0-3 contract
+// 32 local rows of A_h0 at phase 0 and waves 4-7 32 rows of A_h1 at phase 2 against a ones operand
+// (4 extra MFMAs per K-tile); the 8 partials go through red[2][8][64] in LDS and wave 0 folds the
+// previous K-tile's into ks[K] at phase 1.
+template <bool AKC, bool BKC, int EPI, typename TO, int MODE, bool CS = false>
 __global__ void __launch_bounds__(NT, 1) gemm8_kernel(BigArgs g) {
-  constexpr bool STAG = MODE != 2, PRIO = MODE != 3;
-  __shared__ __attribute__((aligned(16))) bf16 lds[LDS_ELEMS];
+  constexpr bool STAG = MODE == 1 || MODE == 3, PRIO = MODE != 3, TILEWAIT = MODE == 4;
+  // CS: operand ring 128 KB | red[2][8][64] 4 KB | ks[K] fp32 12 KB  (the epilogue reuses the front)
+  __shared__ __attribute__((aligned(16))) bf16 lds[CS ? (8 * HALF + 1024 * 2 + CS_KMAX * 2) : LDS_ELEMS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
   const int tiles_n = (g.N + TN - 1) / TN, tiles_m = (g.M + TM - 1) / TM;
@@ -480,10 +491,24 @@ __global__ void __launch_bounds__(NT, 1) gemm8_kernel(BigArgs g) {
   };
 
   // prologue = the stages of phases -6 .. -1
+  auto younger2 = [&](int phi) {      // real stages among phases phi-1, phi
+    return (stage_tile_of(phi - 1) < nk ? 1 : 0) + (stage_tile_of(phi) < nk ? 1 : 0);
+  };
   for (int phi = -6; phi < 0; ++phi) stage_phase(phi);
-  vm_wait(younger(-1));               // retires phases -6, -5 (A_h0(0), B_h0(0))
+  if (TILEWAIT) vm_wait(younger2(-1));  // retires phases -6 .. -3 (every half of tile 0)
+  else vm_wait(younger(-1));          // retires phases -6, -5 (A_h0(0), B_h0(0))
   raw_barrier();
   if (STAG && wm == 1) raw_barrier();  // stagger group 1 by one barrier
+
+  const bool do_cs = CS && AKC && tn == 0;
+  float* red = (float*)(lds + 8 * HALF);
+  float* ks = red + 2 * 8 * 64;
+  const int cs_h = wave >> 2, cs_lr0 = 32 * (wave & 3);     // half, first local row of this wave's 32
+  // valid rows of the lane's 8-row group (local row lr of half h = tile row (lr >> 6) 128 + 64 h + (lr & 63))
+  const int cs_rows = g.M - m0 - ((cs_lr0 >> 6) * 128 + 64 * cs_h + (cs_lr0 & 63) + 8 * (lane >> 4));
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (bf16)(e < cs_rows ? 1.0f : 0.0f);
 
   bf16x8 ar[4][2], br0[2][2], br1[2][2];
   for (int kt = 0; kt < nk; ++kt) {
@@ -491,6 +516,24 @@ __global__ void __launch_bounds__(NT, 1) gemm8_kernel(BigArgs g) {
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const int phi = 4 * kt + p;
+      if (CS && do_cs) {
+        if (p == 2 * cs_h) {            // this K-tile's column sums over the wave's 32 rows
+          const bf16* Ah = Ab + cs_h * HALF;
+#pragma unroll
+          for (int f = 0; f < 4; ++f) {
+            const f32x4 c = mma16(ones, rd_col_rm(Ah, cs_lr0 + 8 * (lane >> 4), 16 * f, lane), f32x4{0.f, 0.f, 0.f, 0.f});
+            if (lane < 16) red[(kt & 1) * 512 + wave * 64 + 16 * f + lane] = c[0];
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");    // visible after this phase's barrier
+        }
+        if (p == 1 && kt > 0 && tid < 64) {
+          const float* rp = red + ((kt - 1) & 1) * 512;
+          float v = 0.f;
+#pragma unroll
+          for (int w = 0; w < 8; ++w) v += rp[w * 64 + tid];
+          ks[(kt - 1) * BK + tid] = v;
+        }
+      }
       // (a) fragment reads of this phase's quadrant
       if (p == 0) {
 #pragma unroll
@@ -514,7 +557,8 @@ __global__ void __launch_bounds__(NT, 1) gemm8_kernel(BigArgs g) {
       }
       // (b) stage one half-tile, (c) retire the one staged 4 phases ago
       stage_phase(phi);
-      vm_wait(younger(phi));
+      if (!TILEWAIT) vm_wait(younger(phi));
+      else if (p == 3) vm_wait(younger2(phi));
       raw_barrier();
       // (e) the quadrant's 16 MFMAs
       const int mh = (p == 0 || p == 1) ? 0 : 1, nh = (p == 1 || p == 2) ? 1 : 0;
@@ -535,6 +579,19 @@ __global__ void __launch_bounds__(NT, 1) gemm8_kernel(BigArgs g) {
   if (STAG && wm == 0) raw_barrier();  // re-align the groups
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if (CS) {
+    if (do_cs && tid < 64) {
+      const float* rp = red + ((nk - 1) & 1) * 512;
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) v += rp[w * 64 + tid];
+      ks[(nk - 1) * BK + tid] = v;
+    }
+    __syncthreads();
+    if (do_cs)
+      for (int k = tid; k < g.K; k += NT) g.colsum_part[(long)tm * g.K + k] = ks[k];
+    __syncthreads();               // the epilogue reuses the front of the LDS
+  }
   // acc[i][j]: i = 4*mh + ii -> rows wm*128 + 64*mh + 16*ii = wm*128 + 16*i (same map as gemm_big)
   big_epilogue<EPI, TO>(g, acc, lds, m0, n0, tid, lane, wm, wn);
 }
@@ -542,9 +599,27 @@ __global__ void __launch_bounds__(NT, 1) gemm8_kernel(BigArgs g) {
 template <bool AKC, bool BKC, int EPI, typename TO>
 int launch_big(const BigArgs& a, int splits, hipStream_t s) {
   const int tiles = ((a.M + TM - 1) / TM) * ((a.N + TN - 1) / TN);
-  if (g_gemm8 && !a.colsum_part) {
+  if (g_gemm8 < 0) {
+    // default schedule (tools/gemm_bench.py --ab, profiles/r1s2_gemm_ab.log): the 8-phase lockstep
+    // schedule with one vmcnt per K-tile for the input-gradient GEMMs (+10-25 %) and the forward
+    // GEMMs except the smallest (N, K <= 768); the 2-phase kernel for the weight gradients
+    const bool use8 = sizeof(TO) == 2 && AKC && (!BKC || a.N > 768 || a.K > 768);
+    if (use8) {
+      if constexpr (AKC && !BKC && sizeof(TO) == 2) {
+        if (a.colsum_part) {
+          hipLaunchKernelGGL((gemm8_kernel<AKC, BKC, EPI, TO, 4, true>), dim3(tiles, splits), dim3(NT), 0, s, a);
+          return (int)hipGetLastError();
+        }
+      }
+      if (!a.colsum_part) {
+        hipLaunchKernelGGL((gemm8_kernel<AKC, BKC, EPI, TO, 4>), dim3(tiles, splits), dim3(NT), 0, s, a);
+        return (int)hipGetLastError();
+      }
+    }
+  } else if (g_gemm8 && !a.colsum_part) {
     const dim3 grid(tiles, splits);
     if (g_gemm8 == 2) hipLaunchKernelGGL((gemm8_kernel<AKC, BKC, EPI, TO, 2>), grid, dim3(NT), 0, s, a);
+    else if (g_gemm8 == 4) hipLaunchKernelGGL((gemm8_kernel<AKC, BKC, EPI, TO, 4>), grid, dim3(NT), 0, s, a);
     else if (g_gemm8 == 3) hipLaunchKernelGGL((gemm8_kernel<AKC, BKC, EPI, TO, 3>), grid, dim3(NT), 0, s, a);
     else hipLaunchKernelGGL((gemm8_kernel<AKC, BKC, EPI, TO, 1>), grid, dim3(NT), 0, s, a);
     return (int)hipGetLastError();
@@ -585,7 +660,7 @@ int eegf_gemm_big(int a_kc, int b_kc, int epi, int out_f32, int M, int N, int K,
   if (lda % 8 || ldb % 8 || ldc % 8 || (aux && ldaux % 8)) return 1;
   if ((((uintptr_t)A | (uintptr_t)B | (uintptr_t)C | (uintptr_t)aux) & 15) != 0) return 1;
   BigArgs a{(const bf16*)A, (const bf16*)B, C, bias, (bf16*)aux, lda, ldb, ldc, ldaux, M, N, K, alpha, beta,
-            epi_scale, 0, a_colsum};
+            epi_scale, 0, a_colsum, g_big_prio};
   if (a_colsum && (!a_kc || out_f32)) return 1;
   if (out_f32) {
     if (a_kc || b_kc || epi != EPI_NONE || M < 256 || N < 256 || K < 4096 || ldc % 4) return 1;
@@ -644,11 +719,13 @@ int eegf_gemm_big_colsum_tiles(int M, int N, int K) {
 
 extern int g_attn256_mode;     // attention.hip
 
-// Tuning / A-B hook (returns the old value): key 1 = 8-phase GEMM schedule (0 off, 1 staggered,
-// 2 lockstep, 3 staggered without setprio); key 2 = L = 256 attention kernels (bit 0 forward,
-// bit 1 backward).
+// Tuning / A-B hook (returns the old value): key 1 = 8-phase GEMM schedule (-1 auto (default), 0 off,
+// 1 staggered, 2 lockstep, 3 staggered without setprio, 4 lockstep with one vmcnt per K-tile); key 2 = L = 256
+// attention kernels (bit 0 forward, bit 1 backward); key 3 = static s_setprio 1 for waves 4-7 of the
+// 2-phase 256x256 kernel.
 extern "C" int eegf_tune(int key, int value) {
   if (key == 1) { const int o = g_gemm8; g_gemm8 = value; return o; }
   if (key == 2) { const int o = g_attn256_mode; g_attn256_mode = value; return o; }
+  if (key == 3) { const int o = g_big_prio; g_big_prio = value; return o; }
   return EEGF_ERR_ARG;
 }

@@ -77,14 +77,16 @@ def run(name, M, N, Kd, layout, epi, iters=20):
         for fn in (f, tf):
             fn()
         torch.cuda.synchronize()
-        r = {0: [], 1: [], 2: [], 3: []}
+        r = {v: [] for v in VARIANTS}
         for _ in range(5):
-            for v in (0, 1, 2, 3):
-                lib.eegf_tune(1, v)
+            for v in VARIANTS:
+                lib.eegf_tune(1, v if v < 5 else 0)      # 5: 2-phase with static priority; -1: default routing
+                lib.eegf_tune(3, 1 if v == 5 else 0)
                 f()
                 torch.cuda.synchronize()
                 r[v].append(timed(f, iters))
-        lib.eegf_tune(1, 1)
+        lib.eegf_tune(1, -1)
+        lib.eegf_tune(3, 0)
         med = {v: sorted(x)[len(x) // 2] for v, x in r.items()}
         tt = timed(tf, iters)
         print(f"{name:16s} {M}x{N}x{Kd} " + " | ".join(f"v{v} {tf_(med[v]):6.1f}" for v in med)
@@ -102,6 +104,7 @@ def run(name, M, N, Kd, layout, epi, iters=20):
 
 
 AB = "--ab" in sys.argv
+VARIANTS = [int(x) for x in next((a.split("=")[1] for a in sys.argv if a.startswith("--variants=")), "0,1,2,3,4").split(",")]
 
 
 if __name__ == "__main__":
