@@ -27,6 +27,7 @@ struct GemmArgs {
   float alpha, beta, epi_scale;
   int ksplit;          // >0: split-K slice length (grid.z = slices, C = fp32 slabs [z][M][N])
   int lds_epi;         // LDS-staged coalesced epilogue (bf16 out, beta == 0)
+  int bt;              // output tile: 128 or 64
 };
 
 DEV void load4(const float* p, float (&v)[4]) { const f32x4 x = *(const f32x4*)p; v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3]; }
@@ -57,29 +58,31 @@ DEV void tile_io(bf16* lds, int ldl, bf16* gp, long ld, int m0, int n0, int M, i
   }
 }
 
-template <typename T>
+template <typename T, int BT = 128>
 struct TileCfg {
   static constexpr int KT = 128 / (int)sizeof(T);        // contraction elements per k-step
   static constexpr int VE = 16 / (int)sizeof(T);         // elements per 16-B chunk
-  // K-contiguous LDS tile: [128 rows][KT] + 16 B pad per row
+  // K-contiguous LDS tile: [BT rows][KT] + 16 B pad per row
   static constexpr int RS_KC = KT + VE;
-  // k-major LDS tile: [KT rows][128] + 32 B pad per row
-  static constexpr int RS_KM = 128 + 2 * VE;
-  static constexpr int SZ_KC = 128 * RS_KC;
+  // k-major LDS tile: [KT rows][BT] + 32 B pad per row
+  static constexpr int RS_KM = BT + 2 * VE;
+  static constexpr int SZ_KC = BT * RS_KC;
   static constexpr int SZ_KM = KT * RS_KM;
+  static constexpr int CHUNKS = BT * 8 / NT;             // 16-B chunks per thread per operand tile
 };
 
-// Load one 16-KB operand tile into 4 x 16-B registers per thread (guarded at the edges).
-// rows_is_mn: true for the K-contiguous layout (tile rows = m or n index).
-template <typename T, bool KC>
-DEV void load_tile(u32x4 (&reg)[4], const T* __restrict__ base, long ld, int mn0, int k0, int MN, int K, int tid) {
-  using C = TileCfg<T>;
+// Load one operand tile (BT x 128 B) into CHUNKS x 16-B registers per thread (guarded at the edges).
+// KC: the K-contiguous layout (tile rows = m or n index).
+template <typename T, bool KC, int BT>
+DEV void load_tile(u32x4* reg, const T* __restrict__ base, long ld, int mn0, int k0, int MN,
+                   int K, int tid) {
+  using C = TileCfg<T, BT>;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < C::CHUNKS; ++i) {
     const int c = tid + NT * i;
     int r, col;            // r = tile row, col = element offset within row
     if (KC) { r = c >> 3; col = (c & 7) * C::VE; }
-    else    { constexpr int CPR = 128 / C::VE; r = c / CPR; col = (c % CPR) * C::VE; }
+    else    { constexpr int CPR = BT / C::VE; r = c / CPR; col = (c % CPR) * C::VE; }
     const int row_idx = KC ? mn0 + r : k0 + r;       // index along the strided axis
     const int col_idx = KC ? k0 + col : mn0 + col;   // index along the contiguous axis
     const int row_lim = KC ? MN : K;
@@ -100,22 +103,25 @@ DEV void load_tile(u32x4 (&reg)[4], const T* __restrict__ base, long ld, int mn0
   }
 }
 
-template <typename T, bool KC>
-DEV void store_tile(T* lds, const u32x4 (&reg)[4], int tid) {
-  using C = TileCfg<T>;
+template <typename T, bool KC, int BT>
+DEV void store_tile(T* lds, const u32x4* reg, int tid) {
+  using C = TileCfg<T, BT>;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < C::CHUNKS; ++i) {
     const int c = tid + NT * i;
     int r, col;
     if (KC) { r = c >> 3; col = (c & 7) * C::VE; }
-    else    { constexpr int CPR = 128 / C::VE; r = c / CPR; col = (c % CPR) * C::VE; }
+    else    { constexpr int CPR = BT / C::VE; r = c / CPR; col = (c % CPR) * C::VE; }
     st16(lds + r * (KC ? C::RS_KC : C::RS_KM) + col, reg[i]);
   }
 }
 
-template <typename T, bool AKC, bool BKC, typename TO, int EPI>
+// BT: output tile BT x BT (128, or 64 for the batch-row GEMMs whose 128-tile grids would leave most
+// CUs idle); 4 waves in 2 x 2, each a (BT/2) x (BT/2) block of NI x NI 16x16 accumulators.
+template <typename T, bool AKC, bool BKC, typename TO, int EPI, int BT = 128>
 __global__ void __launch_bounds__(NT) gemm_kernel(GemmArgs g) {
-  using C = TileCfg<T>;
+  using C = TileCfg<T, BT>;
+  constexpr int WT = BT / 2, NI = WT / 16;
   using F = typename Frag8<T>::type;
   constexpr int SZA = AKC ? C::SZ_KC : C::SZ_KM;
   constexpr int SZB = BKC ? C::SZ_KC : C::SZ_KM;
@@ -125,10 +131,10 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmArgs g) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int tiles_n = (g.N + BN - 1) / BN, tiles_m = (g.M + BM - 1) / BM;
+  const int tiles_n = (g.N + BT - 1) / BT, tiles_m = (g.M + BT - 1) / BT;
   const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
   const int tm = t / tiles_n, tn = t % tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
+  const int m0 = tm * BT, n0 = tn * BT;
   const int z = blockIdx.y;
   int kbeg = 0, kend = g.K;
   if (g.ksplit > 0) { kbeg = blockIdx.z * g.ksplit; kend = min(g.K, kbeg + g.ksplit); }
@@ -137,48 +143,48 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmArgs g) {
   const T* B = (const T*)g.B + (long)z * g.sB;
 
   // acc[i][j] holds the TRANSPOSED 16x16 tile (operands swapped in the MFMA): lane l owns
-  // C[m = m0 + wm*64 + 16i + (l&15)][n = n0 + wn*64 + 16j + 4*(l>>4) + r], r = 0..3, i.e. four
+  // C[m = m0 + wm*WT + 16i + (l&15)][n = n0 + wn*WT + 16j + 4*(l>>4) + r], r = 0..3, i.e. four
   // consecutive columns of one row -> 8/16-byte epilogue loads and stores.
-  f32x4 acc[4][4];
+  f32x4 acc[NI][NI];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < NI; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  u32x4 ra[4], rb[4];
+  u32x4 ra[C::CHUNKS], rb[C::CHUNKS];
   const int nk = (kend - kbeg + C::KT - 1) / C::KT;
-  load_tile<T, AKC>(ra, A, g.lda, m0, kbeg, g.M, kend, tid);
-  load_tile<T, BKC>(rb, B, g.ldb, n0, kbeg, g.N, kend, tid);
+  load_tile<T, AKC, BT>(ra, A, g.lda, m0, kbeg, g.M, kend, tid);
+  load_tile<T, BKC, BT>(rb, B, g.ldb, n0, kbeg, g.N, kend, tid);
 
   for (int kt = 0; kt < nk; ++kt) {
     __syncthreads();                     // previous k-step's LDS reads are done
-    store_tile<T, AKC>(As, ra, tid);
-    store_tile<T, BKC>(Bs, rb, tid);
+    store_tile<T, AKC, BT>(As, ra, tid);
+    store_tile<T, BKC, BT>(Bs, rb, tid);
     __syncthreads();
     if (kt + 1 < nk) {                   // issue next k-step's global loads under the MFMAs
-      load_tile<T, AKC>(ra, A, g.lda, m0, kbeg + (kt + 1) * C::KT, g.M, kend, tid);
-      load_tile<T, BKC>(rb, B, g.ldb, n0, kbeg + (kt + 1) * C::KT, g.N, kend, tid);
+      load_tile<T, AKC, BT>(ra, A, g.lda, m0, kbeg + (kt + 1) * C::KT, g.M, kend, tid);
+      load_tile<T, BKC, BT>(rb, B, g.ldb, n0, kbeg + (kt + 1) * C::KT, g.N, kend, tid);
     }
 #pragma unroll
     for (int kc = 0; kc < C::KT / 32; ++kc) {
-      F a[4], b[4];
+      F a[NI], b[NI];
       const int kk = kc * 32 + 8 * (lane >> 4);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = wm * 64 + i * 16;
+      for (int i = 0; i < NI; ++i) {
+        const int r = wm * WT + i * 16;
         if (AKC) a[i] = ld_row8(As + (r + (lane & 15)) * C::RS_KC + kk);
         else     a[i] = ld_col8(As, C::RS_KM, kk, r, lane);
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c = wn * 64 + j * 16;
+      for (int j = 0; j < NI; ++j) {
+        const int c = wn * WT + j * 16;
         if (BKC) b[j] = ld_row8(Bs + (c + (lane & 15)) * C::RS_KC + kk);
         else     b[j] = ld_col8(Bs, C::RS_KM, kk, c, lane);
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < NI; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mma16(b[j], a[i], acc[i][j]);
+        for (int j = 0; j < NI; ++j) acc[i][j] = mma16(b[j], a[i], acc[i][j]);
     }
   }
 
@@ -186,12 +192,12 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmArgs g) {
   if (g.ksplit > 0) {                    // split-K: raw fp32 partial slab, reduced by gemm_splitk_reduce
     float* slab = (float*)g.C + (long)blockIdx.z * g.M * g.N;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+    for (int i = 0; i < NI; ++i) {
+      const int m = m0 + wm * WT + i * 16 + (lane & 15);
       if (m >= g.M) continue;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+      for (int j = 0; j < NI; ++j) {
+        const int n = n0 + wn * WT + j * 16 + 4 * (lane >> 4);
         float* cp = slab + (long)m * g.N + n;
         const f32x4 v = acc[i][j] * g.alpha;
         if (n + 3 < g.N && ((uintptr_t)cp & 15) == 0) *(f32x4*)cp = v;
@@ -210,7 +216,7 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmArgs g) {
                            EPI == EPI_BIAS_GELU_D || EPI == EPI_MUL_AUX;
   constexpr bool AUX_IN = EPI == EPI_DGELU || EPI == EPI_DRELU || EPI == EPI_DTANH || EPI == EPI_MUL_AUX;
   constexpr bool TWO_OUT = EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_D;   // C and aux both written
-  if constexpr (sizeof(TO) == 2 && sizeof(T) == 2) {
+  if constexpr (sizeof(TO) == 2 && sizeof(T) == 2 && BT == 128) {
     if (g.beta == 0.f && g.lds_epi) {
       // LDS-staged epilogue: the 128x128 bf16 tile goes through LDS so every global access is a
       // full 16-B-per-lane row segment (a wave writes 4 x 256-B rows per instruction).
@@ -279,8 +285,8 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmArgs g) {
     }
   }
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+  for (int j = 0; j < NI; ++j) {
+    const int n = n0 + wn * WT + j * 16 + 4 * (lane >> 4);
     if (n >= g.N) continue;
     const bool nfull = n + 3 < g.N;
     float bias[4] = {0.f, 0.f, 0.f, 0.f};
@@ -293,8 +299,8 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmArgs g) {
       }
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+    for (int i = 0; i < NI; ++i) {
+      const int m = m0 + wm * WT + i * 16 + (lane & 15);
       if (m >= g.M) continue;
       TO* cp = Cp + (long)m * g.ldc + n;
       TO* ap = HAS_AUX && g.aux ? aux + (long)m * g.ldaux + n : nullptr;
@@ -402,8 +408,13 @@ int splitk_reduce_dispatch(int epi, int out_bf16, const float* ws, int splits, i
 
 template <typename T, bool AKC, bool BKC, typename TO, int EPI>
 int launch(const GemmArgs& a, int batch, hipStream_t s, int splits = 1) {
-  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  hipLaunchKernelGGL((gemm_kernel<T, AKC, BKC, TO, EPI>), dim3(tiles, batch, splits), dim3(NT), 0, s, a);
+  if (a.bt == 64) {
+    const int tiles = ((a.M + 63) / 64) * ((a.N + 63) / 64);
+    hipLaunchKernelGGL((gemm_kernel<T, AKC, BKC, TO, EPI, 64>), dim3(tiles, batch, splits), dim3(NT), 0, s, a);
+  } else {
+    const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+    hipLaunchKernelGGL((gemm_kernel<T, AKC, BKC, TO, EPI>), dim3(tiles, batch, splits), dim3(NT), 0, s, a);
+  }
   return (int)hipGetLastError();
 }
 
@@ -477,21 +488,23 @@ static int gemm_impl(int dtype, int out_dtype, int a_kcontig, int b_kcontig, int
     if (!fwd && !(a_kcontig && !b_kcontig)) return EEGF_ERR_ARG;
   }
   GemmArgs a{A, B, C, bias, aux, lda, ldb, ldc, ldaux, strideA, strideB, strideC, strideAux, strideBias, M, N, K, alpha, beta, epi_scale, 0,
-             lds_epi_enabled()};
+             lds_epi_enabled(), 128};
   if (dtype == EEGF_BF16 && batch == 1 && big_enabled()) {
     const int st = eegf_gemm_big(a_kcontig, b_kcontig, epi, out_dtype == EEGF_F32, M, N, K, A, lda, B, ldb, C, ldc,
                                  bias, aux, ldaux, alpha, beta, epi_scale, workspace, ws_bytes, a_colsum, stream);
     if (st != 1) return st;
   }
   if (a_colsum) return EEGF_ERR_ARG;       // fused column sums exist only on the 256x256 path
-  // split-K for under-filled grids: long contractions (weight gradients, K = tokens) and the
-  // batch-row decoder / head GEMMs (M = B); the fixed-order slab reduction applies the epilogue.
-  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  if (batch == 1 && workspace && tiles < 512 && (K >= 4096 || (tiles <= 64 && K >= 512))) {
+  // under-filled grids (the batch-row decoder / head GEMMs, M = B): 64 x 64 tiles quadruple the
+  // workgroups; then split-K for long contractions (weight gradients, K = tokens) and for the
+  // batch-row GEMMs; the fixed-order slab reduction applies the epilogue.
+  if (((M + BM - 1) / BM) * ((N + BN - 1) / BN) * batch < 192) a.bt = 64;
+  const int tiles = ((M + a.bt - 1) / a.bt) * ((N + a.bt - 1) / a.bt);
+  if (batch == 1 && workspace && tiles < 512 && (K >= 4096 || (tiles <= 256 && K >= 512))) {
     const int kt = dtype == EEGF_F32 ? 32 : 64;
     int splits = 1;
     const int min_slice = K >= 4096 ? 1024 : 256;
-    while (splits * tiles < 768 && K / (splits * 2) >= min_slice) splits *= 2;
+    while (splits * tiles < 512 && K / (splits * 2) >= min_slice) splits *= 2;
     while (splits > 1 && (long)splits * M * N * 4 > ws_bytes) splits /= 2;
     if (splits > 1) {
       int ks = (K + splits - 1) / splits;
