@@ -282,7 +282,50 @@ int ln_bwd_t(int nch, const LnBwdArgs& a, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+// ---- batched column sums: many small independent reductions in one launch ----
+// Descriptor (6 x int64): src, dst, ld, rows, width | dtype << 32, float_bits(beta) | first_block << 32.
+// Block b serves the descriptor whose block range holds b: 64 columns, 4 waves over contiguous row
+// quarters, combined in a fixed order (bitwise reproducible); dst[c] = sum + beta * dst[c].
+__global__ void __launch_bounds__(256) colsum_batch_kernel(const long long* __restrict__ desc, int n) {
+  __shared__ float red[4][64];
+  const int blk = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int d = 0;
+  for (int i = 1; i < n; ++i) {
+    if ((int)(desc[6 * i + 5] >> 32) <= blk) d = i;
+    else break;
+  }
+  const long long* D = desc + 6 * d;
+  const long ld = D[2], rows = D[3];
+  const int width = (int)(D[4] & 0xffffffffLL), dtype = (int)(D[4] >> 32);
+  const float beta = __int_as_float((int)(D[5] & 0xffffffffLL));
+  const int c = (blk - (int)(D[5] >> 32)) * 64 + lane;
+  const long r0 = rows * wave / 4, r1 = rows * (wave + 1) / 4;
+  float acc = 0.f;
+  if (c < width) {
+    if (dtype == EEGF_BF16) {
+      const bf16* p = (const bf16*)D[0] + c;
+      for (long r = r0; r < r1; ++r) acc += (float)p[r * ld];
+    } else {
+      const float* p = (const float*)D[0] + c;
+      for (long r = r0; r < r1; ++r) acc += p[r * ld];
+    }
+  }
+  red[wave][lane] = acc;
+  __syncthreads();
+  if (wave == 0 && c < width) {
+    float* dst = (float*)D[1];
+    const float v = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    dst[c] = beta != 0.f ? v + beta * dst[c] : v;
+  }
+}
+
 }  // namespace
+
+extern "C" int eegf_colsum_batch(int n, const long long* desc, int blocks, hipStream_t stream) {
+  if (n <= 0 || !desc || blocks <= 0) return EEGF_ERR_ARG;
+  hipLaunchKernelGGL(colsum_batch_kernel, dim3(blocks), dim3(256), 0, stream, desc, n);
+  return (int)hipGetLastError();
+}
 
 extern "C" int eegf_ln_fwd(int dtype, long rows, int width, const void* x, const void* r, const float* table,
                            int table_period, const float* table2, const float* gamma, const float* beta, float eps,

@@ -34,6 +34,7 @@ SIGNATURES: dict[str, list] = {
     "eegf_ln_bwd_partial_rows": [i64],
     "eegf_ln_bwd": [i32, i64, i32, vp, vp, vp, vp, vp, f32, i32, u64, u64, vp, vp, vp, vp, vp],
     "eegf_colsum": [i32, vp, i64, i64, i32, i32, vp, i64, vp, f32, vp],
+    "eegf_colsum_batch": [i32, vp, i32, vp],
     "eegf_attn_fwd": [i32, i32, i32, i32, vp, i64, vp, f32, f32, u64, u64, vp, i64, vp, vp, vp],
     "eegf_attn_bwd_workspace": [i32, i32],
     "eegf_attn_bwd": [i32, i32, i32, i32, vp, i64, vp, f32, f32, u64, u64, vp, vp, i64, vp, vp, vp, vp, vp],

@@ -22,6 +22,7 @@ derivatives, LN backward with deterministic partial sums and column reductions f
 from __future__ import annotations
 
 import math
+import struct
 from dataclasses import dataclass, field
 
 import torch
@@ -79,7 +80,13 @@ class Workspace:
         if b is None or b.numel() < numel or b.dtype != dtype:
             b = torch.empty(max(numel, 1), dtype=dtype, device=self.device)
             self.bufs[name] = b
+            self._ptrs = None
         return b[:numel]
+
+    def ptrs(self) -> set:
+        if getattr(self, "_ptrs", None) is None:
+            self._ptrs = {b.untyped_storage().data_ptr() for b in self.bufs.values()}
+        return self._ptrs
 
 
 class FusionEngine:
@@ -94,6 +101,11 @@ class FusionEngine:
         self.injected = None        # parity hook: dict(noise=..., gumbels=..., row_noise=...)
         self.needs_grad: set[str] | None = None
         self.probe: dict | None = None   # tag -> [(start_event, end_event)] (bench.py live timing)
+        # column sums deferred during a backward pass (bias / LayerNorm gradients): they feed only the
+        # optimizer, so one batched launch at the end replaces ~140 pairs of small launches
+        self.defer: list | None = None
+        self._defer_k = 0
+        self._parts: set[int] = set()
 
     # ------------------------------------------------------------------ parameter access
     def _refresh_shadow(self):
@@ -174,14 +186,12 @@ class FusionEngine:
         if bias_grad is not None:
             tiles = _lib.lib().eegf_gemm_colsum_tiles(_code(dy), _code(out), 1, M, K, N)
             if tiles > 0 and (ldd or N) == N:
-                part = self.ws.get("acs", tiles * N, torch.float32)
+                part = self._part("acs", tiles * N)
                 call("eegf_gemm_acs", _code(dy), _code(out), 1, 0, epi, M, K, N, P(dy), N, P(w), K, P(out), ldo or K,
                      None, P(aux), ldaux, 1.0, float(beta), float(scale), P(part), _stream())
-                ws = self.ws.get("colsum", 1 << 24, torch.float32)
-                call("eegf_colsum", F32, P(part), N, tiles, N, 1, P(ws), ws.numel(), P(bias_grad), 1.0, _stream())
+                self.colsum(part, N, tiles, N, bias_grad)
                 return out
-            ws = self.ws.get("colsum", 1 << 24, torch.float32)
-            call("eegf_colsum", _code(dy), P(dy), ldd or N, M, N, 1, P(ws), ws.numel(), P(bias_grad), 1.0, _stream())
+            self.colsum(dy, ldd or N, M, N, bias_grad)
         return self.gemm(dy, w, out, M, K, N, 1, 0, ldd or N, K, ldo or K, epi=epi, aux=aux, ldaux=ldaux,
                          scale=scale, beta=beta)
 
@@ -201,9 +211,46 @@ class FusionEngine:
             return
         o = out if out is not None else self.G(name)
         width = width or o.shape[-1]
+        self.colsum(dy, ld or width, rows, width, o, period)
+
+    def colsum(self, src, ld, rows, width, dst, period=1):
+        """dst += column sums of src (rows x width, row stride ld); deferred to the end of the backward
+        pass (eegf_colsum_batch) when small, else a two-stage eegf_colsum now."""
+        if self.defer is not None and period == 1 and rows <= 8192 and self._stable(src):
+            self.defer.append((src, int(ld), int(rows), int(width), _code(src), dst))
+            return
         ws = self.ws.get("colsum", 1 << 24, torch.float32)
-        call("eegf_colsum", _code(dy), P(dy), ld or width, rows, width, period, P(ws), ws.numel(), P(o), 1.0,
-             _stream())
+        call("eegf_colsum", _code(src), P(src), ld, rows, width, period, P(ws), ws.numel(), P(dst), 1.0, _stream())
+
+    def _part(self, name, numel):
+        """fp32 partial-sum buffer; one per call site while column sums are deferred"""
+        if self.defer is not None:
+            self._defer_k += 1
+            name = f"{name}{self._defer_k}"
+            b = self.ws.get(name, numel, torch.float32)
+            self._parts.add(b.untyped_storage().data_ptr())
+            return b
+        return self.ws.get(name, numel, torch.float32)
+
+    def _stable(self, src):
+        """src is not overwritten before the flush: a per-site partial buffer or a tensor of its own
+        (shared workspace buffers are reused by later layers)"""
+        ptr = src.untyped_storage().data_ptr()
+        return ptr in self._parts or ptr not in self.ws.ptrs()
+
+    def _flush_colsums(self):
+        d, self.defer = self.defer, None
+        if not d:
+            return
+        beta = struct.unpack("<i", struct.pack("<f", 1.0))[0]
+        rows, blk = [], 0
+        for src, ld, r, w, code, dst in d:
+            rows.append([P(src), P(dst), ld, r, w | (code << 32), beta | (blk << 32)])
+            blk += (w + 63) // 64
+        host = torch.tensor(rows, dtype=torch.int64).pin_memory()
+        dev = host.to(self.a.device, non_blocking=True)
+        call("eegf_colsum_batch", len(rows), P(dev), blk, _stream())
+        self._colsum_keep = (d, host, dev)      # sources and descriptors live until the next flush
 
     def dropout(self, x, group, p, rng):
         if p > 0:
@@ -217,7 +264,7 @@ class FusionEngine:
 
     def ln_bwd(self, dy, s, mean, rstd, pre, rows, dx, dr, p=0.0, mode=0, rng=0):
         nb = (rows + 63) // 64
-        part = self.ws.get("ln_part", 2 * nb * HID, torch.float32)
+        part = self._part("ln_part", 2 * nb * HID)
         call("eegf_ln_bwd", _code(dy), rows, HID, P(dy), P(s), P(mean), P(rstd), P(self.F(pre + ".weight")), float(p),
              int(mode if p > 0 else 0), self.cfg.seed, rng, P(dx), P(dr), P(part), P(part[nb * HID:]), _stream())
         self.bgrad(part[: nb * HID], pre + ".weight", nb, HID)
@@ -404,6 +451,13 @@ class FusionEngine:
 
     # =================================================================== backward
     def backward(self, sv: Saved, dlogits: torch.Tensor, head_only: bool = False):
+        self.defer, self._defer_k = [], 0
+        try:
+            self._backward(sv, dlogits, head_only)
+        finally:
+            self._flush_colsums()
+
+    def _backward(self, sv: Saved, dlogits: torch.Tensor, head_only: bool = False):
         """Accumulate parameter gradients into the arena grad buffer (beta = 1 everywhere; the
         caller zeroes the ranges it overwrites).  head_only: stop after the privacy stage
         (DP gradient only — the PriGumbel DP pass)."""

@@ -101,6 +101,12 @@ int eegf_ln_bwd(int dtype, long rows, int width, const void* dy, const void* s, 
  * partial reduction.  ws: scratch of ws_elems floats. */
 int eegf_colsum(int dtype, const void* in, long ld, long rows, int width, int period, float* ws,
                 long ws_elems, float* out, float beta, hipStream_t stream);
+/* Batched column sums (bias / LayerNorm gradients of a whole backward pass in one launch): desc is a
+ * device array of n descriptors of 6 int64 each: src, dst (fp32), ld, rows, width | dtype << 32,
+ * float_bits(beta) | first_block << 32, where descriptor i owns blocks [first_block_i,
+ * first_block_{i+1}) (ceil(width / 64) blocks each, first_block ascending); blocks = total.
+ * dst[c] = sum_r src[r*ld + c] + beta * dst[c], fixed order (deterministic). */
+int eegf_colsum_batch(int n, const long long* desc, int blocks, hipStream_t stream);
 
 /* Multi-head self-attention (12 x 64) over the fused QKV projection [B, L, ld_qkv>=2304]
  * (BertSelfAttention, modeling_bert.py:139-199).  key_bias [B, L]: 0 or -1e30 (nullable).
