@@ -89,6 +89,59 @@ __global__ void __launch_bounds__(256) xrow_dot_kernel(const T* __restrict__ mem
   }
 }
 
+// Same product on the MFMA for a bf16 memory: grid (ceil(S/256), B), 4 waves x 16-row blocks.  The fp32
+// vector is split as v = v_hi + v_lo (two bf16 operands, both multiplied against the exact bf16 memory
+// and accumulated in fp32), so the scores keep ~2^-16 relative accuracy in v instead of bf16's 2^-8.
+// A = memory rows straight from global (16 B per lane, 64 B row segments), B = v_hi / v_lo from LDS
+// (heads padded 12 -> 16 with zeros).
+constexpr int XR = 4;       // 64-row blocks per xrow_dot_mfma workgroup
+template <typename TV>
+__global__ void __launch_bounds__(256) xrow_dot_mfma_kernel(const bf16* __restrict__ mem, const TV* __restrict__ vec,
+                                                            const float* __restrict__ kbias, int S,
+                                                            float* __restrict__ out) {
+  constexpr int LDV = E + 8;
+  __shared__ __attribute__((aligned(16))) bf16 vt[2][16 * LDV];
+  const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, li = lane & 15;
+  for (int i = tid; i < 16 * E; i += 256) {
+    const int h = i / E, c = i % E;
+    const float x = h < NH ? to_f32(vec[((long)b * NH + h) * E + c]) : 0.f;
+    const bf16 hi = (bf16)x;
+    vt[0][h * LDV + c] = hi;
+    vt[1][h * LDV + c] = (bf16)(x - (float)hi);
+  }
+  __syncthreads();
+  const bf16* vh = vt[0] + li * LDV + 8 * g;
+  const bf16* vl = vt[1] + li * LDV + 8 * g;
+  // the workgroup covers XR row blocks of 64 (amortises the v staging): wave w takes 16-row blocks
+  // w, w + 4, ...
+  for (int j0 = blockIdx.x * 64 * XR + wave * 16; j0 < min(S, (int)(blockIdx.x + 1) * 64 * XR); j0 += 64) {
+    const bf16* row = mem + ((long)b * S + min(j0 + li, S - 1)) * E + 8 * g;
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+    for (int kc = 0; kc < E / 32; ++kc) {
+      const bf16x8 a = *(const bf16x8*)(row + 32 * kc);
+      acc = mma16(a, *(const bf16x8*)(vh + 32 * kc), acc);
+      acc = mma16(a, *(const bf16x8*)(vl + 32 * kc), acc);
+    }
+    // acc[r] = out[row j0 + 4g + r][head li]
+    if (li < NH) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = j0 + 4 * g + r;
+        if (j < S) out[((long)b * NH + li) * S + j] = acc[r] + (kbias ? kbias[(long)b * S + j] : 0.f);
+      }
+    }
+  }
+}
+template <typename T, typename TV>
+void launch_xrow_dot(const T* mem, const TV* vec, const float* kbias, int B, int S, float* out, hipStream_t st) {
+  if constexpr (sizeof(T) == 2)
+    hipLaunchKernelGGL((xrow_dot_mfma_kernel<TV>), dim3((S + 64 * XR - 1) / (64 * XR), B), dim3(256), 0, st, mem, vec,
+                       kbias, S, out);
+  else
+    hipLaunchKernelGGL((xrow_dot_kernel<T, TV>), dim3((S + 63) / 64, B), dim3(256), 0, st, mem, vec, kbias, S, out);
+}
+
 // Softmax (+dropout) of the 12 raw score rows of batch row b into LDS pt[S][12] (p~);
 // workgroup slab 0 also stores the undropped p (for the backward) and s_h = sum_j p~.
 DEV void softmax_rows(const float* __restrict__ raw, int S, int b, float p_drop, uint64_t seed, uint64_t offset,
@@ -294,8 +347,7 @@ __global__ void __launch_bounds__(256) head_bias_db_kernel(int B, int W, const f
 template <typename T, typename TQ>
 int xfwd(int B, int S, const void* mem, const void* qp, const float* kb, float p, uint64_t seed, uint64_t off,
          float* ws, float* probs, float* psum, void* ctx, hipStream_t st) {
-  hipLaunchKernelGGL((xrow_dot_kernel<T, TQ>), dim3((S + 63) / 64, B), dim3(256), 0, st, (const T*)mem, (const TQ*)qp,
-                     kb, S, ws);
+  launch_xrow_dot<T, TQ>((const T*)mem, (const TQ*)qp, kb, B, S, ws, st);
   const size_t lds = sizeof(float) * ((size_t)S * NH + 4 * NH * SLAB);
   hipFuncSetAttribute((const void*)xctx_kernel<T, TQ>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL((xctx_kernel<T, TQ>), dim3(E / SLAB, B), dim3(512), lds, st, (const T*)mem, ws, S, p, seed, off,
@@ -305,8 +357,7 @@ int xfwd(int B, int S, const void* mem, const void* qp, const float* kb, float p
 template <typename T, typename TQ>
 int xbwd(int B, int S, const void* mem, const void* qp, const float* probs, const float* dpsum, const void* dctx,
          float p, uint64_t seed, uint64_t off, float* ws, void* dmem, float beta, void* dqp, hipStream_t st) {
-  hipLaunchKernelGGL((xrow_dot_kernel<T, TQ>), dim3((S + 63) / 64, B), dim3(256), 0, st, (const T*)mem,
-                     (const TQ*)dctx, (const float*)nullptr, S, ws);
+  launch_xrow_dot<T, TQ>((const T*)mem, (const TQ*)dctx, (const float*)nullptr, B, S, ws, st);
   const size_t lds = sizeof(float) * ((size_t)2 * S * NH + 4 * NH * SLAB);
   hipFuncSetAttribute((const void*)xbwd_cols_kernel<T, TQ>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL((xbwd_cols_kernel<T, TQ>), dim3(E / SLAB, B), dim3(512), lds, st, (const T*)mem, (const TQ*)qp,
