@@ -28,6 +28,33 @@ template <> struct Frag8<float> { typedef f32x8 type; };
 
 #define DEV __device__ __forceinline__
 
+// LDS-DMA (global_load_lds_dwordx4: 16 B per lane, written lane-linearly from the wave-uniform
+// LDS address lds_base) issued as inline asm.  With the builtin, hipcc's waitcnt pass puts an
+// s_waitcnt vmcnt(0) in front of every ds_read_b64_tr_b16 that follows an LDS-DMA (it cannot tell
+// which LDS the transpose read touches), which drains the staging pipeline of every kernel that
+// reads a k-major operand.  Hidden in asm, the DMA is invisible to the pass: its completion is
+// tracked by the kernels' own counted s_waitcnt vmcnt + barriers (the pass's waits for ordinary
+// loads only get more conservative, never wrong: vmcnt retires in order).  M0 is set in the same
+// asm statement; nothing else in these kernels uses M0.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+DEV void glds16_asm(const void* g, const void* lds_base) {
+  typedef __attribute__((address_space(3))) void lv;
+  const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lv*)lds_base);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(l) : "memory", "m0");
+}
+// saddr form: wave-uniform 64-bit base + per-lane 32-bit byte offset (no 64-bit address VGPRs)
+DEV void glds16_asm_s(const void* base, uint32_t voff, const void* lds_base) {
+  typedef __attribute__((address_space(3))) void lv;
+  const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lv*)lds_base);
+  const uint64_t b = (uint64_t)(uintptr_t)base;
+  const uint64_t bu = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+                      (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(bu), "s"(l)
+               : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
 DEV float to_f32(float x) { return x; }
 DEV float to_f32(bf16 x) { return (float)x; }
 template <typename T> DEV T from_f32(float x);

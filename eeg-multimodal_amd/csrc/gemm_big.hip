@@ -41,9 +41,7 @@ int g_big_prio = [] { const char* e = getenv("EEGF_GEMM_PRIO"); return e ? atoi(
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) const void glb_void;
 
-DEV void glds16(const bf16* g, bf16* lds_base) {
-  __builtin_amdgcn_global_load_lds((glb_void*)g, (lds_void*)lds_base, 16, 0, 0);
-}
+DEV void glds16(const bf16* g, bf16* lds_base) { glds16_asm(g, lds_base); }   // common.h: why asm
 
 DEV int swz_row(int r) { return (r >> 1) & 7; }
 DEV int swz_k(int k) { return 2 * ((k & 3) | (((k >> 3) & 1) << 2)); }
@@ -596,6 +594,274 @@ __global__ void __launch_bounds__(NT, 1) gemm8_kernel(BigArgs g) {
   big_epilogue<EPI, TO>(g, acc, lds, m0, n0, tid, lane, wm, wn);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Persistent form of the lockstep 8-phase schedule (MODE 4), bf16 output, K-contiguous A.
+// grid = min(tiles, CUs); workgroup b runs the tiles v = b, b + grid, ... (each mapped through
+// xcd_remap exactly as the one-shot grid would place block v), and the K-tile STREAM runs on across
+// tiles: stream index G = it * nk + kt, buffer G & 1, and the stages of a tile's last phases already
+// fetch the next tile's K-tiles 0 / 1.  The epilogue stores straight from the accumulators (8-byte
+// row segments, no LDS: the ring holds the next tile's operands), so it overlaps those loads instead
+// of following a prologue bubble.  CS: the fused A column sums of gemm8_kernel, per tile.
+// Measured (tools/gemm_bench.py --ab, profiles/r1s2_gemm_persist_ab.log): 5-10 % SLOWER than the one-
+// shot gemm8 MODE 4 on every bench shape except the aux-input epilogues (+10 %), so opt-in only.
+int g_gemm8p = [] { const char* e = getenv("EEGF_GEMM8P"); return e ? atoi(e) : 0; }();
+
+int big_cus() {
+  static const int cus = [] {
+    int dev = 0, n = 256;
+    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    return n > 0 ? n : 256;
+  }();
+  return cus;
+}
+
+DEV bf16x4 pack4(const float (&v)[4]) {
+  bf16x4 x;
+  x[0] = (bf16)v[0]; x[1] = (bf16)v[1]; x[2] = (bf16)v[2]; x[3] = (bf16)v[3];
+  return x;
+}
+
+// acc[i][j][r] -> row wm*128 + 16i + (lane&15), column wn*64 + 16j + 4(lane>>4) + r of the tile.
+// The compiler's waitcnt pass treats vmcnt as out of order once stores and loads are both pending
+// (gfx9 counts stores in vmcnt), so any wait it computes after an epilogue is vmcnt(0), which would
+// drain the next tile's operand stages.  Hence: the tile's bias row arrives in LDS by LDS-DMA at the
+// START of the tile (retired by the tile's own counted waits, published by its phase barriers), the
+// aux / C inputs are all loaded before the first store, and interior tiles (EDGE = false) have no
+// data-dependent branches around their loads and stores.
+template <int EPI>
+constexpr bool epi_has_bias() {
+  return EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_TANH || EPI == EPI_BIAS_GELU_D;
+}
+
+template <int EPI, bool EDGE>
+DEV void direct_epilogue_body(const BigArgs& g, f32x4 (&acc)[8][4], const float* bias_lds, int m0, int n0, int lane,
+                              int wm, int wn) {
+  constexpr bool HAS_BIAS = epi_has_bias<EPI>();
+  constexpr bool AUX_IN = EPI == EPI_DGELU || EPI == EPI_DRELU || EPI == EPI_DTANH || EPI == EPI_MUL_AUX;
+  bf16* Cb = (bf16*)g.C;
+  const int rl = m0 + wm * 128 + (lane & 15);
+  const int cl = n0 + wn * 64 + 4 * (lane >> 4);
+  const bool load_in = AUX_IN || (EPI == EPI_NONE && g.beta != 0.f);
+  const bf16* src = AUX_IN ? g.aux : Cb;
+  const long lds_ = AUX_IN ? g.ldaux : g.ldc;
+  bf16x4 av[8][4];
+  if (load_in) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        int m = rl + 16 * i, n = cl + 16 * j;
+        if (EDGE) { m = min(m, g.M - 1); n = min(n, g.N - 4); }
+        av[i][j] = *(const bf16x4*)(src + (long)m * lds_ + n);
+      }
+  }
+  f32x4 bias[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    bias[j] = HAS_BIAS ? *(const f32x4*)(bias_lds + wn * 64 + 16 * j + 4 * (lane >> 4)) : f32x4{0.f, 0.f, 0.f, 0.f};
+  {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = rl + 16 * i;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = cl + 16 * j;
+        float o[4], o2[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = g.alpha * acc[i][j][r];
+          const float a = load_in ? (float)av[i][j][r] : 0.f;
+          if (HAS_BIAS) v += bias[j][r];
+          if (EPI == EPI_BIAS_RELU) v = fmaxf(v, 0.f);
+          else if (EPI == EPI_BIAS_TANH) v = tanhf(v);
+          else if (EPI == EPI_DGELU) v *= gelu_grad(a);
+          else if (EPI == EPI_DRELU) v = a > 0.f ? v * g.epi_scale : 0.f;
+          else if (EPI == EPI_DTANH) v *= (1.f - a * a);
+          else if (EPI == EPI_MUL_AUX) v *= a;
+          else if (EPI == EPI_NONE && g.beta != 0.f) v += g.beta * a;
+          o[r] = v;
+        }
+        if (EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_D) {
+#pragma unroll
+          for (int h2 = 0; h2 < 2; ++h2) {
+            f32x2 gl, gd;
+            gelu2(f32x2{o[2 * h2], o[2 * h2 + 1]}, gl, EPI == EPI_BIAS_GELU_D ? &gd : nullptr);
+            o2[2 * h2] = EPI == EPI_BIAS_GELU_D ? gd.x : o[2 * h2];      // aux: gelu' or the pre-activation
+            o2[2 * h2 + 1] = EPI == EPI_BIAS_GELU_D ? gd.y : o[2 * h2 + 1];
+            o[2 * h2] = gl.x;
+            o[2 * h2 + 1] = gl.y;
+          }
+        }
+        if (!EDGE || (m < g.M && n < g.N)) {
+          *(bf16x4*)(Cb + (long)m * g.ldc + n) = pack4(o);
+          if (EPI == EPI_BIAS_GELU_D || (EPI == EPI_BIAS_GELU && g.aux))
+            *(bf16x4*)(g.aux + (long)m * g.ldaux + n) = pack4(o2);
+        }
+      }
+    }
+  }
+  // edge tiles: the math may sink into the exec-masked store blocks, leaving the aux loads of
+  // skipped blocks pending in the waitcnt pass's model (it then drains at the next K-loop head);
+  // retire them here, once per edge tile (the builtin, unlike an asm wait, is seen by the pass)
+  if (EDGE && load_in) __builtin_amdgcn_s_waitcnt(0x0F70);     // vmcnt(0)
+}
+
+template <int EPI>
+DEV void direct_epilogue(const BigArgs& g, f32x4 (&acc)[8][4], const float* bias_lds, int m0, int n0, int lane, int wm,
+                         int wn) {
+  if (m0 + TM <= g.M && n0 + TN <= g.N) direct_epilogue_body<EPI, false>(g, acc, bias_lds, m0, n0, lane, wm, wn);
+  else direct_epilogue_body<EPI, true>(g, acc, bias_lds, m0, n0, lane, wm, wn);
+}
+
+template <bool BKC, int EPI, bool CS = false>
+__global__ void __launch_bounds__(NT, 1) gemm8p_kernel(BigArgs g) {
+  // operand ring 128 KB | bias rows [2][256] fp32 2 KB (+ CS: red[2][8][64] 4 KB | ks[K] fp32 12 KB)
+  __shared__ __attribute__((aligned(16))) bf16 lds[8 * HALF + 1024 + (CS ? 1024 * 2 + CS_KMAX * 2 : 0)];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int tiles_n = (g.N + TN - 1) / TN, tiles = ((g.M + TM - 1) / TM) * tiles_n;
+  const int my = (tiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int nk = g.K / BK;                 // >= 2
+  const int total = my * nk;               // K-tile stream of this workgroup
+
+  auto tile_of = [&](int it, int& tm, int& tn) {
+    const int t = xcd_remap((int)blockIdx.x + it * (int)gridDim.x, tiles);
+    tm = t / tiles_n;
+    tn = t - tm * tiles_n;
+  };
+  int tmc, tnc, tmn, tnn;
+  tile_of(0, tmc, tnc);
+  if (my > 1) tile_of(1, tmn, tnn); else { tmn = tmc; tnn = tnc; }
+  int kend = nk;                           // stream end of the current tile
+
+  // stage half `which` (0 A_h0, 1 A_h1, 2 B_h0, 3 B_h1) of stream K-tile s (current or next tile)
+  auto stage_s = [&](int s, int which) {
+    const bool nx = s >= kend;
+    const int k0 = (s - (nx ? kend : kend - nk)) * BK;
+    bf16* d = lds + (s & 1) * 4 * HALF + which * HALF;
+    if (which < 2) stage_half(d, g.A, g.lda, (nx ? tmn : tmc) * TM, 6, 128, 64 * which, g.M, k0, wave, lane);
+    else if (BKC) stage_half(d, g.B, g.ldb, (nx ? tnn : tnc) * TN, 5, 64, 32 * (which - 2), g.N, k0, wave, lane);
+    else stage_half_km(d, g.B, g.ldb, (nx ? tnn : tnc) * TN, 5, 64, 32 * (which - 2), g.N, k0, wave, lane);
+  };
+  auto stage_tile_of = [&](int phi) { const int tt = phi >> 2, p = phi & 3; return tt + (p <= 1 ? 1 : 2); };
+  auto stage_phase = [&](int phi) {
+    const int tt = stage_tile_of(phi), p = phi & 3;
+    if (tt >= total) return;
+    stage_s(tt, p == 0 ? 3 : p == 1 ? 1 : p == 2 ? 0 : 2);
+  };
+  auto younger2 = [&](int phi) {
+    return (stage_tile_of(phi - 1) < total ? 1 : 0) + (stage_tile_of(phi) < total ? 1 : 0);
+  };
+  for (int phi = -6; phi < 0; ++phi) stage_phase(phi);
+  vm_wait(younger2(-1));
+  raw_barrier();
+
+  float* bias_rows = (float*)(lds + 8 * HALF);
+  float* red = bias_rows + 512;
+  float* ks = red + 2 * 8 * 64;
+  const int cs_h = wave >> 2, cs_lr0 = 32 * (wave & 3);
+  auto rdB = [&](const bf16* Bh, int jj, int kc) {
+    return BKC ? rd_row(Bh, wn * 32 + jj * 16 + (lane & 15), 4 * kc + (lane >> 4))
+               : rd_colh(Bh, 32 * kc + 8 * (lane >> 4), wn * 32 + jj * 16, lane);
+  };
+  bf16x8 ar[4][2], br0[2][2], br1[2][2];
+  f32x4 acc[8][4];
+  for (int it = 0; it < my; ++it) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // the tile's bias row -> bias_rows[it & 1] by one LDS-DMA of wave 0: older than every stage of
+    // this tile, so the first phase-3 vm_wait retires it and that phase's barrier publishes it
+    if (epi_has_bias<EPI>() && wave == 0)
+      glds16((const bf16*)(g.bias + min(tnc * TN + 4 * lane, g.N - 4)), (bf16*)(bias_rows + (it & 1) * 256));
+    const bool do_cs = CS && tnc == 0;
+    bf16x8 ones;
+    if (CS) {
+      const int cs_rows = g.M - tmc * TM - ((cs_lr0 >> 6) * 128 + 64 * cs_h + (cs_lr0 & 63) + 8 * (lane >> 4));
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ones[e] = (bf16)(e < cs_rows ? 1.0f : 0.0f);
+    }
+    for (int kt = 0; kt < nk; ++kt) {
+      const int G = it * nk + kt;
+      const bf16* Ab = lds + (G & 1) * 4 * HALF;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int phi = 4 * G + p;
+        if (CS && do_cs) {
+          if (p == 2 * cs_h) {
+            const bf16* Ah = Ab + cs_h * HALF;
+#pragma unroll
+            for (int f = 0; f < 4; ++f) {
+              const f32x4 c = mma16(ones, rd_col_rm(Ah, cs_lr0 + 8 * (lane >> 4), 16 * f, lane), f32x4{0.f, 0.f, 0.f, 0.f});
+              if (lane < 16) red[(kt & 1) * 512 + wave * 64 + 16 * f + lane] = c[0];
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          }
+          if (p == 1 && kt > 0 && tid < 64) {
+            const float* rp = red + ((kt - 1) & 1) * 512;
+            float v = 0.f;
+#pragma unroll
+            for (int w = 0; w < 8; ++w) v += rp[w * 64 + tid];
+            ks[(kt - 1) * BK + tid] = v;
+          }
+        }
+        if (p == 0) {
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+            for (int kc = 0; kc < 2; ++kc) br0[jj][kc] = rdB(Ab + 2 * HALF, jj, kc);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if (p == 1) {
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+            for (int kc = 0; kc < 2; ++kc) br1[jj][kc] = rdB(Ab + 3 * HALF, jj, kc);
+        }
+        if (p == 0 || p == 2) {
+          const bf16* Ah = Ab + (p == 0 ? 0 : HALF);
+#pragma unroll
+          for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+            for (int kc = 0; kc < 2; ++kc) ar[ii][kc] = rd_row(Ah, wm * 64 + ii * 16 + (lane & 15), 4 * kc + (lane >> 4));
+        }
+        stage_phase(phi);
+        if (p == 3) vm_wait(younger2(phi));
+        raw_barrier();
+        const int mh = (p == 0 || p == 1) ? 0 : 1, nh = (p == 1 || p == 2) ? 1 : 0;
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+            for (int kc = 0; kc < 2; ++kc) {
+              const bf16x8 bv = nh == 0 ? br0[jj][kc] : br1[jj][kc];
+              acc[mh * 4 + ii][nh * 2 + jj] = mma16(bv, ar[ii][kc], acc[mh * 4 + ii][nh * 2 + jj]);
+            }
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+    if (CS && do_cs) {
+      if (tid < 64) {
+        const float* rp = red + ((nk - 1) & 1) * 512;
+        float v = 0.f;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) v += rp[w * 64 + tid];
+        ks[(nk - 1) * BK + tid] = v;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      for (int k = tid; k < g.K; k += NT) g.colsum_part[(long)tmc * g.K + k] = ks[k];
+    }
+    direct_epilogue<EPI>(g, acc, bias_rows + (it & 1) * 256, tmc * TM, tnc * TN, lane, wm, wn);
+    tmc = tmn;
+    tnc = tnn;
+    kend += nk;
+    if (it + 2 < my) tile_of(it + 2, tmn, tnn);
+  }
+}
+
 template <bool AKC, bool BKC, int EPI, typename TO>
 int launch_big(const BigArgs& a, int splits, hipStream_t s) {
   const int tiles = ((a.M + TM - 1) / TM) * ((a.N + TN - 1) / TN);
@@ -604,6 +870,22 @@ int launch_big(const BigArgs& a, int splits, hipStream_t s) {
     // schedule with one vmcnt per K-tile for the input-gradient GEMMs (+10-25 %) and the forward
     // GEMMs except the smallest (N, K <= 768); the 2-phase kernel for the weight gradients
     const bool use8 = sizeof(TO) == 2 && AKC && (!BKC || a.N > 768 || a.K > 768);
+    if constexpr (AKC && sizeof(TO) == 2) {
+      const bool usep = g_gemm8p > 0;
+      if (usep && splits == 1 && a.K >= 2 * BK) {
+        const dim3 grid(tiles < big_cus() ? tiles : big_cus());
+        if constexpr (!BKC) {
+          if (a.colsum_part) {
+            hipLaunchKernelGGL((gemm8p_kernel<BKC, EPI, true>), grid, dim3(NT), 0, s, a);
+            return (int)hipGetLastError();
+          }
+        }
+        if (!a.colsum_part) {
+          hipLaunchKernelGGL((gemm8p_kernel<BKC, EPI>), grid, dim3(NT), 0, s, a);
+          return (int)hipGetLastError();
+        }
+      }
+    }
     if (use8) {
       if constexpr (AKC && !BKC && sizeof(TO) == 2) {
         if (a.colsum_part) {
@@ -722,10 +1004,12 @@ extern int g_attn256_mode;     // attention.hip
 // Tuning / A-B hook (returns the old value): key 1 = 8-phase GEMM schedule (-1 auto (default), 0 off,
 // 1 staggered, 2 lockstep, 3 staggered without setprio, 4 lockstep with one vmcnt per K-tile); key 2 = L = 256
 // attention kernels (bit 0 forward, bit 1 backward); key 3 = static s_setprio 1 for waves 4-7 of the
-// 2-phase 256x256 kernel.
+// 2-phase 256x256 kernel; key 4 = persistent 8-phase kernel (0 off (default), 1 every eligible
+// bf16-output GEMM).
 extern "C" int eegf_tune(int key, int value) {
   if (key == 1) { const int o = g_gemm8; g_gemm8 = value; return o; }
   if (key == 2) { const int o = g_attn256_mode; g_attn256_mode = value; return o; }
   if (key == 3) { const int o = g_big_prio; g_big_prio = value; return o; }
+  if (key == 4) { const int o = g_gemm8p; g_gemm8p = value; return o; }
   return EEGF_ERR_ARG;
 }

@@ -80,13 +80,16 @@ def run(name, M, N, Kd, layout, epi, iters=20):
         r = {v: [] for v in VARIANTS}
         for _ in range(5):
             for v in VARIANTS:
-                lib.eegf_tune(1, v if v < 5 else 0)      # 5: 2-phase with static priority; -1: default routing
+                # 5: 2-phase with static priority; 6: persistent 8-phase; -1: default routing
+                lib.eegf_tune(1, v if v < 5 else (-1 if v == 6 else 0))
                 lib.eegf_tune(3, 1 if v == 5 else 0)
+                lib.eegf_tune(4, 1 if v == 6 else 0)
                 f()
                 torch.cuda.synchronize()
                 r[v].append(timed(f, iters))
         lib.eegf_tune(1, -1)
         lib.eegf_tune(3, 0)
+        lib.eegf_tune(4, 0)
         med = {v: sorted(x)[len(x) // 2] for v, x in r.items()}
         tt = timed(tf, iters)
         print(f"{name:16s} {M}x{N}x{Kd} " + " | ".join(f"v{v} {tf_(med[v]):6.1f}" for v in med)
