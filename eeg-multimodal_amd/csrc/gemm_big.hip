@@ -17,6 +17,8 @@
 //     (in-wave shuffles, then 8 waves through 4 KB of LDS left free by the operand buffers) and
 //     write one fp32 partial row per 256-row tile: colsum_part[tile_m][K].
 // Edges: rows/cols beyond M/N are clamped to valid memory and never stored; K % 64 == 0.
+#include <type_traits>
+
 #include "common.h"
 #include "eegfusion_internal.h"
 
@@ -106,11 +108,11 @@ DEV bf16x8 rd_col_rm(const bf16* t, int r0, int c0, int lane) {
   return r;
 }
 
-template <bool LOAD>
+template <bool LOAD, int NTH = NT>
 DEV void tile_io(bf16* lds, bf16* gp, long ld, int m0, int n0, int M, int N, int tid) {
 #pragma unroll 4
-  for (int k = 0; k < (TM * TN / 8) / NT; ++k) {
-    const int c = tid + NT * k;
+  for (int k = 0; k < (TM * TN / 8) / NTH; ++k) {
+    const int c = tid + NTH * k;
     const int r = c >> 5, cc = (c & 31) * 8;
     const int m = m0 + r, n = n0 + cc;
     if (m >= M || n >= N) continue;
@@ -128,10 +130,12 @@ DEV void ld4(const bf16* p, float (&v)[4]) { const bf16x4 x = *(const bf16x4*)p;
 DEV void st4(bf16* p, const float (&v)[4]) { bf16x4 x; x[0] = (bf16)v[0]; x[1] = (bf16)v[1]; x[2] = (bf16)v[2]; x[3] = (bf16)v[3]; *(bf16x4*)p = x; }
 
 // Shared epilogue of the 256x256 kernels: acc[i][j] holds rows wm*128 + 16i + (lane&15), columns
-// wn*64 + 16j + 4*(lane>>4) + 0..3 of the block tile (m0, n0).
-template <int EPI, typename TO>
-DEV void big_epilogue(const BigArgs& g, f32x4 (&acc)[8][4], bf16* lds, int m0, int n0, int tid, int lane, int wm,
+// wn*16NJ + 16j + 4*(lane>>4) + 0..3 of the block tile (m0, n0) (NJ = 4: 8 waves of 128x64, NJ = 8:
+// 4 waves of 128x128); NTH threads.
+template <int EPI, typename TO, int NJ = 4, int NTH = NT>
+DEV void big_epilogue(const BigArgs& g, f32x4 (&acc)[8][NJ], bf16* lds, int m0, int n0, int tid, int lane, int wm,
                       int wn) {
+  constexpr int WN = 16 * NJ;
   constexpr bool HAS_BIAS = EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_TANH ||
                             EPI == EPI_BIAS_GELU_D;
   constexpr bool AUX_IN = EPI == EPI_DGELU || EPI == EPI_DRELU || EPI == EPI_DTANH || EPI == EPI_MUL_AUX;
@@ -145,8 +149,8 @@ DEV void big_epilogue(const BigArgs& g, f32x4 (&acc)[8][4], bf16* lds, int m0, i
       const int m = m0 + wm * 128 + i * 16 + (lane & 15);
       if (m >= g.M) continue;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+      for (int j = 0; j < NJ; ++j) {
+        const int n = n0 + wn * WN + j * 16 + 4 * (lane >> 4);
         float* cp = Cf + (long)m * ldc + n;
         f32x4 v = acc[i][j] * g.alpha;
         if (n + 3 < g.N && ((uintptr_t)cp & 15) == 0) {
@@ -164,12 +168,12 @@ DEV void big_epilogue(const BigArgs& g, f32x4 (&acc)[8][4], bf16* lds, int m0, i
   bf16* ct = lds;
   bf16* Cb = (bf16*)g.C;
   if (AUX_IN || g.beta != 0.f) {
-    tile_io<true>(ct, AUX_IN ? g.aux : Cb, AUX_IN ? g.ldaux : g.ldc, m0, n0, g.M, g.N, tid);
+    tile_io<true, NTH>(ct, AUX_IN ? g.aux : Cb, AUX_IN ? g.ldaux : g.ldc, m0, n0, g.M, g.N, tid);
     __syncthreads();
   }
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int nl = wn * 64 + j * 16 + 4 * (lane >> 4);
+  for (int j = 0; j < NJ; ++j) {
+    const int nl = wn * WN + j * 16 + 4 * (lane >> 4);
     const int n = n0 + nl;
     float bias[4] = {0.f, 0.f, 0.f, 0.f};
     if (HAS_BIAS)
@@ -216,9 +220,9 @@ DEV void big_epilogue(const BigArgs& g, f32x4 (&acc)[8][4], bf16* lds, int m0, i
     // store the pre-activation tile, then compute GELU while those stores drain (raw barriers: a
     // __syncthreads() here would wait for the stores); LDS reads of the tile are complete per
     // thread once its stores have issued
-    tile_io<false>(ct, g.aux, g.ldaux, m0, n0, g.M, g.N, tid);
+    tile_io<false, NTH>(ct, g.aux, g.ldaux, m0, n0, g.M, g.N, tid);
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int i = 0; i < 8; ++i)
         if (EPI == EPI_BIAS_GELU) {
@@ -232,15 +236,15 @@ DEV void big_epilogue(const BigArgs& g, f32x4 (&acc)[8][4], bf16* lds, int m0, i
         }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-        st4(ct + (wm * 128 + i * 16 + (lane & 15)) * LDC + wn * 64 + j * 16 + 4 * (lane >> 4), o);
+        st4(ct + (wm * 128 + i * 16 + (lane & 15)) * LDC + wn * WN + j * 16 + 4 * (lane >> 4), o);
       }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
-  tile_io<false>(ct, Cb, g.ldc, m0, n0, g.M, g.N, tid);
+  tile_io<false, NTH>(ct, Cb, g.ldc, m0, n0, g.M, g.N, tid);
   }
 }
 
@@ -426,14 +430,16 @@ DEV void raw_barrier() {
 // with ds_read_b64_tr_b16); fp32 output = split-K slabs over blockIdx.y as gemm_big_kernel.
 // MODE 1: staggered groups, per-phase vmcnt; 2: lockstep, per-phase vmcnt; 3: as 1 without setprio;
 // 4: lockstep with one vmcnt per K-tile (phase 3: every half staged up to phase 1 of this tile retired,
-//    the two younger ones stay in flight across the barrier).
+//    the two younger ones stay in flight across the barrier); 5: as 4 plus a barrier after each
+//    phase's MFMAs (the guide template's two barriers per phase).
 // CS: fused column sums of A (as gemm_big_kernel's): in workgroups of tile column 0, waves 0-3 contract
 // 32 local rows of A_h0 at phase 0 and waves 4-7 32 rows of A_h1 at phase 2 against a ones operand
 // (4 extra MFMAs per K-tile); the 8 partials go through red[2][8][64] in LDS and wave 0 folds the
 // previous K-tile's into ks[K] at phase 1.
 template <bool AKC, bool BKC, int EPI, typename TO, int MODE, bool CS = false>
 __global__ void __launch_bounds__(NT, 1) gemm8_kernel(BigArgs g) {
-  constexpr bool STAG = MODE == 1 || MODE == 3, PRIO = MODE != 3, TILEWAIT = MODE == 4;
+  constexpr bool STAG = MODE == 1 || MODE == 3, PRIO = MODE != 3, TILEWAIT = MODE == 4 || MODE == 5;
+  constexpr bool POSTBAR = STAG || MODE == 5;       // second barrier per phase, after the MFMAs
   // CS: operand ring 128 KB | red[2][8][64] 4 KB | ks[K] fp32 12 KB  (the epilogue reuses the front)
   __shared__ __attribute__((aligned(16))) bf16 lds[CS ? (8 * HALF + 1024 * 2 + CS_KMAX * 2) : LDS_ELEMS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -571,7 +577,7 @@ __global__ void __launch_bounds__(NT, 1) gemm8_kernel(BigArgs g) {
             acc[mh * 4 + ii][nh * 2 + jj] = mma16(bv, ar[ii][kc], acc[mh * 4 + ii][nh * 2 + jj]);
           }
       if (PRIO) __builtin_amdgcn_s_setprio(0);
-      if (STAG) raw_barrier();
+      if (POSTBAR) raw_barrier();
     }
   }
   if (STAG && wm == 0) raw_barrier();  // re-align the groups
@@ -862,6 +868,152 @@ __global__ void __launch_bounds__(NT, 1) gemm8p_kernel(BigArgs g) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// 4-wave 256x256 kernel (hipBLASLt's MT256x256x64 geometry measured on this chip: 256 threads, one
+// wave per SIMD): 2 x 2 waves of 128x128 (64 accumulators = 256 registers per lane, AGPR-backed),
+// BK = 32 K-tiles in a 5-deep LDS ring (5 x 32 KB), K-tile t + 5 staged while t computes, the next
+// K-tile's fragments read while the current one's 64 MFMAs run (8 groups of {2 ds_read_b128, 1 LDS-DMA,
+// 8 MFMAs} pinned by sched_barriers), one counted vmcnt + one barrier per K-tile.  A, B K-contiguous.
+// LDS image of an operand K-tile: [256 rows][32 k] bf16 = 64-B rows; 16-B chunk c of row r stored at
+// chunk c ^ sw4(r), sw4(r) = 3 * ((r >> 3) & 1): conflict-free for the ds_read_b128 lane groups of a
+// 16-row fragment read (lanes 16q + i read row i, chunk q).
+constexpr int BK4 = 32, NT4 = 256, SLOT4 = 2 * TM * BK4;   // elements per ring slot (A + B, 32 KB)
+constexpr int NSLOT4 = 5;                                     // ring depth: 5 x 32 KB = the 160 KB of LDS
+static_assert(NSLOT4 * SLOT4 >= TM * LDC, "the epilogue tile reuses the ring");
+DEV void vm_wait_tiles(int n) {    // n younger K-tiles (8 LDS-DMAs each) may stay in flight
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+  }
+}
+DEV int sw4(int r) { return 3 * ((r >> 3) & 1); }
+// MFMA with the accumulator pinned to AGPRs (256 of them hold the 64 accumulators): hipcc otherwise
+// keeps MFMA accumulators in VGPRs and spills.  Volatile: program order is the issue order.
+DEV void mma16_acc(f32x4& acc, bf16x8 b, bf16x8 a) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
+}
+// first K-tile: the accumulator is DEFINED in AGPRs (srcC = 0), so no VGPR copy of it ever exists
+DEV void mma16_acc0(f32x4& acc, bf16x8 b, bf16x8 a) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(acc) : "v"(b), "v"(a));
+}
+
+template <int EPI, typename TO>
+__global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
+  __shared__ __attribute__((aligned(16))) bf16 lds[NSLOT4 * SLOT4];   // ring NSLOT4 x 32 KB | epilogue tile
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int tiles_n = (g.N + TN - 1) / TN, tiles_m = (g.M + TM - 1) / TM;
+  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int tm = t / tiles_n, tn = t % tiles_n;
+  const int m0 = tm * TM, n0 = tn * TN;
+  int kbeg = 0, kend = g.K;
+  if (g.ksplit > 0) { kbeg = blockIdx.y * g.ksplit; kend = min(g.K, kbeg + g.ksplit); }
+  const int nk = (kend - kbeg) / BK4;
+
+  // staging: 8 LDS-DMAs per thread per K-tile (4 A + 4 B), each wave-instruction 16 rows x 64 B, in
+  // the saddr form: uniform K-tile base (SGPRs, advanced per K-tile) + a per-lane 32-bit byte offset
+  // fixed for the whole loop (row clamped to the matrix, swizzled chunk)
+  const int srow = lane >> 2;
+  uint32_t voffA[4], voffB[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int r = (wave * 4 + j) * 16 + srow;
+    const int c = (lane & 3) ^ sw4(r);
+    voffA[j] = (uint32_t)(((long)(min(m0 + r, g.M - 1) - m0) * g.lda + c * 8) * 2);
+    voffB[j] = (uint32_t)(((long)(min(n0 + r, g.N - 1) - n0) * g.ldb + c * 8) * 2);
+  }
+  const bf16* baseA = g.A + (long)m0 * g.lda + kbeg;
+  const bf16* baseB = g.B + (long)n0 * g.ldb + kbeg;
+  auto stage_part = [&](int kt, int slot, int j) {           // part j = 0..7 of K-tile kt -> ring slot
+    bf16* dst = lds + slot * SLOT4 + (j < 4 ? 0 : TM * BK4) + (wave * 4 + (j & 3)) * 16 * BK4;
+    if (j < 4) glds16_asm_s(baseA + kt * BK4, voffA[j & 3], dst);
+    else glds16_asm_s(baseB + kt * BK4, voffB[j & 3], dst);
+  };
+  // fragment reads: rows r0 + (lane & 15) of a [256][32] image, chunk lane >> 4; the swizzle of row
+  // r0 + 16s + i equals that of row i (r0 % 16 == 0), so one per-lane offset + immediates serve all
+  const int fr = lane & 15, fq = lane >> 4;
+  const int offA = (wm * 128 + fr) * BK4 + ((fq ^ sw4(fr)) << 3);
+  const int offB = TM * BK4 + (wn * 128 + fr) * BK4 + ((fq ^ sw4(fr)) << 3);
+
+  f32x4 acc[8][8];           // defined by the first K-tile's MFMAs (mma16_acc0)
+
+  // prologue: K-tiles 0 .. NSLOT4-1 staged; 0 and 1 retired
+  for (int kt = 0; kt < NSLOT4; ++kt)
+    if (kt < nk)
+      for (int j = 0; j < 8; ++j) stage_part(kt, kt, j);
+  vm_wait_tiles(max(0, min(nk, NSLOT4) - 2));
+  raw_barrier();
+  bf16x8 fa[2][8], fb[2][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    fa[0][i] = *(const bf16x8*)(lds + offA + i * 16 * BK4);
+    fb[0][i] = *(const bf16x8*)(lds + offB + i * 16 * BK4);
+  }
+  // K-tile 0's slot is restaged in the first K-tile: every wave's reads of it must be done
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  raw_barrier();
+
+  // one K-tile k (ring slot `slot`): fragments fa/fb[H] (read in the previous K-tile), the next
+  // K-tile's (slot nslot) into [H ^ 1]; TAIL: near the end of K (fewer tiles left to read / stage)
+  auto ktile = [&](auto Hc, int k, int slot, int nslot, auto Ic, auto Tc) {
+    constexpr int H = decltype(Hc)::value;
+    constexpr bool INIT = decltype(Ic)::value, TAIL = decltype(Tc)::value;
+    const bool more = !TAIL || k + 1 < nk, st = !TAIL || k + NSLOT4 < nk;
+    const bf16* nimg = lds + nslot * SLOT4;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      if (more) {
+        fa[H ^ 1][s] = *(const bf16x8*)(nimg + offA + s * 16 * BK4);
+        fb[H ^ 1][s] = *(const bf16x8*)(nimg + offB + s * 16 * BK4);
+      }
+      if (st) stage_part(k + NSLOT4, slot, s);
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        if (INIT) mma16_acc0(acc[s][jj], fb[H][jj], fa[H][s]);
+        else mma16_acc(acc[s][jj], fb[H][jj], fa[H][s]);
+      }
+    }
+    // K-tile k + 2 retired (its fragments are read in the next K-tile); younger: k + 3 .. k + NSLOT4
+    if (!TAIL) vm_wait_tiles(NSLOT4 - 2);
+    else vm_wait_tiles(max(0, min(nk - 1, k + NSLOT4) - (k + 2)));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads of k + 1 done: its slot may be restaged
+    raw_barrier();
+  };
+  using C0 = std::integral_constant<int, 0>;
+  using C1 = std::integral_constant<int, 1>;
+  using F = std::false_type;
+  using T = std::true_type;
+  auto nxt = [](int sl) { return sl == NSLOT4 - 1 ? 0 : sl + 1; };
+  int slot = 0;
+  if (nk > NSLOT4) ktile(C0{}, 0, slot, nxt(slot), T{}, F{});
+  else ktile(C0{}, 0, slot, nxt(slot), T{}, T{});
+  slot = nxt(slot);
+  int kt = 1;
+  // steady state: every K-tile stages K-tile k + NSLOT4 and reads k + 1
+  for (; kt + 1 + NSLOT4 < nk; kt += 2) {
+    ktile(C1{}, kt, slot, nxt(slot), F{}, F{});
+    slot = nxt(slot);
+    ktile(C0{}, kt + 1, slot, nxt(slot), F{}, F{});
+    slot = nxt(slot);
+  }
+  for (; kt < nk; kt += 2) {
+    ktile(C1{}, kt, slot, nxt(slot), F{}, T{});
+    slot = nxt(slot);
+    if (kt + 1 < nk) {
+      ktile(C0{}, kt + 1, slot, nxt(slot), F{}, T{});
+      slot = nxt(slot);
+    }
+  }
+  // the asm MFMAs are opaque to the hazard recognizer: cover the result latency before the first
+  // accumulator read
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  big_epilogue<EPI, TO, 8, NT4>(g, acc, lds, m0, n0, tid, lane, wm, wn);
+}
+
 template <bool AKC, bool BKC, int EPI, typename TO>
 int launch_big(const BigArgs& a, int splits, hipStream_t s) {
   const int tiles = ((a.M + TM - 1) / TM) * ((a.N + TN - 1) / TN);
@@ -902,6 +1054,8 @@ int launch_big(const BigArgs& a, int splits, hipStream_t s) {
     const dim3 grid(tiles, splits);
     if (g_gemm8 == 2) hipLaunchKernelGGL((gemm8_kernel<AKC, BKC, EPI, TO, 2>), grid, dim3(NT), 0, s, a);
     else if (g_gemm8 == 4) hipLaunchKernelGGL((gemm8_kernel<AKC, BKC, EPI, TO, 4>), grid, dim3(NT), 0, s, a);
+    else if (g_gemm8 == 5) hipLaunchKernelGGL((gemm8_kernel<AKC, BKC, EPI, TO, 5>), grid, dim3(NT), 0, s, a);
+    else if (g_gemm8 == 6 && AKC && BKC) hipLaunchKernelGGL((gemm4w_kernel<EPI, TO>), grid, dim3(NT4), 0, s, a);
     else if (g_gemm8 == 3) hipLaunchKernelGGL((gemm8_kernel<AKC, BKC, EPI, TO, 3>), grid, dim3(NT), 0, s, a);
     else hipLaunchKernelGGL((gemm8_kernel<AKC, BKC, EPI, TO, 1>), grid, dim3(NT), 0, s, a);
     return (int)hipGetLastError();

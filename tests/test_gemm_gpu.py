@@ -371,3 +371,35 @@ def test_gemm_big_persistent_dgrad_colsum(persist, epi, M, N, K):
         assert torch.equal(k_out, c)
     finally:
         _tune(4, old)
+
+
+@pytest.mark.parametrize("epi", ["none", "bias", "bias_gelu", "bias_gelu_d", "gelu_noaux", "none_beta"])
+@pytest.mark.parametrize("M,N,K", [(4352, 808, 768), (2048, 2304, 96), (8192, 3072, 32), (16384, 768, 3072)])
+def test_gemm_big_4wave_fwd(epi, M, N, K):
+    """The 4-wave 256x256 kernel (128x128 per wave, AGPR accumulators, BK = 32 ring) on the forward
+    layout, selected with eegf_tune(1, 6): edge tiles, K = one K-tile, odd K-tile counts."""
+    k = _k()
+    old = _tune(1, 6)
+    try:
+        torch.manual_seed(23)
+        x = (torch.randn(M, K, device="cuda") * 0.3).to(torch.bfloat16)
+        w = (torch.randn(N, K, device="cuda") * 0.3).to(torch.bfloat16)
+        b = torch.randn(N, device="cuda")
+        if epi in ("none", "none_beta"):
+            c = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+            beta = 1.0 if epi == "none_beta" else 0.0
+            ref = beta * c.double() + 0.5 * (x.double() @ w.double().t())
+            k.gemm(x, w, c, M=M, N=N, K=K, a_kc=1, b_kc=1, lda=K, ldb=K, ldc=N, alpha=0.5, beta=beta)
+            torch.cuda.synchronize()
+            _check(c, ref, torch.bfloat16)
+            return
+        e = "bias_gelu" if epi == "gelu_noaux" else epi
+        aux = torch.empty(M, N, device="cuda", dtype=torch.bfloat16) if epi in ("bias_gelu", "bias_gelu_d") else None
+        out = k.linear(x, w, b, epi=e, aux=aux)
+        torch.cuda.synchronize()
+        ref, pre = _ref_epi(x.double() @ w.double().t(), e, b, None, 1.0)
+        _check(out, ref, torch.bfloat16)
+        if aux is not None:
+            _check(aux, pre, torch.bfloat16)
+    finally:
+        _tune(1, old)

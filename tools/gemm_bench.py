@@ -27,6 +27,8 @@ SHAPES = [
     ("ffn1_wgrad", 3072, 768, R, "wgrad", "none"),
     ("ffn2_wgrad", 768, 3072, R, "wgrad", "none"),
     ("ao_wgrad", 768, 768, R, "wgrad", "none"),
+    ("sq4k", 4096, 4096, 4096, "fwd", "none"),       # the guide's 8-phase template reference shape
+    ("sq8k", 8192, 8192, 8192, "fwd", "none"),
 ]
 
 
@@ -81,7 +83,8 @@ def run(name, M, N, Kd, layout, epi, iters=20):
         for _ in range(5):
             for v in VARIANTS:
                 # 5: 2-phase with static priority; 6: persistent 8-phase; -1: default routing
-                lib.eegf_tune(1, v if v < 5 else (-1 if v == 6 else 0))
+                # 0-4: key 1 = v; 5: 2-phase + static prio; 6: persistent; 7: 8-phase MODE 5; 8: 4-wave
+                lib.eegf_tune(1, {5: 0, 6: -1, 7: 5, 8: 6}.get(v, v))
                 lib.eegf_tune(3, 1 if v == 5 else 0)
                 lib.eegf_tune(4, 1 if v == 6 else 0)
                 f()
