@@ -899,7 +899,20 @@ DEV void mma16_acc0(f32x4& acc, bf16x8 b, bf16x8 a) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(acc) : "v"(b), "v"(a));
 }
 
-template <int EPI, typename TO>
+// the two ds_read_b64_tr_b16 of rd_col at precomputed element offsets o0 / o1
+DEV bf16x8 rd_col_off(const bf16* t, int o0, int o1) {
+  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(t + o0));
+  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(t + o1));
+  bf16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+// AKC / BKC: operand K-contiguous (row-major [rows][K] image, ds_read_b128 fragments) or k-major
+// ([K][cols] in memory: [32 k][256 cols] image with the swz_k chunk swizzle of stage_kmajor,
+// ds_read_b64_tr_b16 fragments: input-gradient B, weight-gradient A and B)
+template <bool AKC, bool BKC, int EPI, typename TO>
 __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
   __shared__ __attribute__((aligned(16))) bf16 lds[NSLOT4 * SLOT4];   // ring NSLOT4 x 32 KB | epilogue tile
   const int tid = threadIdx.x, lane = tid & 63;
@@ -916,27 +929,64 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
   // staging: 8 LDS-DMAs per thread per K-tile (4 A + 4 B), each wave-instruction 16 rows x 64 B, in
   // the saddr form: uniform K-tile base (SGPRs, advanced per K-tile) + a per-lane 32-bit byte offset
   // fixed for the whole loop (row clamped to the matrix, swizzled chunk)
-  const int srow = lane >> 2;
+  //   K-contiguous part j: rows (4w + j) 16 + lane / 4, 16-B chunk (lane & 3) ^ sw4(row) of the 64 B;
+  //   k-major part j: k-rows (4w + j) 2 + lane / 32, 16-B column chunk (lane & 31) ^ swz_k(k) of 512 B
+  auto voff_of = [&](bool kc, int j, int c0, int cmax, long ld) -> uint32_t {
+    if (kc) {
+      const int r = (wave * 4 + j) * 16 + (lane >> 2);
+      const int c = (lane & 3) ^ sw4(r);
+      return (uint32_t)(((long)(min(c0 + r, cmax - 1) - c0) * ld + c * 8) * 2);
+    }
+    const int k = (wave * 4 + j) * 2 + (lane >> 5);
+    const int c = (lane & 31) ^ swz_k(k);
+    return (uint32_t)(((long)k * ld + min(c0 + c * 8, cmax - 8) - c0) * 2);
+  };
   uint32_t voffA[4], voffB[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int r = (wave * 4 + j) * 16 + srow;
-    const int c = (lane & 3) ^ sw4(r);
-    voffA[j] = (uint32_t)(((long)(min(m0 + r, g.M - 1) - m0) * g.lda + c * 8) * 2);
-    voffB[j] = (uint32_t)(((long)(min(n0 + r, g.N - 1) - n0) * g.ldb + c * 8) * 2);
+    voffA[j] = voff_of(AKC, j, m0, g.M, g.lda);
+    voffB[j] = voff_of(BKC, j, n0, g.N, g.ldb);
   }
-  const bf16* baseA = g.A + (long)m0 * g.lda + kbeg;
-  const bf16* baseB = g.B + (long)n0 * g.ldb + kbeg;
+  // uniform base of K-tile kt: K-contiguous advances 32 elements, k-major 32 rows
+  const bf16* baseA = AKC ? g.A + (long)m0 * g.lda + kbeg : g.A + (long)kbeg * g.lda + m0;
+  const bf16* baseB = BKC ? g.B + (long)n0 * g.ldb + kbeg : g.B + (long)kbeg * g.ldb + n0;
+  const long stepA = AKC ? BK4 : (long)BK4 * g.lda, stepB = BKC ? BK4 : (long)BK4 * g.ldb;
   auto stage_part = [&](int kt, int slot, int j) {           // part j = 0..7 of K-tile kt -> ring slot
-    bf16* dst = lds + slot * SLOT4 + (j < 4 ? 0 : TM * BK4) + (wave * 4 + (j & 3)) * 16 * BK4;
-    if (j < 4) glds16_asm_s(baseA + kt * BK4, voffA[j & 3], dst);
-    else glds16_asm_s(baseB + kt * BK4, voffB[j & 3], dst);
+    const bool kc = j < 4 ? AKC : BKC;
+    bf16* dst = lds + slot * SLOT4 + (j < 4 ? 0 : TM * BK4) + (wave * 4 + (j & 3)) * (kc ? 16 * BK4 : 2 * TN);
+    if (j < 4) glds16_asm_s(baseA + kt * stepA, voffA[j & 3], dst);
+    else glds16_asm_s(baseB + kt * stepB, voffB[j & 3], dst);
   };
-  // fragment reads: rows r0 + (lane & 15) of a [256][32] image, chunk lane >> 4; the swizzle of row
-  // r0 + 16s + i equals that of row i (r0 % 16 == 0), so one per-lane offset + immediates serve all
+  // fragment reads.  K-contiguous: rows r0 + (lane & 15) of a [256][32] image, chunk lane >> 4; the
+  // swizzle of row r0 + 16s + i equals that of row i (r0 % 16 == 0): one per-lane offset +
+  // immediates.  k-major: rd_col of k-rows 8 (lane >> 4) + .., columns r0 + 16s + (lane & 15), at
+  // per-fragment offsets precomputed once (16 VGPRs per operand)
   const int fr = lane & 15, fq = lane >> 4;
   const int offA = (wm * 128 + fr) * BK4 + ((fq ^ sw4(fr)) << 3);
   const int offB = TM * BK4 + (wn * 128 + fr) * BK4 + ((fq ^ sw4(fr)) << 3);
+  int tA0[8], tA1[8], tB0[8], tB1[8];
+  auto col_offs = [&](int c0, int& o0, int& o1) {
+    const int q = fr >> 2, p4 = fr & 3;
+    const int col = c0 + 4 * p4, ch = col >> 3, off = col & 7;
+    const int ka = 8 * fq + q, kb = ka + 4;
+    o0 = ka * TN + (((ch ^ swz_k(ka)) << 3) | off);
+    o1 = kb * TN + (((ch ^ swz_k(kb)) << 3) | off);
+  };
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (!AKC) col_offs(wm * 128 + 16 * i, tA0[i], tA1[i]);
+    if (!BKC) {
+      col_offs(wn * 128 + 16 * i, tB0[i], tB1[i]);
+      tB0[i] += TM * BK4;
+      tB1[i] += TM * BK4;
+    }
+  }
+  auto rdA = [&](const bf16* img, int i) {
+    return AKC ? *(const bf16x8*)(img + offA + i * 16 * BK4) : rd_col_off(img, tA0[i], tA1[i]);
+  };
+  auto rdB = [&](const bf16* img, int i) {
+    return BKC ? *(const bf16x8*)(img + offB + i * 16 * BK4) : rd_col_off(img, tB0[i], tB1[i]);
+  };
 
   f32x4 acc[8][8];           // defined by the first K-tile's MFMAs (mma16_acc0)
 
@@ -949,8 +999,8 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
   bf16x8 fa[2][8], fb[2][8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    fa[0][i] = *(const bf16x8*)(lds + offA + i * 16 * BK4);
-    fb[0][i] = *(const bf16x8*)(lds + offB + i * 16 * BK4);
+    fa[0][i] = rdA(lds, i);
+    fb[0][i] = rdB(lds, i);
   }
   // K-tile 0's slot is restaged in the first K-tile: every wave's reads of it must be done
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -966,8 +1016,8 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       if (more) {
-        fa[H ^ 1][s] = *(const bf16x8*)(nimg + offA + s * 16 * BK4);
-        fb[H ^ 1][s] = *(const bf16x8*)(nimg + offB + s * 16 * BK4);
+        fa[H ^ 1][s] = rdA(nimg, s);
+        fb[H ^ 1][s] = rdB(nimg, s);
       }
       if (st) stage_part(k + NSLOT4, slot, s);
 #pragma unroll
@@ -1022,6 +1072,13 @@ int launch_big(const BigArgs& a, int splits, hipStream_t s) {
     // schedule with one vmcnt per K-tile for the input-gradient GEMMs (+10-25 %) and the forward
     // GEMMs except the smallest (N, K <= 768); the 2-phase kernel for the weight gradients
     const bool use8 = sizeof(TO) == 2 && AKC && (!BKC || a.N > 768 || a.K > 768);
+    // the 4-wave kernel (profiles/r1s2_gemm4w_ab.log, r1s2_gemm4w_kmajor_ab.log): +7-8 % on the
+    // weight gradients and on K >= 2048 (K-loop-bound; at K = 768 its unoverlapped epilogue loses);
+    // it has no fused column sums
+    if (!a.colsum_part && (sizeof(TO) == 4 ? (!AKC && !BKC) : a.K >= 2048)) {
+      hipLaunchKernelGGL((gemm4w_kernel<AKC, BKC, EPI, TO>), dim3(tiles, splits), dim3(NT4), 0, s, a);
+      return (int)hipGetLastError();
+    }
     if constexpr (AKC && sizeof(TO) == 2) {
       const bool usep = g_gemm8p > 0;
       if (usep && splits == 1 && a.K >= 2 * BK) {
@@ -1055,7 +1112,7 @@ int launch_big(const BigArgs& a, int splits, hipStream_t s) {
     if (g_gemm8 == 2) hipLaunchKernelGGL((gemm8_kernel<AKC, BKC, EPI, TO, 2>), grid, dim3(NT), 0, s, a);
     else if (g_gemm8 == 4) hipLaunchKernelGGL((gemm8_kernel<AKC, BKC, EPI, TO, 4>), grid, dim3(NT), 0, s, a);
     else if (g_gemm8 == 5) hipLaunchKernelGGL((gemm8_kernel<AKC, BKC, EPI, TO, 5>), grid, dim3(NT), 0, s, a);
-    else if (g_gemm8 == 6 && AKC && BKC) hipLaunchKernelGGL((gemm4w_kernel<EPI, TO>), grid, dim3(NT4), 0, s, a);
+    else if (g_gemm8 == 6) hipLaunchKernelGGL((gemm4w_kernel<AKC, BKC, EPI, TO>), grid, dim3(NT4), 0, s, a);
     else if (g_gemm8 == 3) hipLaunchKernelGGL((gemm8_kernel<AKC, BKC, EPI, TO, 3>), grid, dim3(NT), 0, s, a);
     else hipLaunchKernelGGL((gemm8_kernel<AKC, BKC, EPI, TO, 1>), grid, dim3(NT), 0, s, a);
     return (int)hipGetLastError();

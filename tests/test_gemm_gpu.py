@@ -403,3 +403,42 @@ def test_gemm_big_4wave_fwd(epi, M, N, K):
             _check(aux, pre, torch.bfloat16)
     finally:
         _tune(1, old)
+
+
+@pytest.mark.parametrize("epi", ["none", "mul_aux", "dgelu"])
+@pytest.mark.parametrize("M,N,K", [(4352, 808, 768), (2048, 3072, 96), (8192, 768, 2304)])
+def test_gemm_big_4wave_dgrad(epi, M, N, K):
+    """4-wave kernel with a k-major B (input gradient, ds_read_b64_tr_b16 fragments)."""
+    k = _k()
+    old = _tune(1, 6)
+    try:
+        torch.manual_seed(24)
+        dy = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+        w = (torch.randn(K, N, device="cuda") * 0.1).to(torch.bfloat16)
+        aux = torch.randn(M, N, device="cuda").to(torch.bfloat16) if epi != "none" else None
+        out = k.linear_dgrad(dy, w, epi=epi, aux=aux)
+        torch.cuda.synchronize()
+        ref, _ = _ref_epi(dy.double() @ w.double(), epi, None, aux, 1.0)
+        _check(out, ref, torch.bfloat16)
+    finally:
+        _tune(1, old)
+
+
+@pytest.mark.parametrize("M,N,K", [(2304, 768, 65536), (768, 3072, 16384), (808, 264, 8192)])
+def test_gemm_big_4wave_wgrad(M, N, K):
+    """4-wave kernel with k-major A and B (weight gradient), fp32 split-K slabs, beta accumulate."""
+    k = _k()
+    old = _tune(1, 6)
+    try:
+        torch.manual_seed(25)
+        dy = torch.randn(K, M, device="cuda").to(torch.bfloat16)
+        x = torch.randn(K, N, device="cuda").to(torch.bfloat16)
+        dw = torch.randn(M, N, device="cuda")
+        ref = dw.double() + dy.double().t() @ x.double()
+        ws = torch.empty(24 << 20, device="cuda")
+        k.gemm(dy, x, dw, M=M, N=N, K=K, a_kc=0, b_kc=0, lda=M, ldb=N, ldc=N, beta=1.0, workspace=ws)
+        torch.cuda.synchronize()
+        err = ((dw.double() - ref).abs().max() / ref.abs().max()).item()
+        assert err <= 2e-3, err
+    finally:
+        _tune(1, old)
