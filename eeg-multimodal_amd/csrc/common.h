@@ -53,6 +53,16 @@ DEV void glds16_asm_s(const void* base, uint32_t voff, const void* lds_base) {
   asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(bu), "s"(l)
                : "memory", "m0");
 }
+// saddr form with a 32-bit LDS byte address (no generic->LDS pointer cast per call) and a base the
+// caller knows to be wave-uniform
+DEV void glds16_asm_sa(const void* base, uint32_t voff, uint32_t lds_addr) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(base), "s"(lds_addr)
+               : "memory", "m0");
+}
+DEV uint32_t lds_addr_of(const void* p) {
+  typedef __attribute__((address_space(3))) void lv;
+  return (uint32_t)(uintptr_t)(lv*)p;
+}
 #pragma clang diagnostic pop
 
 DEV float to_f32(float x) { return x; }

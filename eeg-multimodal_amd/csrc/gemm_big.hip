@@ -951,11 +951,13 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
   const bf16* baseA = AKC ? g.A + (long)m0 * g.lda + kbeg : g.A + (long)kbeg * g.lda + m0;
   const bf16* baseB = BKC ? g.B + (long)n0 * g.ldb + kbeg : g.B + (long)kbeg * g.ldb + n0;
   const long stepA = AKC ? BK4 : (long)BK4 * g.lda, stepB = BKC ? BK4 : (long)BK4 * g.ldb;
-  auto stage_part = [&](int kt, int slot, int j) {           // part j = 0..7 of K-tile kt -> ring slot
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr_of(lds));
+  auto stage_part = [&](const bf16* bA, const bf16* bB, int slot, int j) {   // part j of a K-tile -> ring slot
     const bool kc = j < 4 ? AKC : BKC;
-    bf16* dst = lds + slot * SLOT4 + (j < 4 ? 0 : TM * BK4) + (wave * 4 + (j & 3)) * (kc ? 16 * BK4 : 2 * TN);
-    if (j < 4) glds16_asm_s(baseA + kt * stepA, voffA[j & 3], dst);
-    else glds16_asm_s(baseB + kt * stepB, voffB[j & 3], dst);
+    const uint32_t dst = lds0 + 2u * (slot * SLOT4 + (j < 4 ? 0 : TM * BK4) +
+                                      (wave * 4 + (j & 3)) * (kc ? 16 * BK4 : 2 * TN));
+    if (j < 4) glds16_asm_sa(bA, voffA[j & 3], dst);
+    else glds16_asm_sa(bB, voffB[j & 3], dst);
   };
   // fragment reads.  K-contiguous: rows r0 + (lane & 15) of a [256][32] image, chunk lane >> 4; the
   // swizzle of row r0 + 16s + i equals that of row i (r0 % 16 == 0): one per-lane offset +
@@ -993,7 +995,7 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
   // prologue: K-tiles 0 .. NSLOT4-1 staged; 0 and 1 retired
   for (int kt = 0; kt < NSLOT4; ++kt)
     if (kt < nk)
-      for (int j = 0; j < 8; ++j) stage_part(kt, kt, j);
+      for (int j = 0; j < 8; ++j) stage_part(baseA + kt * stepA, baseB + kt * stepB, kt, j);
   vm_wait_tiles(max(0, min(nk, NSLOT4) - 2));
   raw_barrier();
   bf16x8 fa[2][8], fb[2][8];
@@ -1013,18 +1015,26 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
     constexpr bool INIT = decltype(Ic)::value, TAIL = decltype(Tc)::value;
     const bool more = !TAIL || k + 1 < nk, st = !TAIL || k + NSLOT4 < nk;
     const bf16* nimg = lds + nslot * SLOT4;
+    const bf16* sA = baseA + (k + NSLOT4) * stepA;        // uniform K-tile bases of the stage
+    const bf16* sB = baseB + (k + NSLOT4) * stepB;
+    auto mma = [&](int s, int jj) {
+      if (INIT) mma16_acc0(acc[s][jj], fb[H][jj], fa[H][s]);
+      else mma16_acc(acc[s][jj], fb[H][jj], fa[H][s]);
+    };
+    // group s: the non-MFMA work sits in the shadows of the group's first MFMAs
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
-      if (more) {
-        fa[H ^ 1][s] = rdA(nimg, s);
-        fb[H ^ 1][s] = rdB(nimg, s);
-      }
-      if (st) stage_part(k + NSLOT4, slot, s);
+      mma(s, 0);
+      if (more) fa[H ^ 1][s] = rdA(nimg, s);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(s, 1);
+      if (more) fb[H ^ 1][s] = rdB(nimg, s);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(s, 2);
+      if (st) stage_part(sA, sB, slot, s);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int jj = 0; jj < 8; ++jj) {
-        if (INIT) mma16_acc0(acc[s][jj], fb[H][jj], fa[H][s]);
-        else mma16_acc(acc[s][jj], fb[H][jj], fa[H][s]);
-      }
+      for (int jj = 3; jj < 8; ++jj) mma(s, jj);
     }
     // K-tile k + 2 retired (its fragments are read in the next K-tile); younger: k + 3 .. k + NSLOT4
     if (!TAIL) vm_wait_tiles(NSLOT4 - 2);
