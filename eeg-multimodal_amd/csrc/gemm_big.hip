@@ -610,6 +610,9 @@ __global__ void __launch_bounds__(NT, 1) gemm8_kernel(BigArgs g) {
 // of following a prologue bubble.  CS: the fused A column sums of gemm8_kernel, per tile.
 // Measured (tools/gemm_bench.py --ab, profiles/r1s2_gemm_persist_ab.log): 5-10 % SLOWER than the one-
 // shot gemm8 MODE 4 on every bench shape except the aux-input epilogues (+10 %), so opt-in only.
+// 4-wave kernel with fused column sums (eegf_tune key 5): work in progress, the sums of K-tile 1 miss
+// half the rows (tools/dbg_acs.py) -- off by default, dgrad+colsum stays on gemm8_kernel CS
+int g_gemm4w_cs = 0;
 int g_gemm8p = [] { const char* e = getenv("EEGF_GEMM8P"); return e ? atoi(e) : 0; }();
 
 int big_cus() {
@@ -912,9 +915,17 @@ DEV bf16x8 rd_col_off(const bf16* t, int o0, int o1) {
 // AKC / BKC: operand K-contiguous (row-major [rows][K] image, ds_read_b128 fragments) or k-major
 // ([K][cols] in memory: [32 k][256 cols] image with the swz_k chunk swizzle of stage_kmajor,
 // ds_read_b64_tr_b16 fragments: input-gradient B, weight-gradient A and B)
-template <bool AKC, bool BKC, int EPI, typename TO>
+// CS (AKC only): fused column sums of A over the tile's rows for tile column 0 (the bias gradient of
+// an input-gradient GEMM): wave w sums rows 64w .. 64w + 63 of the staged K-tile with 4 MFMAs
+// against a ones operand (A^T fragments by transpose reads), parks its 32 partials in
+// red[k & 1][w]; wave 0 folds the previous K-tile's 4 partials (fixed order) into ks[K] after the
+// K-tile barrier.  The ring is 4 deep then (128 KB + red 1 KB + ks 12 KB).
+template <bool AKC, bool BKC, int EPI, typename TO, bool CS = false>
 __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
-  __shared__ __attribute__((aligned(16))) bf16 lds[NSLOT4 * SLOT4];   // ring NSLOT4 x 32 KB | epilogue tile
+  constexpr int NSLOT4 = CS ? 4 : ::NSLOT4;
+  constexpr int LDS4 = CS ? (NSLOT4 * SLOT4 + 512 + CS_KMAX * 2) : NSLOT4 * SLOT4;
+  static_assert(LDS4 * 2 <= 160 * 1024 && LDS4 >= TM * LDC, "LDS budget / epilogue tile");
+  __shared__ __attribute__((aligned(16))) bf16 lds[LDS4];   // ring NSLOT4 x 32 KB | epilogue tile (| red | ks)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
@@ -989,6 +1000,60 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
   auto rdB = [&](const bf16* img, int i) {
     return BKC ? *(const bf16x8*)(img + offB + i * 16 * BK4) : rd_col_off(img, tB0[i], tB1[i]);
   };
+  float* red = (float*)(lds + NSLOT4 * SLOT4);            // [2][4 waves][32]
+  float* ks = red + 256;                                   // [K]
+  const bool do_cs = CS && tn == 0;
+  // column sums on the MFMA: D = ones[16 x 32 rows] x A^T-chunk[32 rows x 16 k] (every D row = the
+  // 16 column sums), A^T read from the row-major image with ds_read_b64_tr_b16.  Wave w: rows
+  // 64w + 32rc + .. (rc = 0, 1), k-blocks cb = 0, 1 -> 4 MFMAs + 4 fragment reads per K-tile.
+  bf16x8 cs_ones[2];
+  int cs_o0[2][2], cs_o1[2][2];
+#pragma unroll
+  for (int rc = 0; rc < 2; ++rc) {
+    const int rb = 64 * wave + 32 * rc + 8 * fq;           // first row of the lane's 8-row group
+#pragma unroll
+    for (int e = 0; e < 8; ++e) cs_ones[rc][e] = (bf16)(m0 + rb + e < g.M ? 1.0f : 0.0f);
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      const int q = fr >> 2, p4 = fr & 3, col = 16 * cb + 4 * p4, ch = col >> 3, off = col & 7;
+      const int ra = rb + q, rbb = rb + 4 + q;
+      cs_o0[rc][cb] = ra * BK4 + (((ch ^ sw4(ra)) << 3) | off);
+      cs_o1[rc][cb] = rbb * BK4 + (((ch ^ sw4(rbb)) << 3) | off);
+    }
+  }
+  f32x4 csd[2];
+  bf16x8 cst[2];
+  // chunk c = 0..3 of a K-tile image: (rc, cb) = (c & 1, c >> 1).  In the loop the read of chunk c
+  // sits in group c and its MFMA in group c + 1, after N younger LDS ops of that wave (group c + 1's
+  // fragment reads: 1 ds_read_b128 + 2 transpose reads, and chunk c + 1's 2 reads when c < 3; wave 0's
+  // fold only adds younger ops): lgkmcnt(N) retires exactly the chunk's read.
+  auto cs_read = [&](const bf16* img, int c) {
+    cst[c & 1] = rd_col_off(img, cs_o0[c & 1][c >> 1], cs_o1[c & 1][c >> 1]);
+  };
+  // csd is zeroed (VALU) at the start of the K-tile, a group (>= 8 MFMAs) before the chunk MFMAs
+  // read it: the asm MFMAs are invisible to the hazard recognizer, and an "=v" output tied to a
+  // "+v" input of the next chunk let the compiler place a copy right behind the MFMA (read before
+  // the result was written: the rc = 1 rows went missing)
+  auto cs_zero = [&]() {
+    csd[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+    csd[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  auto cs_mfma = [&](int c, int) {       // compiler-visible MFMA: the hazard recognizer covers it
+    csd[c >> 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cs_ones[c & 1], cst[c & 1], csd[c >> 1], 0, 0, 0);
+  };
+  auto cs_store = [&](int k) {      // lanes 0..15 hold the 16 sums of each k-block (D row 0)
+    if (lane < 16) {
+      float* r = red + (k & 1) * 128 + wave * 32;
+      r[lane] = csd[0][0];
+      r[16 + lane] = csd[1][0];
+    }
+  };
+  auto cs_fold = [&](int k) {                              // wave 0: ks[k*32 + l] = sum of the 4 partials
+    if (wave == 0 && lane < 32) {
+      const float* r = red + (k & 1) * 128 + lane;
+      ks[k * BK4 + lane] = ((r[0] + r[32]) + r[64]) + r[96];
+    }
+  };
 
   f32x4 acc[8][8];           // defined by the first K-tile's MFMAs (mma16_acc0)
 
@@ -1004,13 +1069,26 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
     fa[0][i] = rdA(lds, i);
     fb[0][i] = rdB(lds, i);
   }
+  if (CS && do_cs) {      // K-tiles 0 and 1's column sums (retired above); the loop does k + 1's, k >= 1
+#pragma unroll
+    for (int t2 = 0; t2 < 2; ++t2) {
+      if (t2 == 1 && nk < 2) break;
+      cs_zero();
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        cs_read(lds + t2 * SLOT4, c);
+        cs_mfma(c, 0);
+      }
+      cs_store(t2);
+    }
+  }
   // K-tile 0's slot is restaged in the first K-tile: every wave's reads of it must be done
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   raw_barrier();
 
   // one K-tile k (ring slot `slot`): fragments fa/fb[H] (read in the previous K-tile), the next
   // K-tile's (slot nslot) into [H ^ 1]; TAIL: near the end of K (fewer tiles left to read / stage)
-  auto ktile = [&](auto Hc, int k, int slot, int nslot, auto Ic, auto Tc) {
+  auto ktile = [&](auto Hc, int k, int slot, int nslot, auto Ic, auto Tc) __attribute__((always_inline)) {
     constexpr int H = decltype(Hc)::value;
     constexpr bool INIT = decltype(Ic)::value, TAIL = decltype(Tc)::value;
     const bool more = !TAIL || k + 1 < nk, st = !TAIL || k + NSLOT4 < nk;
@@ -1033,8 +1111,21 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
       mma(s, 2);
       if (st) stage_part(sA, sB, slot, s);
       __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int jj = 3; jj < 8; ++jj) mma(s, jj);
+      // CS: sums of the NEXT K-tile from its image (tile k's own slot is being restaged now); fold
+      // of tile k's partials (stored in the previous K-tile / the prologue, published by its barrier)
+      mma(s, 3);
+      if (CS && !INIT && do_cs && more && s == 0) cs_zero();
+      if (CS && !INIT && do_cs && more && s < 4) cs_read(nimg, s);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(s, 4);
+      if (CS && !INIT && do_cs && more && s >= 1 && s <= 4) cs_mfma(s - 1, s == 4 ? 3 : 5);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(s, 5);
+      if (CS && s == 1 && do_cs) cs_fold(k);
+      if (CS && !INIT && s == 7 && do_cs && more) cs_store(k + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(s, 6);
+      mma(s, 7);
     }
     // K-tile k + 2 retired (its fragments are read in the next K-tile); younger: k + 3 .. k + NSLOT4
     if (!TAIL) vm_wait_tiles(NSLOT4 - 2);
@@ -1070,6 +1161,10 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
   // the asm MFMAs are opaque to the hazard recognizer: cover the result latency before the first
   // accumulator read
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_waitcnt vmcnt(0)" ::: "memory");
+  if (CS && do_cs) {                     // every K-tile folded in the loop (fold(k) in K-tile k)
+    __syncthreads();
+    for (int k = tid; k < g.K; k += NT4) g.colsum_part[(long)tm * g.K + k] = ks[k];
+  }
   __syncthreads();
   big_epilogue<EPI, TO, 8, NT4>(g, acc, lds, m0, n0, tid, lane, wm, wn);
 }
@@ -1083,11 +1178,20 @@ int launch_big(const BigArgs& a, int splits, hipStream_t s) {
     // GEMMs except the smallest (N, K <= 768); the 2-phase kernel for the weight gradients
     const bool use8 = sizeof(TO) == 2 && AKC && (!BKC || a.N > 768 || a.K > 768);
     // the 4-wave kernel (profiles/r1s2_gemm4w_ab.log, r1s2_gemm4w_kmajor_ab.log): +7-8 % on the
-    // weight gradients and on K >= 2048 (K-loop-bound; at K = 768 its unoverlapped epilogue loses);
-    // it has no fused column sums
-    if (!a.colsum_part && (sizeof(TO) == 4 ? (!AKC && !BKC) : a.K >= 2048)) {
-      hipLaunchKernelGGL((gemm4w_kernel<AKC, BKC, EPI, TO>), dim3(tiles, splits), dim3(NT4), 0, s, a);
-      return (int)hipGetLastError();
+    // weight gradients and on K >= 2048 (K-loop-bound; at K = 768 its unoverlapped epilogue loses)
+    if (sizeof(TO) == 4 ? (!AKC && !BKC) : a.K >= 2048) {
+      if (g_gemm4w_cs > 0) {            // fused column sums on the 4-wave kernel: opt-in, NOT parity-green
+        if constexpr (AKC && !BKC && sizeof(TO) == 2) {
+          if (a.colsum_part) {
+            hipLaunchKernelGGL((gemm4w_kernel<AKC, BKC, EPI, TO, true>), dim3(tiles, splits), dim3(NT4), 0, s, a);
+            return (int)hipGetLastError();
+          }
+        }
+      }
+      if (!a.colsum_part) {
+        hipLaunchKernelGGL((gemm4w_kernel<AKC, BKC, EPI, TO>), dim3(tiles, splits), dim3(NT4), 0, s, a);
+        return (int)hipGetLastError();
+      }
     }
     if constexpr (AKC && sizeof(TO) == 2) {
       const bool usep = g_gemm8p > 0;
@@ -1232,5 +1336,6 @@ extern "C" int eegf_tune(int key, int value) {
   if (key == 2) { const int o = g_attn256_mode; g_attn256_mode = value; return o; }
   if (key == 3) { const int o = g_big_prio; g_big_prio = value; return o; }
   if (key == 4) { const int o = g_gemm8p; g_gemm8p = value; return o; }
+  if (key == 5) { const int o = g_gemm4w_cs; g_gemm4w_cs = value; return o; }
   return EEGF_ERR_ARG;
 }

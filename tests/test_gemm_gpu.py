@@ -269,7 +269,8 @@ def test_gemm_big_dgrad_beta(M, N, K):
 
 
 @pytest.mark.parametrize("epi", ["none", "dgelu"])
-@pytest.mark.parametrize("M,N,K,beta", [(4352, 808, 768, 0.0), (2056, 768, 3072, 1.0), (4096, 768, 2304, 1.0)])
+@pytest.mark.parametrize("M,N,K,beta", [(4352, 808, 768, 0.0), (2056, 768, 3072, 1.0), (4096, 768, 2304, 1.0),
+                                        (16648, 808, 2304, 0.0), (4104, 3072, 3072, 1.0)])
 def test_gemm_acs_fused_bias_grad(epi, M, N, K, beta):
     if epi == "dgelu":
         beta = 0.0          # activation-derivative epilogues read aux in place of C (beta must be 0)
