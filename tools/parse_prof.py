@@ -4,6 +4,7 @@ usage: python tools/parse_prof.py <round_tag> <stats_dir> [<pmc_fetch_dir> <pmc_
 
 * <stats_dir>/run_kernel_stats.csv (from --kernel-trace --stats) -> profiles/<tag>_kernel_stats.md
   (per-kernel totals, per-step times and the average duration of the roofline kernel).
+  Also accepts the run_results.db layout? no: run with --output-format csv.
 * --pmc FETCH_SIZE / WRITE_SIZE passes (separate runs) -> per-launch HBM bytes for the roofline
   kernel (gemm_big_kernel<true, EPI_BIAS_GELU> = BERT FFN1 forward):
       bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024
@@ -16,8 +17,10 @@ import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-FFN1S = ("gemm_big_kernelILb1ELi2E", "gemm_big_kernel<true, 2>")   # <B_KC=true, EPI_BIAS_GELU>
-FFN1 = FFN1S[1]
+# BERT FFN1 forward: the 8-phase kernel with EPI_BIAS_GELU (pass 1, GELU only) and EPI_BIAS_GELU_D
+# (pass 2, GELU + GELU'); bench.py's live roofline averages both, so do the stats and traffic here
+FFN1S = ("gemm8_kernelILb1ELb1ELi2EDF16bLi4E", "gemm8_kernelILb1ELb1ELi8EDF16bLi4E")
+FFN1 = "gemm8_kernel<true, true, EPI_BIAS_GELU{,_D}, bf16, 4>"
 
 
 def short(name: str) -> str:
@@ -31,13 +34,15 @@ def stats(tag, d, steps):
            f"bench.py PriGumbel B=256 bf16, {steps} iterations (warm-up included) traced; "
            f"total kernel time {tot / 1e6:.1f} ms = {tot / 1e6 / steps:.2f} ms/iteration", "",
            "| ms/iter | % | calls/iter | avg us | kernel |", "|---:|---:|---:|---:|---|"]
-    ffn1 = None
+    ffn1_ns, ffn1_calls = 0.0, 0
     for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"])):
         t = float(r["TotalDurationNs"])
         out.append(f"| {t / 1e6 / steps:.3f} | {100 * t / tot:.1f} | {int(r['Calls']) / steps:.1f} | "
                    f"{float(r['AverageNs']) / 1e3:.1f} | `{short(r['Name'])}` |")
         if any(k in r["Name"] for k in FFN1S):
-            ffn1 = float(r["AverageNs"]) / 1e6
+            ffn1_ns += t
+            ffn1_calls += int(r["Calls"])
+    ffn1 = ffn1_ns / ffn1_calls / 1e6 if ffn1_calls else None
     if ffn1:
         out += ["", f"roofline kernel (FFN1 fwd, `{FFN1}...`): average {ffn1:.4f} ms = "
                     f"{309.24e9 / (ffn1 * 1e-3) / 1e12:.1f} TFLOP/s algorithmic (309.2 GFLOP per launch)"]
@@ -63,7 +68,8 @@ if __name__ == "__main__":
         fetch, write = pmc(args[2], "FETCH_SIZE"), pmc(args[3], "WRITE_SIZE")
         if fetch is not None and write is not None:
             hbm = 2 * fetch * 1024 + write * 1024
-            alg = 65536 * 768 * 2 + 3072 * 768 * 2 + 2 * 65536 * 3072 * 2 + 3072 * 4
+            # A + W + bias read; output 1 tensor (pass 1) or 2 (pass 2): averaged like the launches
+            alg = 65536 * 768 * 2 + 3072 * 768 * 2 + 1.5 * 65536 * 3072 * 2 + 3072 * 4
             d = {"ffn1_fwd": {"hbm_bytes_per_launch": hbm, "fetch_kb": fetch, "write_kb": write,
                               "algorithmic_bytes": alg, "round": tag,
                               "note": "2*FETCH_SIZE + WRITE_SIZE (KB->B), gfx950 FETCH correction"}}
