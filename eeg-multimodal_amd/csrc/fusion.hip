@@ -253,6 +253,42 @@ __global__ void __launch_bounds__(256) ce_kernel(const T* logits, const long lon
   }
 }
 
+// feawei DP initialisation (past_acc.py:98-103; past_acc_feawei.py:153-163): m = colsum / count is the
+// column mean of the normalised features of a forward pass over the train set; z = (m - mean m) /
+// std m (np.std, ddof 0) when zscore, else z = m; w = 1 - sigmoid(k z) in fp32;
+// DP = (base + w) - 0.5.  One 256-thread workgroup; mean and variance accumulate in fp64 (the
+// reference's feature matrix is a float64 numpy array), two passes.
+DEV double block_sum_f64(double v, double* red) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ __launch_bounds__(256) void feawei_kernel(int D, const float* colsum, double inv_count, float k,
+                                                     int zscore, const float* base, float* dp) {
+  __shared__ double red[4];
+  double mu = 0.0, sd = 1.0;
+  if (zscore) {
+    double s = 0.0;
+    for (int c = threadIdx.x; c < D; c += 256) s += (double)colsum[c] * inv_count;
+    mu = block_sum_f64(s, red) / D;
+    double q = 0.0;
+    for (int c = threadIdx.x; c < D; c += 256) {
+      const double d = (double)colsum[c] * inv_count - mu;
+      q += d * d;
+    }
+    sd = sqrt(block_sum_f64(q, red) / D);
+  }
+  for (int c = threadIdx.x; c < D; c += 256) {
+    const double m = (double)colsum[c] * inv_count;
+    const float x = (float)((double)k * (zscore ? (m - mu) / sd : m));
+    const float w = 1.0f - 1.0f / (1.0f + expf(-x));
+    dp[c] = (base[c] + w) - 0.5f;
+  }
+}
+
 }  // namespace
 
 extern "C" int eegf_fusion_fwd(int dtype, int B, int variant, const void* pooled, long ld_pooled, const void* img,
@@ -308,5 +344,13 @@ extern "C" int eegf_cross_entropy(int dtype, int B, int C, const void* logits, c
     hipLaunchKernelGGL(ce_kernel<bf16>, dim3(1), dim3(256), 0, stream, (const bf16*)logits, labels, B, C, reduction,
                        dscale, loss, correct, (bf16*)dlogits);
   else return EEGF_ERR_ARG;
+  return (int)hipGetLastError();
+}
+
+extern "C" int eegf_feawei_init(int D, const float* colsum, long count, float k, int zscore, const float* base,
+                                float* dp, hipStream_t stream) {
+  if (D <= 0 || count <= 0 || !colsum || !base || !dp) return EEGF_ERR_ARG;
+  hipLaunchKernelGGL(feawei_kernel, dim3(1), dim3(256), 0, stream, D, colsum, 1.0 / (double)count, k, zscore,
+                     base, dp);
   return (int)hipGetLastError();
 }

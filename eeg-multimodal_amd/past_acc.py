@@ -62,6 +62,22 @@ class ConcatModel(PriGumbelModel):
         super().__init__(float(epsilon), contract="T")
 
 
+def feawei_init(model, dataloader, k=1.0, zscore=True, device=None):
+    """feawei DP initialisation (past_acc.py:98-103; past_acc_feawei.py:127-163): a train-mode,
+    hard=False feature pass over `dataloader` (reference 5-tuples), column means of the normalised
+    features, z-score (zscore=True) and DP = cat(0.4, 0.5, 0.3) + 1 - sigmoid(k z) - 0.5.  Runs on
+    the device (eegfusion.feawei); sets and returns model.DP."""
+    from eegfusion.feawei import init_dp_
+    device = device or model.arena.device
+    model.train()
+
+    def batches():
+        for frame_input, vedio_mask, title_input, text_mask, *_ in dataloader:
+            yield model._token_batch(*(t.to(device) for t in (frame_input, vedio_mask, title_input, text_mask)))
+
+    return init_dp_(model, batches(), k=k, zscore=zscore)
+
+
 def main2(epsilon, suffix, batch_size=8, epochs=50, learning_rate=1e-6, feature_dir='feature',
           record_dir='model_dict/eps_experiment/', device=None):
     """past_acc.py:142-250: DP pass (hard=False) -> DP Adam; model pass (hard=True) -> model Adam."""

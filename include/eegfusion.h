@@ -180,6 +180,13 @@ int eegf_cross_entropy(int dtype, int B, int C, const void* logits, const long l
                        int reduction, float dscale, float* loss, int* correct, void* dlogits,
                        hipStream_t stream);
 
+/* feawei DP initialisation (past_acc.py:98-103 with k = 1, zscore = 1; past_acc_feawei.py:153-163
+ * with k = 5, zscore = 0): colsum [D] = column sums over `count` rows of the normalised features
+ * (eegf_colsum with beta = 1 across batches); z = (m - mean m) / std m (population std) or z = m;
+ * dp[c] = base[c] + (1 - sigmoid(k z_c)) - 0.5, base = cat(0.4, 0.5, 0.3 per 768) in the reference. */
+int eegf_feawei_init(int D, const float* colsum, long count, float k, int zscore, const float* base, float* dp,
+                     hipStream_t stream);
+
 /* y = alpha*x + beta*y ; dx = dy*(1-y^2) */
 int eegf_axpby(int dtype, long n, float alpha, const void* x, float beta, void* y, hipStream_t stream);
 int eegf_tanh_bwd(int dtype, long n, const void* dy, const void* y, void* dx, hipStream_t stream);

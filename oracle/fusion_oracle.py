@@ -216,6 +216,24 @@ def head(p, f):
     return _lin(h, p, "classifier")
 
 
+# ------------------------------------------------------------------------- feawei init
+def feawei_dp_init(features, k=1.0, zscore=True, base=(0.4, 0.5, 0.3)):
+    """DP initialisation from a feature pass, numpy as in the reference:
+    features [N, 2304] (the reference vstacks them into a float64 array, past_acc_feawei.py:141-144);
+    mean_values = np.mean(weight, axis=0); z-score with np.std (past_acc.py:100, k = 1) or raw
+    (past_acc_feawei.py:153-163, k = 5); w_init = 1 - F.sigmoid(torch.tensor(k * z, float32));
+    DP = cat(full(0.4), full(0.5), full(0.3)) + w_init - 0.5 (past_acc.py:101-103)."""
+    import numpy as np
+    weight = np.vstack((np.empty((0, features.shape[1])), np.asarray(features)))
+    mean_values = np.mean(weight, axis=0)
+    if zscore:
+        mean_values = (mean_values - np.mean(mean_values)) / np.std(mean_values)
+    w_init = 1 - F.sigmoid(torch.tensor(k * mean_values, dtype=torch.float32))
+    blk = features.shape[1] // len(base)
+    dp0 = torch.cat([torch.full((1, blk), float(b)) for b in base], dim=1)
+    return dp0 + w_init.unsqueeze(0) - 0.5
+
+
 # ---------------------------------------------------------------------------- full path
 def encoders(p, batch, cfg: PathConfig):
     """→ (pooled [B,768], img [B,768], cross [B,768])."""
