@@ -100,6 +100,9 @@ class FusionEngine:
         self.rng_counter = 0
         self.injected = None        # parity hook: dict(noise=..., gumbels=..., row_noise=...)
         self.needs_grad: set[str] | None = None
+        # grad_ready(names): called during the backward, on the host, once the listed parameters'
+        # gradients are final in stream order (the DDP reducer starts their all-reduce there)
+        self.grad_ready = None
         self.probe: dict | None = None   # tag -> [(start_event, end_event)] (bench.py live timing)
         # column sums deferred during a backward pass (bias / LayerNorm gradients): they feed only the
         # optimizer, so one batched launch at the end replaces ~140 pairs of small launches
@@ -595,6 +598,9 @@ class FusionEngine:
         self.wgrad(dpp, mem, "bert.pooler.dense.weight", B, ldx=L * HID)
         self.dgrad(dpp, self.W("bert.pooler.dense.weight"), dmem, B, ldo=L * HID, beta=1.0)
 
+        # decoder / head / pooler / visual weight matrices are final here
+        self._ready(lambda n: not n.startswith(("bert.encoder.", "bert.embeddings.", "eeg_encoder.")))
+
         # ---------------- BERT encoder backward
         dh = dmem
         dfo = self.ws.get("b_dfo", R * HID, self.dt).view(R, HID)
@@ -636,6 +642,7 @@ class FusionEngine:
                 self.dgrad(dqkv, self.Wspan(qn, 3).view(3 * HID, HID), dhn, R, beta=1.0, bias_grad=gb)
             elif gb is not None:
                 self.bgrad(dqkv, bn, R, width=3 * HID, out=gb)
+            self._ready(lambda n, pre=pre: n.startswith(pre))
             dh = dhn
         if lowest > 0:
             return
@@ -655,6 +662,18 @@ class FusionEngine:
         elif self.need(e + "word_embeddings.weight"):
             call("eegf_embed_scatter_add", self.code, R, HID, P(t["ids"]), P(demb),
                  P(self.G(e + "word_embeddings.weight")), _stream())
+
+    def _ready(self, pred):
+        """Report weight matrices matching pred as final.  Vectors (biases, LayerNorm, embeddings,
+        DP) are left out: their column sums are deferred to the end of the backward."""
+        if self.grad_ready is None:
+            return
+        gp = self.graph_params()
+        names = [n for n, (_, shp) in self.a.offsets.items()
+                 if n in gp and self.need(n) and pred(n) and len(shp) == 2 and n != "DP"
+                 and "norm" not in n.lower() and "embeddings" not in n]
+        if names:
+            self.grad_ready(names)
 
     def _lowest_needed_layer(self) -> int:
         if self.needs_grad is None:

@@ -86,20 +86,27 @@ def _init_bert_(bert: nn.Module, std=0.02):
             nn.init.zeros_(m.bias)
 
 
+_LAYER_MATRICES = ("attention.self.query.weight", "attention.self.key.weight", "attention.self.value.weight",
+                   "attention.output.dense.weight", "intermediate.dense.weight", "output.dense.weight")
+
+
 def _qkv_first_order(named):
-    """Order parameters so each layer's Q/K/V weights then Q/K/V biases are adjacent in the arena."""
+    """Arena order: each BERT layer's six weight matrices first and back to back (Q|K|V adjacent, so
+    the fused QKV projection reads one [2304, 768] matrix; the whole block is one contiguous
+    gradient range that the DDP reducer all-reduces as soon as that layer's backward is done),
+    then its Q/K/V biases (adjacent) and the remaining vectors in module order."""
     named = list(named)
+    byname = dict(named)
     out, seen = [], set()
     for n, p in named:
         if n in seen:
             continue
         if n.endswith("attention.self.query.weight"):
-            base = n[: -len("query.weight")]
-            for k in ("query.weight", "key.weight", "value.weight", "query.bias", "key.bias", "value.bias"):
-                out.append((base + k, dict(named)[base + k]))
+            base = n[: -len("attention.self.query.weight")]
+            for k in _LAYER_MATRICES + ("attention.self.query.bias", "attention.self.key.bias",
+                                        "attention.self.value.bias"):
+                out.append((base + k, byname[base + k]))
                 seen.add(base + k)
-        elif ".attention.self." in n:
-            continue
         else:
             out.append((n, p))
             seen.add(n)

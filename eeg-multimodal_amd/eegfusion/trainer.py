@@ -11,7 +11,8 @@ pass 1 runs the encoders forward without saving activations and backpropagates o
 head and the privacy stage; pass 2's DP gradient is likewise dead (DP_optimizer.zero_grad()
 clears it before its next use) and is not computed.  Parameter values after the step are
 identical to the reference loop.  With world_size > 1 the gradients are averaged over ranks with
-RCCL all-reduce on the flat arena grad buffer (one launch per bucket) before each Adam.
+RCCL all-reduce on arena grad ranges before each Adam; pass 2's all-reduces start during the
+backward, one BERT layer at a time (GradReducer).
 """
 from __future__ import annotations
 
@@ -58,11 +59,29 @@ class FlatAdam:
 
 
 class GradReducer:
-    """Average a flat gradient range over ranks: RCCL all_reduce(SUM) in buckets, then scale."""
+    """Average gradients over ranks: RCCL all_reduce(SUM) of arena grad ranges, then scale by 1/N.
+
+    Two uses:
+      * `reducer(g)`: one contiguous range, reduced now in buckets (the 9 KB DP gradient of pass 1);
+      * `begin(arena, names)` / `ready(names)` / `finish(lo, hi)` around a backward: the engine calls
+        `ready` (FusionEngine.grad_ready) as soon as a group of weight gradients is final in stream
+        order — the decoder/head/pooler matrices before the BERT backward starts, then each BERT
+        layer's contiguous six-matrix block (~28 MB) right after that layer — and each group's
+        all_reduce is issued at once (async_op) so RCCL runs it on its own stream while the
+        remaining layers' backward kernels run; `finish` reduces what is left (biases, LayerNorm,
+        embeddings: their column sums are deferred to the end of the backward), makes the compute
+        stream wait for every outstanding collective, and scales the range by 1/N.
+    Only parameters in `names` are reduced: the unused decoder template layer and (contract W) the
+    word embeddings (31 M of 148 M elements) never enter a bucket.  The issue order is the same on
+    every rank (same backward sequence), as RCCL requires.  With world_size 1 nothing is launched,
+    but the ranges are still recorded (`self.log`), so a single-GPU test can check coverage.
+    """
 
     def __init__(self, bucket_elems: int = 32 << 20):
         self.bucket = bucket_elems
         self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+        self.works, self.todo, self.log = [], set(), []
+        self.arena = None
 
     def __call__(self, g: torch.Tensor):
         if self.world == 1:
@@ -70,6 +89,48 @@ class GradReducer:
         for i in range(0, g.numel(), self.bucket):
             dist.all_reduce(g[i: i + self.bucket], op=dist.ReduceOp.SUM)
         g.mul_(1.0 / self.world)
+
+    @staticmethod
+    def ranges(arena, names, align: int = 64) -> list[tuple[int, int]]:
+        """Coalesced [lo, hi) arena ranges covering `names` (gaps of pure alignment padding merge)."""
+        spans = sorted((arena.offsets[n][0], arena.offsets[n][0] + arena._numel(arena.offsets[n][1]))
+                       for n in names)
+        out: list[list[int]] = []
+        for lo, hi in spans:
+            if out and lo - out[-1][1] < align:
+                out[-1][1] = max(out[-1][1], hi)
+            else:
+                out.append([lo, hi])
+        return [(lo, hi) for lo, hi in out]
+
+    def begin(self, arena, names):
+        self.arena, self.todo, self.works, self.log = arena, set(names), [], []
+
+    def ready(self, names):
+        names = [n for n in names if n in self.todo]
+        if not names:
+            return
+        self.todo.difference_update(names)
+        self._launch(self.ranges(self.arena, names))
+
+    def _launch(self, rngs):
+        g = self.arena.grad
+        for lo, hi in rngs:
+            for i in range(lo, hi, self.bucket):
+                j = min(hi, i + self.bucket)
+                self.log.append((i, j))
+                if self.world > 1:
+                    self.works.append(dist.all_reduce(g[i:j], op=dist.ReduceOp.SUM, async_op=True))
+
+    def finish(self, lo: int, hi: int):
+        if self.todo:
+            self._launch(self.ranges(self.arena, self.todo))
+            self.todo = set()
+        for w in self.works:
+            w.wait()                    # compute stream waits for the RCCL stream (no host sync)
+        self.works = []
+        if self.world > 1:
+            self.arena.grad[lo:hi].mul_(1.0 / self.world)
 
 
 class PriGumbelTrainer:
@@ -107,9 +168,14 @@ class PriGumbelTrainer:
         dl = self._ce(logits, labels, 1)
         self.model_opt.zero_grad()
         e.needs_grad = self.model_params
-        e.backward(sv, dl)
+        self.reduce.begin(e.a, self.model_params)
+        e.grad_ready = self.reduce.ready
+        try:
+            e.backward(sv, dl)
+        finally:
+            e.grad_ready = None
         e.needs_grad = None
-        self.reduce(e.a.grad[self.model_opt.lo:self.model_opt.hi])
+        self.reduce.finish(self.model_opt.lo, self.model_opt.hi)
         self.model_opt.step()
         return self.loss, self.correct
 
@@ -134,8 +200,13 @@ class SinglePassTrainer:
              self.loss.data_ptr(), self.correct.data_ptr(), dl.data_ptr(), _s())
         self.opt.zero_grad()
         e.needs_grad = self.params
-        e.backward(sv, dl)
+        self.reduce.begin(e.a, self.params)
+        e.grad_ready = self.reduce.ready
+        try:
+            e.backward(sv, dl)
+        finally:
+            e.grad_ready = None
         e.needs_grad = None
-        self.reduce(e.a.grad)
+        self.reduce.finish(0, e.a.numel)
         self.opt.step()
         return self.loss, self.correct

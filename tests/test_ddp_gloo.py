@@ -48,3 +48,57 @@ def test_grad_reducer_and_sharding_gloo():
     expect = (torch.arange(1000, dtype=torch.float32) * 1.5).tolist()
     assert res[0][0] == expect and res[1][0] == expect
     assert set(res[0][1]).isdisjoint(res[1][1]) and len(res[0][1]) + len(res[1][1]) == 12
+
+
+def _overlap_worker(rank, world, port, q):
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    sys.path[:0] = [str(root / "eeg-multimodal_amd"), str(root)]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from eegfusion.arena import ParamArena
+    from eegfusion.trainer import GradReducer
+    specs = [("l1.w", (40, 8)), ("l1.b", (8,)), ("unused.w", (30, 7)), ("l0.w", (16, 16)), ("l0.b", (5,)),
+             ("DP", (1, 12))]
+    a = ParamArena(specs, "cpu")
+    a.grad.copy_(torch.arange(a.numel, dtype=torch.float32) * (rank + 1))
+    r = GradReducer(bucket_elems=100)
+    lo, hi = a.model_range
+    r.begin(a, ["l1.w", "l1.b", "l0.w", "l0.b"])
+    r.ready(["l1.w"])                    # issued early (async), 4 buckets of <= 100
+    r.ready(["l0.w", "l1.w"])            # l1.w already issued: ignored
+    r.finish(lo, hi)                     # l1.b, l0.b, then wait + 1/N
+    out = {n: a.gview(n).flatten().tolist() for n, _ in specs}
+    q.put((rank, out, r.log))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_overlapped_reducer_gloo():
+    """begin/ready/finish: every named range is averaged exactly once, names outside the set are
+    never reduced (only scaled by 1/N with the range), DP (outside [lo, hi)) is untouched."""
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_overlap_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {r: (out, log) for r, out, log in (q.get(timeout=120) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    from eegfusion.arena import ParamArena
+    specs = [("l1.w", (40, 8)), ("l1.b", (8,)), ("unused.w", (30, 7)), ("l0.w", (16, 16)), ("l0.b", (5,)),
+             ("DP", (1, 12))]
+    a = ParamArena(specs, "cpu")
+    base = torch.arange(a.numel, dtype=torch.float32)
+    for rank in range(world):
+        out, log = res[rank]
+        for n in ("l1.w", "l1.b", "l0.w", "l0.b"):
+            assert out[n] == (a.view(n, base) * 1.5).flatten().tolist(), n
+        assert out["unused.w"] == (a.view("unused.w", base) * (rank + 1) / world).flatten().tolist()
+        assert out["DP"] == (a.view("DP", base) * (rank + 1)).flatten().tolist()
+        assert all(j - i <= 100 for i, j in log)
+        assert log == res[0][1]          # identical issue order on every rank
