@@ -248,7 +248,11 @@ class FusionModel(nn.Module):
             # title_input <- eeg [B,C,T], frame_input <- act [B,1,A]
             return {"eeg": title_input.contiguous().float(), "act": frame_input.reshape(frame_input.shape[0], -1)
                     .contiguous().float()}
-        return {"title_input": title_input.contiguous().long(), "text_mask": text_mask.contiguous().long(),
+        # token ids / mask arrive as [B, L], or [B, 1, L] when a pickle holds [1, L] per sample
+        # (the shape data.py:25's comment names); both mean the same sequence
+        B = title_input.shape[0]
+        return {"title_input": title_input.reshape(B, -1).contiguous().long(),
+                "text_mask": text_mask.reshape(B, -1).contiguous().long(),
                 "frame_input": frame_input.contiguous().float()}
 
     def extra_repr(self):
