@@ -66,6 +66,17 @@ class ParamArena:
         buf = self.master if buf is None else buf
         return buf[off0:off1]
 
+    def ranges(self, names) -> list[tuple[int, int]]:
+        """Coalesced [lo, hi) element ranges covering `names` (gaps of pure alignment padding merge)."""
+        spans = sorted((self.offsets[n][0], self.offsets[n][0] + self._numel(self.offsets[n][1])) for n in names)
+        out: list[list[int]] = []
+        for lo, hi in spans:
+            if out and lo - out[-1][1] < ALIGN:
+                out[-1][1] = max(out[-1][1], hi)
+            else:
+                out.append([lo, hi])
+        return [(lo, hi) for lo, hi in out]
+
     def offset(self, name: str) -> int:
         return self.offsets[name][0]
 

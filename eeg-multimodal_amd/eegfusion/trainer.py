@@ -32,9 +32,15 @@ class FlatAdam:
     """torch.optim.Adam over one contiguous arena range, one fused launch per step (eegf_adam)."""
 
     def __init__(self, engine: FusionEngine, rng: tuple[int, int], lr=1e-6, betas=(0.9, 0.999), eps=1e-8,
-                 weight_decay=0.0, write_shadow=True):
+                 weight_decay=0.0, write_shadow=True, names=None):
         self.e = engine
         self.lo, self.hi = rng
+        # names: the group's parameters that take part in the graph.  torch.optim.Adam skips a
+        # parameter whose .grad is None (never touching its state), so only their coalesced
+        # sub-ranges are stepped: the unused template decoder layer and the contract-W word
+        # embeddings (31 M elements) are not streamed through Adam.
+        self.sub = [(max(lo, self.lo), min(hi, self.hi)) for lo, hi in engine.a.ranges(names)
+                    if lo < self.hi and hi > self.lo] if names is not None else [(self.lo, self.hi)]
         a = engine.a
         n = self.hi - self.lo
         self.m = torch.zeros(n, dtype=torch.float32, device=a.device)
@@ -53,9 +59,11 @@ class FlatAdam:
         if self.write_shadow and self.e.dt == torch.bfloat16:
             self.e._refresh_shadow()
             sh = a.shadow[self.lo:self.hi].data_ptr()
-        call("eegf_adam", self.hi - self.lo, a.master[self.lo:].data_ptr(), a.grad[self.lo:].data_ptr(),
-             self.m.data_ptr(), self.v.data_ptr(), sh, float(self.lr), float(self.betas[0]), float(self.betas[1]),
-             float(self.eps), float(self.wd), self.t, _s())
+        for lo, hi in self.sub:
+            o = lo - self.lo
+            call("eegf_adam", hi - lo, a.master[lo:].data_ptr(), a.grad[lo:].data_ptr(), self.m[o:].data_ptr(),
+                 self.v[o:].data_ptr(), None if sh is None else a.shadow[lo:].data_ptr(), float(self.lr),
+                 float(self.betas[0]), float(self.betas[1]), float(self.eps), float(self.wd), self.t, _s())
 
 
 class GradReducer:
@@ -91,17 +99,8 @@ class GradReducer:
         g.mul_(1.0 / self.world)
 
     @staticmethod
-    def ranges(arena, names, align: int = 64) -> list[tuple[int, int]]:
-        """Coalesced [lo, hi) arena ranges covering `names` (gaps of pure alignment padding merge)."""
-        spans = sorted((arena.offsets[n][0], arena.offsets[n][0] + arena._numel(arena.offsets[n][1]))
-                       for n in names)
-        out: list[list[int]] = []
-        for lo, hi in spans:
-            if out and lo - out[-1][1] < align:
-                out[-1][1] = max(out[-1][1], hi)
-            else:
-                out.append([lo, hi])
-        return [(lo, hi) for lo, hi in out]
+    def ranges(arena, names) -> list[tuple[int, int]]:
+        return arena.ranges(names)
 
     def begin(self, arena, names):
         self.arena, self.todo, self.works, self.log = arena, set(names), [], []
@@ -137,10 +136,10 @@ class PriGumbelTrainer:
     def __init__(self, engine: FusionEngine, lr: float = 1e-6, reducer: GradReducer | None = None):
         self.e = engine
         a = engine.a
-        self.model_opt = FlatAdam(engine, a.model_range, lr=lr)
-        self.dp_opt = FlatAdam(engine, a.dp_range, lr=lr, write_shadow=False)
         gp = engine.graph_params()
         self.model_params = {n for n in gp if n != "DP"}
+        self.model_opt = FlatAdam(engine, a.model_range, lr=lr, names=self.model_params)
+        self.dp_opt = FlatAdam(engine, a.dp_range, lr=lr, write_shadow=False)
         self.reduce = reducer or GradReducer()
         dev = a.device
         self.loss = torch.zeros(2, dtype=torch.float32, device=dev)
@@ -186,8 +185,8 @@ class SinglePassTrainer:
 
     def __init__(self, engine: FusionEngine, lr: float = 1e-6, reducer: GradReducer | None = None):
         self.e = engine
-        self.opt = FlatAdam(engine, (0, engine.a.numel), lr=lr)
         self.params = engine.graph_params()
+        self.opt = FlatAdam(engine, (0, engine.a.numel), lr=lr, names=self.params)
         self.reduce = reducer or GradReducer()
         self.loss = torch.zeros(1, dtype=torch.float32, device=engine.a.device)
         self.correct = torch.zeros(1, dtype=torch.int32, device=engine.a.device)
