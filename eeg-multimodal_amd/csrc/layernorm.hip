@@ -11,12 +11,15 @@
 #include "eegfusion_internal.h"
 #include <algorithm>
 
+int g_ln_rpw = 16;  // max rows per wave of eegf_ln_fwd (eegf_tune key 6); see eegf_ln_fwd
+
 namespace {
 
 template <typename T> struct V4;
 template <> struct V4<float> {
   typedef f32x4 raw;
   static DEV f32x4 load(const float* p) { return *(const f32x4*)p; }
+  static DEV f32x4 cvt(f32x4 v) { return v; }
   static DEV void store(float* p, f32x4 v) { *(f32x4*)p = v; }
 };
 template <> struct V4<bf16> {
@@ -25,6 +28,7 @@ template <> struct V4<bf16> {
     bf16x4 v = *(const bf16x4*)p;
     return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
   }
+  static DEV f32x4 cvt(bf16x4 v) { return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]}; }
   static DEV void store(bf16* p, f32x4 v) {
     bf16x4 o;
     o[0] = (bf16)v[0]; o[1] = (bf16)v[1]; o[2] = (bf16)v[2]; o[3] = (bf16)v[3];
@@ -32,64 +36,113 @@ template <> struct V4<bf16> {
   }
 };
 
+// LayerNorm dropout stream (hidden dropout of BertEmbeddings / BertSelfOutput / BertOutput and the
+// decoder's dropout1-3): the attention-probability stream of common.h (keep_bits8: Philox4x32-7,
+// eight 16-bit draws per call): element e = row*W + col is kept iff halfword (e & 7) of call e >> 3
+// clears thr16.  Lane l holds 4-element group g = l + 64c of chunk c, so lanes 2k, 2k+1 share one
+// call per chunk: a chunk pair (c, c+1) costs one call per lane (even lanes draw chunk c's call,
+// odd lanes chunk c+1's, swapped with one shuffle); an unpaired last chunk costs one call per lane.
+// nib[c] bit j = keep bit of element col + j.  All 64 lanes of the wave must be active.
+template <int NCH>
+DEV void ln_keep(uint64_t seed, uint64_t offset, long row, int lane, float p, uint32_t (&nib)[NCH]) {
+  const uint32_t thr = thr16_of(p);
+  const int odd = lane & 1;
+  const uint64_t rowcall = (uint64_t)row * (NCH * 32);
+#pragma unroll
+  for (int c = 0; c + 1 < NCH; c += 2) {
+    const uint32_t mine = keep_bits8(seed, offset, rowcall + (uint64_t)(((lane & ~1) + 64 * (c + odd)) >> 1), thr);
+    const uint32_t other = __shfl_xor(mine, 1, 64);
+    nib[c] = ((odd ? other : mine) >> (4 * odd)) & 15u;
+    nib[c + 1] = ((odd ? mine : other) >> (4 * odd)) & 15u;
+  }
+  if (NCH & 1) {
+    const int c = NCH - 1;
+    nib[c] = (keep_bits8(seed, offset, rowcall + (uint64_t)(((lane & ~1) + 64 * c) >> 1), thr) >> (4 * odd)) & 15u;
+  }
+}
+
 struct LnFwdArgs {
   const void* x; const void* r; const float* table; const float* table2;
   const float* gamma; const float* beta;
   void* y; void* s; float* mean; float* rstd;
   long rows; int table_period; float eps; float p; int drop_mode; uint64_t seed, offset;
+  int rpw;  // rows per wave (consecutive rows; eegf_tune key 6)
 };
 
+// One wave per row, rpw consecutive rows per wave (eegf_tune key 6); with rpw > 1 the next row's
+// x / r are loaded before the current row is reduced (two rows of loads in flight per wave).
 template <typename T, int NCH>
 __global__ void __launch_bounds__(256) ln_fwd_kernel(LnFwdArgs a) {
+  typedef typename V4<T>::raw R4;
   constexpr int W = NCH * 256;
   const int lane = threadIdx.x & 63;
-  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= a.rows) return;
-  const T* x = (const T*)a.x + row * W;
-  f32x4 v[NCH];
-  float sum = 0.f;
+  const long row0 = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * a.rpw;
+  if (row0 >= a.rows) return;
+  const long rend = row0 + a.rpw < a.rows ? row0 + a.rpw : a.rows;
+  const bool drop = a.drop_mode != 0 && a.p > 0.f;
+  const float dscale = drop ? 1.0f / (1.0f - a.p) : 1.0f;
+  R4 px[NCH], pr[NCH];
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     const int col = (lane + 64 * c) * 4;
-    v[c] = V4<T>::load(x + col);
-    if (a.drop_mode == 1 && a.p > 0.f) {
-      float m[4];
-      drop_mask4(a.seed, a.offset, (uint64_t)(row * W + col) >> 2, a.p, m);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[c][e] *= m[e];
-    }
-    if (a.r) v[c] += V4<T>::load((const T*)a.r + row * W + col);
-    if (a.table) v[c] += *(const f32x4*)(a.table + (row % a.table_period) * W + col);
-    if (a.table2) v[c] += *(const f32x4*)(a.table2 + col);
-    if (a.s) V4<T>::store((T*)a.s + row * W + col, v[c]);
-    sum += v[c][0] + v[c][1] + v[c][2] + v[c][3];
+    px[c] = *(const R4*)((const T*)a.x + row0 * W + col);
+    if (a.r) pr[c] = *(const R4*)((const T*)a.r + row0 * W + col);
   }
-  const float mean = wave_sum(sum) * (1.0f / W);
-  float sq = 0.f;
+  for (long row = row0; row < rend; ++row) {
+    R4 cx[NCH], cr[NCH];
 #pragma unroll
-  for (int c = 0; c < NCH; ++c)
+    for (int c = 0; c < NCH; ++c) { cx[c] = px[c]; cr[c] = pr[c]; }
+    if (row + 1 < rend) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) { const float d = v[c][e] - mean; sq += d * d; }
-  const float rstd = rsqrtf(wave_sum(sq) * (1.0f / W) + a.eps);
-  T* y = (T*)a.y + row * W;
-#pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-    const int col = (lane + 64 * c) * 4;
-    const f32x4 g = *(const f32x4*)(a.gamma + col), b = *(const f32x4*)(a.beta + col);
-    f32x4 o;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) o[e] = (v[c][e] - mean) * rstd * g[e] + b[e];
-    if (a.drop_mode == 2 && a.p > 0.f) {
-      float m[4];
-      drop_mask4(a.seed, a.offset, (uint64_t)(row * W + col) >> 2, a.p, m);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] *= m[e];
+      for (int c = 0; c < NCH; ++c) {
+        const int col = (lane + 64 * c) * 4;
+        px[c] = *(const R4*)((const T*)a.x + (row + 1) * W + col);
+        if (a.r) pr[c] = *(const R4*)((const T*)a.r + (row + 1) * W + col);
+      }
     }
-    V4<T>::store(y + col, o);
-  }
-  if (lane == 0) {
-    if (a.mean) a.mean[row] = mean;
-    if (a.rstd) a.rstd[row] = rstd;
+    f32x4 v[NCH];
+    float sum = 0.f;
+    uint32_t nib[NCH];
+    if (drop) ln_keep<NCH>(a.seed, a.offset, row, lane, a.p, nib);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = (lane + 64 * c) * 4;
+      v[c] = V4<T>::cvt(cx[c]);
+      if (drop && a.drop_mode == 1) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[c][e] *= ((nib[c] >> e) & 1u) ? dscale : 0.f;
+      }
+      if (a.r) v[c] += V4<T>::cvt(cr[c]);
+      if (a.table) v[c] += *(const f32x4*)(a.table + (row % a.table_period) * W + col);
+      if (a.table2) v[c] += *(const f32x4*)(a.table2 + col);
+      if (a.s) V4<T>::store((T*)a.s + row * W + col, v[c]);
+      sum += v[c][0] + v[c][1] + v[c][2] + v[c][3];
+    }
+    const float mean = wave_sum(sum) * (1.0f / W);
+    float sq = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { const float d = v[c][e] - mean; sq += d * d; }
+    const float rstd = rsqrtf(wave_sum(sq) * (1.0f / W) + a.eps);
+    T* y = (T*)a.y + row * W;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = (lane + 64 * c) * 4;
+      const f32x4 g = *(const f32x4*)(a.gamma + col), b = *(const f32x4*)(a.beta + col);
+      f32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (v[c][e] - mean) * rstd * g[e] + b[e];
+      if (drop && a.drop_mode == 2) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] *= ((nib[c] >> e) & 1u) ? dscale : 0.f;
+      }
+      V4<T>::store(y + col, o);
+    }
+    if (lane == 0) {
+      if (a.mean) a.mean[row] = mean;
+      if (a.rstd) a.rstd[row] = rstd;
+    }
   }
 }
 
@@ -118,15 +171,17 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
     const float mean = a.mean[row], rstd = a.rstd[row];
     f32x4 dy[NCH], xh[NCH];
     float s1 = 0.f, s2 = 0.f;
+    uint32_t nib[NCH];
+    const bool drop = a.drop_mode != 0 && a.p > 0.f;
+    const float dscale = drop ? 1.0f / (1.0f - a.p) : 1.0f;
+    if (drop) ln_keep<NCH>(a.seed, a.offset, row, lane, a.p, nib);
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int col = (lane + 64 * c) * 4;
       dy[c] = V4<T>::load((const T*)a.dy + row * W + col);
-      if (a.drop_mode == 2 && a.p > 0.f) {
-        float m[4];
-        drop_mask4(a.seed, a.offset, (uint64_t)(row * W + col) >> 2, a.p, m);
+      if (drop && a.drop_mode == 2) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) dy[c][e] *= m[e];
+        for (int e = 0; e < 4; ++e) dy[c][e] *= ((nib[c] >> e) & 1u) ? dscale : 0.f;
       }
       const f32x4 sv = V4<T>::load((const T*)a.s + row * W + col);
 #pragma unroll
@@ -148,11 +203,9 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) ds[e] = rstd * (dy[c][e] * gam[c][e] - s1 - xh[c][e] * s2);
       if (a.dr) V4<T>::store((T*)a.dr + row * W + col, ds);
-      if (a.drop_mode == 1 && a.p > 0.f) {
-        float m[4];
-        drop_mask4(a.seed, a.offset, (uint64_t)(row * W + col) >> 2, a.p, m);
+      if (drop && a.drop_mode == 1) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) ds[e] *= m[e];
+        for (int e = 0; e < 4; ++e) ds[e] *= ((nib[c] >> e) & 1u) ? dscale : 0.f;
       }
       if (a.dx) V4<T>::store((T*)a.dx + row * W + col, ds);
     }
@@ -258,7 +311,7 @@ int colsum_t(const void* in, long ld, long rows, int width, int period, float* w
 
 template <typename T>
 int ln_fwd_t(int nch, const LnFwdArgs& a, hipStream_t st) {
-  const dim3 grid((unsigned)((a.rows + 3) / 4));
+  const dim3 grid((unsigned)((a.rows + 4L * a.rpw - 1) / (4L * a.rpw)));
   switch (nch) {
     case 1: hipLaunchKernelGGL((ln_fwd_kernel<T, 1>), grid, dim3(256), 0, st, a); break;
     case 2: hipLaunchKernelGGL((ln_fwd_kernel<T, 2>), grid, dim3(256), 0, st, a); break;
@@ -335,7 +388,10 @@ extern "C" int eegf_ln_fwd(int dtype, long rows, int width, const void* x, const
   if (table && table_period <= 0) return EEGF_ERR_ARG;
   if (drop_p < 0.f || drop_p >= 1.f || drop_mode < 0 || drop_mode > 2) return EEGF_ERR_ARG;
   LnFwdArgs a{x, r, table, table2, gamma, beta, y, s_out, mean, rstd, rows, table_period, eps, drop_p, drop_mode,
-              seed, offset};
+              seed, offset, 1};
+  // rows per wave: up to g_ln_rpw while the grid keeps >= 1024 workgroups (4 per CU); measured at
+  // 65536 x 768 bf16 (tools/ln_bench.py): 86 -> 67 us without, 97 -> 88 us with the residual store
+  while (a.rpw * 2 <= g_ln_rpw && rows / (4L * a.rpw * 2) >= 1024) a.rpw *= 2;
   if (dtype == EEGF_F32) return ln_fwd_t<float>(width / 256, a, stream);
   if (dtype == EEGF_BF16) return ln_fwd_t<bf16>(width / 256, a, stream);
   return EEGF_ERR_ARG;

@@ -64,7 +64,9 @@ int eegf_gemm(int dtype, int out_dtype, int a_kcontig, int b_kcontig, int epi,
  *   key 2: L = 256 attention kernels (bit 0 persistent forward (default on), bit 1 persistent backward);
  *   key 3: static s_setprio for waves 4-7 of the 2-phase kernel;
  *   key 4: persistent 8-phase kernel (0 off, default);
- *   key 5: fused column sums on the 4-wave kernel (0 off, default; experimental, not parity-green). */
+ *   key 5: fused column sums on the 4-wave kernel (0 off, default; experimental, not parity-green).
+ *   key 6: maximum rows per wave of eegf_ln_fwd (1..64, default 16; fewer when the grid would drop
+ *          below 1024 workgroups). */
 int eegf_tune(int key, int value);
 /* Rows of the a_colsum partial buffer eegf_gemm_acs writes for this shape (ceil(M/256)), or 0 when
  * the fused column sums are unavailable (needs bf16 in/out, K-contiguous A, M >= 2048, N >= 256,

@@ -30,10 +30,12 @@ def replay(seed: int, R: int, p: float):
         kind = site[0]
         i = site[1] if len(site) > 1 else 0
         off, stream = {
-            "emb": (R + 1, drop_mask), "attn_out": (R + 10 + 3 * i, drop_mask),
-            "ffn_out": (R + 11 + 3 * i, drop_mask), "attn_probs": (R + 12 + 3 * i, attn_mask),
-            "dec_sa": (R + 100 + 8 * i, drop_mask), "dec_ca": (R + 101 + 8 * i, drop_mask),
-            "dec_ff": (R + 102 + 8 * i, drop_mask), "dec_sa_w": (R + 103 + 8 * i, drop_mask),
+            # LayerNorm-fused sites (emb, attn_out, ffn_out, dec_sa/ca/ff) draw from the Philox-7
+            # 16-bit stream shared with the attention probabilities (layernorm.hip ln_keep)
+            "emb": (R + 1, attn_mask), "attn_out": (R + 10 + 3 * i, attn_mask),
+            "ffn_out": (R + 11 + 3 * i, attn_mask), "attn_probs": (R + 12 + 3 * i, attn_mask),
+            "dec_sa": (R + 100 + 8 * i, attn_mask), "dec_ca": (R + 101 + 8 * i, attn_mask),
+            "dec_ff": (R + 102 + 8 * i, attn_mask), "dec_sa_w": (R + 103 + 8 * i, drop_mask),
             "dec_ca_probs": (R + 104 + 8 * i, drop_mask), "dec_ff_inner": (R + 105 + 8 * i, drop_mask),
         }[kind]
         m = stream(seed, off, np.arange(x.numel(), dtype=np.uint64), p)

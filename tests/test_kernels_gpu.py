@@ -5,6 +5,7 @@ bf16 ≤ 3e-2 relative (bf16 storage, fp32 math).
 """
 import math
 
+import numpy as np
 import pytest
 import torch
 import torch.nn.functional as F
@@ -59,6 +60,11 @@ def test_layernorm_fwd_bwd(dt, mode):
     if mode == 1:
         m = ((s.double() - rd) != 0).double() / (1 - p)      # dropped lanes store s == r exactly
         assert abs(1 - (1 - p) * m.mean().item() - p) < 0.02
+        from philox_ref import attn_mask                      # element-exact: the Philox-7 16-bit stream
+        want = torch.from_numpy(attn_mask(123, 7, np.arange(R * W, dtype=np.uint64), p) > 0).view(R, W)
+        got = (m > 0).cpu()
+        # bf16: a kept x*scale below half an ulp of r rounds s back to r and reads as dropped
+        assert torch.equal(got, want) if dt == torch.float32 else not (got & ~want).any()
         v = xd * m + rd
         assert _rel(s, v) < _tol(dt)
     else:
@@ -67,6 +73,9 @@ def test_layernorm_fwd_bwd(dt, mode):
     if mode == 2:
         kept = y.double().abs() > 0
         assert abs(1 - kept.double().mean().item() - p) < 0.02
+        from philox_ref import attn_mask
+        want = torch.from_numpy(attn_mask(123, 7, np.arange(R * W, dtype=np.uint64), p) > 0).view(R, W)
+        assert torch.equal(kept.cpu(), want) if dt == torch.float32 else not (kept.cpu() & ~want).any()
         ref = torch.where(kept, ref / (1 - p), torch.zeros_like(ref))
     assert _rel(y, ref) < _tol(dt)
     # backward vs autograd (mode 0 only: masks already checked)
