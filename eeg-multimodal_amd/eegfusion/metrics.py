@@ -7,7 +7,9 @@ defaults (torchmetrics 1.x: average="macro", top_k=1, multidim_average="global")
 scores from the confusion counts, safe division (0 where a denominator is 0), and the macro mean
 over the classes that occur in preds or target.  Parity unpinned (no torchmetrics to compare).
 
-Everything stays on the device: one bincount of target*C + pred gives the confusion matrix.
+Everything stays on the device: one bincount of target*C + pred gives the confusion matrix.  Under
+torch.distributed (one process per GPU) the confusion counts are all-reduced before
+the scores are formed, so every rank reports the metric of the global evaluation set.
 """
 from __future__ import annotations
 
@@ -21,8 +23,13 @@ def confusion(preds: torch.Tensor, target: torch.Tensor, num_classes: int) -> to
     return torch.bincount(t * num_classes + p, minlength=num_classes * num_classes).view(num_classes, num_classes)
 
 
-def _stat_scores(preds, target, num_classes):
-    cm = confusion(preds, target, num_classes).double()
+def _stat_scores(preds, target, num_classes, sync=True):
+    cm = confusion(preds, target, num_classes)
+    if sync:
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            dist.all_reduce(cm, op=dist.ReduceOp.SUM)
+    cm = cm.double()
     tp = cm.diagonal()
     fp = cm.sum(0) - tp
     fn = cm.sum(1) - tp
@@ -37,12 +44,12 @@ def _sdiv(a, b):
 class _Multiclass:
     name = ""
 
-    def __init__(self, task: str = "multiclass", num_classes: int = 2, average: str = "macro"):
+    def __init__(self, task: str = "multiclass", num_classes: int = 2, average: str = "macro", sync: bool = True):
         if task != "multiclass":
             raise ValueError(f"{self.name}: only task='multiclass' is supported")
         if average not in ("macro", "micro"):
             raise ValueError(f"{self.name}: average must be 'macro' or 'micro'")
-        self.num_classes, self.average = int(num_classes), average
+        self.num_classes, self.average, self.sync = int(num_classes), average, bool(sync)
 
     def cuda(self):                      # torchmetrics modules are moved with .cuda() (train.py:77)
         return self
@@ -54,7 +61,7 @@ class _Multiclass:
         raise NotImplementedError
 
     def __call__(self, preds: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
-        tp, fp, fn, tn = _stat_scores(preds, target, self.num_classes)
+        tp, fp, fn, tn = _stat_scores(preds, target, self.num_classes, self.sync)
         if self.average == "micro":
             return self.score(tp.sum(), fp.sum(), fn.sum(), tn.sum()).float()
         s = self.score(tp, fp, fn, tn)

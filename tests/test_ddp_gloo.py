@@ -102,3 +102,42 @@ def test_overlapped_reducer_gloo():
         assert out["DP"] == (a.view("DP", base) * (rank + 1)).flatten().tolist()
         assert all(j - i <= 100 for i, j in log)
         assert log == res[0][1]          # identical issue order on every rank
+
+
+def _metrics_worker(rank, world, port, q):
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    sys.path[:0] = [str(root / "eeg-multimodal_amd"), str(root)]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from eegfusion.metrics import Accuracy, F1Score
+    preds = [torch.tensor([0, 1, 1, 0]), torch.tensor([1, 1, 0])][rank]
+    target = [torch.tensor([0, 1, 0, 0]), torch.tensor([1, 0, 0])][rank]
+    q.put((rank, float(Accuracy(num_classes=2)(preds, target)), float(F1Score(num_classes=2)(preds, target)),
+           float(Accuracy(num_classes=2, sync=False)(preds, target))))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_metrics_allreduce_confusion_gloo():
+    """Eval metrics under DDP: confusion counts are summed over ranks, so both ranks report the
+    metric of the union of their shards."""
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_metrics_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {r: rest for r, *rest in (q.get(timeout=120) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    from eegfusion.metrics import Accuracy, F1Score
+    P = torch.tensor([0, 1, 1, 0, 1, 1, 0])
+    T = torch.tensor([0, 1, 0, 0, 1, 0, 0])
+    acc, f1 = float(Accuracy(num_classes=2)(P, T)), float(F1Score(num_classes=2)(P, T))
+    for r in range(world):
+        assert abs(res[r][0] - acc) < 1e-12 and abs(res[r][1] - f1) < 1e-12
+    assert abs(res[0][2] - (2 / 3 + 1) / 2) < 1e-6         # sync=False: the rank's own shard (float32)
