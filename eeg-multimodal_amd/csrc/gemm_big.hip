@@ -1337,6 +1337,7 @@ extern "C" int eegf_tune(int key, int value) {
   if (key == 3) { const int o = g_big_prio; g_big_prio = value; return o; }
   if (key == 4) { const int o = g_gemm8p; g_gemm8p = value; return o; }
   if (key == 5) { const int o = g_gemm4w_cs; g_gemm4w_cs = value; return o; }
+  if (key == 7) { const int o = g_ln_bwd_rpb; if (value < 4 || value > 1024 || value % 4) return EEGF_ERR_ARG; g_ln_bwd_rpb = value; return o; }
   if (key == 6) { const int o = g_ln_rpw; if (value < 1 || value > 64) return EEGF_ERR_ARG; g_ln_rpw = value; return o; }
   return EEGF_ERR_ARG;
 }

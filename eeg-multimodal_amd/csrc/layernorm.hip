@@ -11,6 +11,7 @@
 #include "eegfusion_internal.h"
 #include <algorithm>
 
+int g_ln_bwd_rpb = 64;  // rows per workgroup of eegf_ln_bwd for rows >= 65536 (eegf_tune key 7)
 int g_ln_rpw = 16;  // max rows per wave of eegf_ln_fwd (eegf_tune key 6); see eegf_ln_fwd
 
 namespace {
@@ -398,8 +399,8 @@ extern "C" int eegf_ln_fwd(int dtype, long rows, int width, const void* x, const
 }
 
 extern "C" long eegf_ln_bwd_partial_rows(long rows) {
-  (void)rows;
-  return 64;  // rows per block of eegf_ln_bwd: partial buffers hold ceil(rows/64) x width floats
+  // rows per block of eegf_ln_bwd: partial buffers hold ceil(rows / this) x width floats
+  return rows >= 65536 ? g_ln_bwd_rpb : 64;
 }
 
 extern "C" int eegf_ln_bwd(int dtype, long rows, int width, const void* dy, const void* s, const float* mean,
@@ -408,7 +409,8 @@ extern "C" int eegf_ln_bwd(int dtype, long rows, int width, const void* dy, cons
                            float* dgamma_part, float* dbeta_part, hipStream_t stream) {
   if (rows <= 0 || width % 256 != 0 || width > 1024 || !dy || !s || !mean || !rstd || !gamma) return EEGF_ERR_ARG;
   if (drop_p < 0.f || drop_p >= 1.f || drop_mode < 0 || drop_mode > 2) return EEGF_ERR_ARG;
-  LnBwdArgs a{dy, s, mean, rstd, gamma, dx, dr, dgamma_part, dbeta_part, rows, 64, drop_p, drop_mode, seed, offset};
+  LnBwdArgs a{dy, s, mean, rstd, gamma, dx, dr, dgamma_part, dbeta_part, rows,
+              (int)eegf_ln_bwd_partial_rows(rows), drop_p, drop_mode, seed, offset};
   if (dtype == EEGF_F32) return ln_bwd_t<float>(width / 256, a, stream);
   if (dtype == EEGF_BF16) return ln_bwd_t<bf16>(width / 256, a, stream);
   return EEGF_ERR_ARG;

@@ -266,7 +266,8 @@ class FusionEngine:
              P(s), P(mean), P(rstd), _stream())
 
     def ln_bwd(self, dy, s, mean, rstd, pre, rows, dx, dr, p=0.0, mode=0, rng=0):
-        nb = (rows + 63) // 64
+        rpb = _lib.lib().eegf_ln_bwd_partial_rows(rows)
+        nb = (rows + rpb - 1) // rpb
         part = self._part("ln_part", 2 * nb * HID)
         call("eegf_ln_bwd", _code(dy), rows, HID, P(dy), P(s), P(mean), P(rstd), P(self.F(pre + ".weight")), float(p),
              int(mode if p > 0 else 0), self.cfg.seed, rng, P(dx), P(dr), P(part), P(part[nb * HID:]), _stream())

@@ -66,7 +66,8 @@ int eegf_gemm(int dtype, int out_dtype, int a_kcontig, int b_kcontig, int epi,
  *   key 4: persistent 8-phase kernel (0 off, default);
  *   key 5: fused column sums on the 4-wave kernel (0 off, default; experimental, not parity-green).
  *   key 6: maximum rows per wave of eegf_ln_fwd (1..64, default 16; fewer when the grid would drop
- *          below 1024 workgroups). */
+ *          below 1024 workgroups);
+ *   key 7: rows per workgroup of eegf_ln_bwd when rows >= 65536 (multiple of 4, default 64). */
 int eegf_tune(int key, int value);
 /* Rows of the a_colsum partial buffer eegf_gemm_acs writes for this shape (ceil(M/256)), or 0 when
  * the fused column sums are unavailable (needs bf16 in/out, K-contiguous A, M >= 2048, N >= 256,

@@ -32,7 +32,7 @@ def run(save):
 
 
 ref = {}
-for rpw in (1, 2, 4, 8, 16):
+for rpw in (1, 4, 16, 32):
     _lib.lib().eegf_tune(6, rpw)
     for save in (False, True):
         for _ in range(3):
@@ -53,3 +53,34 @@ for rpw in (1, 2, 4, 8, 16):
             not save or torch.equal(out[1], ref[save][1]))
         print(f"rpw {rpw:2d} save {int(save)}: {us:7.1f} us  {nbytes / us / 1e3:6.0f} GB/s  same={same}", flush=True)
 _lib.lib().eegf_tune(6, 16)
+
+# backward: rows per workgroup (eegf_tune key 7); partial buffers sized by eegf_ln_bwd_partial_rows
+dy = torch.randn(R, W, device=dev, generator=g).bfloat16()
+dx = torch.empty_like(y)
+dr = torch.empty_like(y)
+run(True)
+refb = None
+for rpb in (64, 128, 256, 32):
+    _lib.lib().eegf_tune(7, rpb)
+    nb = -(-R // _lib.lib().eegf_ln_bwd_partial_rows(R))
+    part = torch.empty(2, nb, W, device=dev)
+
+    def runb():
+        call("eegf_ln_bwd", BF16, R, W, dy.data_ptr(), s.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+             gam.data_ptr(), 0.1, 1, 7, 11, dx.data_ptr(), dr.data_ptr(), part[0].data_ptr(), part[1].data_ptr(),
+             st.cuda_stream)
+    for _ in range(3):
+        runb()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(50):
+        runb()
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1000 / 50
+    dg = part[0].double().sum(0)
+    out = (dx.clone(), dr.clone(), dg)
+    refb = refb or out
+    same = torch.equal(out[0], refb[0]) and torch.equal(out[1], refb[1]) and float((dg - refb[2]).abs().max()) < 1e-3
+    print(f"bwd rpb {rpb:3d}: {us:7.1f} us  {R * W * 2 * 4 / us / 1e3:6.0f} GB/s  same={same}", flush=True)
+_lib.lib().eegf_tune(7, 64)
