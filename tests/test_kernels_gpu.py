@@ -302,7 +302,7 @@ def test_dropout_grouped(dt, group):
 
 @pytest.mark.parametrize("dt", DT)
 @pytest.mark.parametrize("hard", [False, True])
-@pytest.mark.parametrize("eps", [0.1, 1.0, 10.0])
+@pytest.mark.parametrize("eps", [0.1, 1.0, 3.0, 5.0, 10.0])      # BASELINE configs[4] sweep
 def test_fusion_prigumbel_injected(dt, hard, eps):
     """Fusion kernel vs the oracle gate on injected draws (fp64 autograd of the same formulas)."""
     import sys
