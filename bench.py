@@ -6,28 +6,35 @@ synthetic 64-channel x 256-step EEG windows + 32-d action vectors, contract W): 
 full PriGumbel iteration of past_acc.py:194-212 — pass 1 (hard=False) forward + DP-gradient
 backward + DP Adam, pass 2 (hard=True) forward + full backward + model Adam — all in
 libeegfusion.so HIP kernels, gradients averaged over ranks with RCCL all-reduce when N > 1.
-Per-GPU batch is fixed as N grows (weak scaling).  `--variant priconcat` times the single-pass
-PriConcat step (configs[1]) instead.
+Per-GPU batch is fixed as N grows (weak scaling).
 
-Run: python bench.py [--gpus N --steps K --warmup W]   (N > 1 under torch.distributed.run)
+Modes:
+  (default)              configs[2] (N = 1) / configs[3] (N = 8): PriGumbel, B = 256 per GPU
+  --variant priconcat    configs[1]: the single-pass PriConcat step
+  --eps-sweep 0.1,1,3,5,10 --feawei 2048 --batch 512
+                         configs[4]: a feawei feature pass (forward-only over N synthetic samples,
+                         DP initialised on the device, past_acc_feawei.py:127-163), then K timed
+                         iterations per eps of the sweep (fresh optimizer state per eps, as each
+                         past_acc.py:254-260 run starts one); value = all timed samples / all timed time
+
+Multi-GPU: one process per GPU over RCCL.  Under torch.distributed.run the world size comes from
+WORLD_SIZE and must equal --gpus (else exit 2).  `python bench.py --gpus N` without a launcher starts
+N fresh rank processes through torch.distributed.run itself (before any GPU call) and exits with
+their status.  The JSON line reports the world size the process group saw.
+
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
 import argparse
 import json
-import math
 import os
+import subprocess
 import sys
 import time
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent
-sys.path.insert(0, str(ROOT / "eeg-multimodal_amd"))
-sys.path.insert(0, str(ROOT))
-
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
 
 HID, L, C, A = 768, 256, 64, 32
 F_PER_SAMPLE = 46.03e9            # forward GEMM+attention FLOPs per sample, contract W (SURVEY §8(d))
@@ -35,21 +42,65 @@ PEAK_BF16 = 2500.0                # TFLOP/s dense bf16 MFMA (MI355X_MICROARCH.md
 METRIC = "samples/sec at batch 256, 64ch×256 EEG + 32-d action, 1/2/4/8 GPUs"
 
 
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--variant", default="prigumbel", choices=["prigumbel", "priconcat"])
+    ap.add_argument("--eps", type=float, default=1.0)
+    ap.add_argument("--eps-sweep", default="", help="comma-separated eps values (configs[4]: 0.1,1,3,5,10)")
+    ap.add_argument("--eps-mode", default="newfrac", choices=["newfrac", "new"])
+    ap.add_argument("--feawei", type=int, default=0, help="feawei feature pass over this many synthetic samples")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-batch", type=int, default=16)
+    ap.add_argument("--cpu-iters", type=int, default=3)
+    ap.add_argument("--master-port", type=int, default=29531)
+    ap.add_argument("--selftest", action="store_true",
+                    help="launcher / process-group check only (gloo, CPU): rank 0 prints the world size")
+    return ap.parse_args(argv)
+
+
+def launch_ranks(args) -> int:
+    """`--gpus N` outside a launcher: N fresh rank processes (torch.distributed.run, 127.0.0.1),
+    started before this process touches the GPU; returns their exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={args.master_port}", str(Path(__file__).resolve()),
+           *sys.argv[1:]]
+    return subprocess.call(cmd, env={**os.environ, "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
+
+
 def flops_per_sample(variant: str) -> float:
     # PriGumbel iteration = pass-1 fwd + pass-2 fwd+bwd = 4F; PriConcat step = fwd+bwd = 3F
     return (4.0 if variant == "prigumbel" else 3.0) * F_PER_SAMPLE
 
 
-def cpu_baseline(variant: str, batch: int = 2, iters: int = 3) -> dict:
-    """The CPU oracle (torch fp32 restatement, oracle/fusion_oracle.py) timed on the host cores on a
-    bounded sample of the same iteration."""
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(variant: str, batch: int, iters: int) -> dict:
+    """The CPU oracle (torch fp32 restatement, oracle/fusion_oracle.py; pinned against the reference's
+    own outputs by tests/test_oracle_golden.py) timed on the host cores on a bounded sample of the
+    same iteration.  Threads = the CPUs this process may run on (sched_getaffinity), capped by
+    OMP_NUM_THREADS (the GPU box's CPU share)."""
+    import torch
     from oracle import fusion_oracle as O
-    threads = torch.get_num_threads()
+    avail = len(os.sched_getaffinity(0))
+    threads = min(avail, int(os.environ.get("OMP_NUM_THREADS", avail)) or avail)
+    torch.set_num_threads(threads)
     g = torch.Generator().manual_seed(0)
     shapes = O.param_shapes("W", "prigumbel" if variant == "prigumbel" else "priconcat")
     p = {}
     for k, s in shapes.items():
-        if "LayerNorm.weight" in k or ".norm" in k and k.endswith("weight"):
+        if ("LayerNorm" in k or ".norm" in k) and k.endswith("weight"):
             t = torch.ones(s)
         elif len(s) >= 2:
             t = torch.randn(s, generator=g) * 0.02
@@ -58,7 +109,7 @@ def cpu_baseline(variant: str, batch: int = 2, iters: int = 3) -> dict:
         p[k] = t.requires_grad_()
     eeg = torch.randn(batch, C, L, generator=g)
     act = torch.randn(batch, A, generator=g) * 0.5
-    labels = torch.randint(0, 2, (batch,), generator=g)
+    labels = (torch.rand(batch, generator=g) < 0.66).long()
     batch_d = dict(eeg=eeg, act=act)
     model_p = [v for k, v in p.items() if k != "DP"]
     mopt = torch.optim.Adam(model_p, lr=1e-6)
@@ -97,53 +148,89 @@ def cpu_baseline(variant: str, batch: int = 2, iters: int = 3) -> dict:
         iteration()
     dt = time.perf_counter() - t0
     return {"value": round(batch * iters / dt, 4), "unit": "samples/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(), "cpus_available": avail,
             "sample": f"oracle/fusion_oracle.py {variant} iteration (torch CPU fp32, dropout 0), batch {batch}, "
-                      f"64x256 EEG + 32-d action, {iters} timed iterations after 1 warm-up, {dt:.1f} s"}
+                      f"64x256 EEG + 32-d action, {iters} timed iterations after 1 warm-up, {dt:.1f} s; "
+                      f"batch {batch} not 256: one B=256 iteration takes ~45 s on 16 cores, too long for the "
+                      f"default run's few-minute budget (BASELINE.md §3)"}
 
 
-def load_traffic(tag: str):
-    f = ROOT / "profiles" / "traffic.json"
+def load_profile_json(name: str, tag: str):
+    f = ROOT / "profiles" / name
     if not f.exists():
         return None
     try:
-        d = json.loads(f.read_text())
-        return d.get(tag, {}).get("hbm_bytes_per_launch")
+        return json.loads(f.read_text()).get(tag)
     except Exception:
         return None
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
-    ap.add_argument("--variant", default="prigumbel", choices=["prigumbel", "priconcat"])
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-batch", type=int, default=8)
-    ap.add_argument("--cpu-iters", type=int, default=4)
-    args = ap.parse_args()
+def probe_stats(probe: dict) -> dict:
+    out = {}
+    for tag, v in probe.items():
+        if not v:
+            continue
+        ms = [s.elapsed_time(e) for s, e, _ in v]
+        fl = sum(f for _, _, f in v)
+        out[tag] = {"launches": len(v), "avg_ms": sum(ms) / len(ms), "tflops": fl / (sum(ms) * 1e-3) / 1e12,
+                    "flops_per_launch": fl / len(v)}
+    return out
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+
+def main():
+    args = parse_args()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    world_env = int(env_world or "1")
+    if world_env != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}; refusing to report a mismatched run",
+              file=sys.stderr)
+        sys.exit(2)
+
+    sys.path.insert(0, str(ROOT / "eeg-multimodal_amd"))
+    sys.path.insert(0, str(ROOT))
+    import torch
+    import torch.distributed as dist
+
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    world, backend = 1, None
+    if args.selftest:
+        if world_env > 1:
+            dist.init_process_group("gloo")
+        w = dist.get_world_size() if world_env > 1 else 1
+        t = torch.ones(1)
+        if w > 1:
+            dist.all_reduce(t)
+        if rank == 0:
+            print(json.dumps({"selftest": True, "world_size": w, "allreduce": float(t.item()),
+                              "backend": dist.get_backend() if w > 1 else None}), flush=True)
+        if w > 1:
+            dist.destroy_process_group()
+        return
+    if world_env > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        world, backend = dist.get_world_size(), dist.get_backend()
+        if world != args.gpus:
+            print(f"bench.py: process group has {world} ranks, --gpus {args.gpus}", file=sys.stderr)
+            sys.exit(2)
     dev = torch.device("cuda", local)
 
     from eegfusion.modules import PriConcatModel, PriGumbelModel
     from eegfusion.trainer import GradReducer, PriGumbelTrainer, SinglePassTrainer
 
+    sweep = [float(x) for x in args.eps_sweep.split(",") if x.strip()] or [args.eps]
     torch.manual_seed(980616)                              # identical init on every rank
     if args.variant == "prigumbel":
-        model = PriGumbelModel(1.0, contract="W", eps_mode="newfrac", dropout=0.1, seed=980616 + rank)
+        model = PriGumbelModel(sweep[0], contract="W", eps_mode=args.eps_mode, dropout=0.1, seed=980616 + rank)
     else:
         model = PriConcatModel(None, contract="W", dropout=0.1, seed=980616 + rank)
     model = model.to(dev).set_compute_dtype(torch.bfloat16)
     eng = model.engine
     reducer = GradReducer()
-    trainer = (PriGumbelTrainer if args.variant == "prigumbel" else SinglePassTrainer)(eng, lr=1e-6, reducer=reducer)
+    trainer_cls = PriGumbelTrainer if args.variant == "prigumbel" else SinglePassTrainer
 
     B = args.batch
     g = torch.Generator(device=dev).manual_seed(980616 + 7919 * rank)   # disjoint synthetic shard per rank
@@ -152,52 +239,104 @@ def main():
     labels = (torch.rand(B, generator=g, device=dev) < 0.66).long()
     batch = {"eeg": eeg, "act": act}
 
-    for _ in range(args.warmup):
-        trainer.step(batch, labels)
-    tags = ("ffn1_fwd", "qkv_fwd", "ffn2_fwd", "attn_fwd")
-    eng.probe = {t: [] for t in tags}
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        loss, _ = trainer.step(batch, labels)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = t.item()
-    probe, eng.probe = eng.probe, None
-    kms = {t: sum(s.elapsed_time(e) for s, e in v) / max(len(v), 1) for t, v in probe.items()}
+    feawei = None
+    if args.feawei > 0 and args.variant == "prigumbel":
+        from eegfusion.feawei import FeatureMean
+        # forward-only pass (train mode, hard=False) over this rank's shard of args.feawei samples,
+        # column sums all-reduced so every rank initialises the same DP
+        per_rank = (args.feawei + world - 1) // world
+        acc = FeatureMean(dev)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with torch.no_grad():
+            for i in range(0, per_rank, B):
+                nb = min(B, per_rank - i)
+                fb = {"eeg": torch.randn(nb, C, L, generator=g, device=dev),
+                      "act": torch.randn(nb, A, generator=g, device=dev) * 0.5}
+                _, sv = eng.forward(fb, False, True, save=False)
+                acc.add(sv.t["fuse"]["xn"])
+            if world > 1:
+                dist.all_reduce(acc.sum)
+                acc.count *= world
+            dp0 = acc.dp_init(k=1.0, zscore=True)
+        torch.cuda.synchronize()
+        feawei = {"samples": acc.count, "seconds": round(time.perf_counter() - t0, 3), "k": 1.0, "zscore": True}
+
+    tags = ("ffn1_fwd", "qkv_fwd", "ffn2_fwd", "attn_fwd", "attn_bwd", "dgrad_cs", "dgrad_ffn2")
+    total_dt, per_eps, loss = 0.0, [], None
+    probe_all = {t: [] for t in tags}
+    for eps in sweep:
+        eng.cfg.eps = eps
+        model.eps = torch.tensor(eps)
+        if feawei is not None:
+            model.DP.data.copy_(dp0)
+        trainer = trainer_cls(eng, lr=1e-6, reducer=reducer)      # fresh Adam state per run
+        for _ in range(args.warmup):
+            trainer.step(batch, labels)
+        eng.probe = {t: [] for t in tags}
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            loss, _ = trainer.step(batch, labels)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([dt], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = t.item()
+        for t in tags:
+            probe_all[t] += eng.probe[t]
+        eng.probe = None
+        total_dt += dt
+        per_eps.append({"eps": eps, "samples_per_s": round(world * B * args.steps / dt, 2),
+                        "ms_per_step": round(dt / args.steps * 1e3, 3), "loss": float(loss[-1].item())})
 
     if rank == 0:
-        value = world * B * args.steps / dt
-        R = B * L
-        ffn1_flops = 2.0 * R * 3072 * 768                 # algorithmic FLOPs per FFN1 launch
-        ach = ffn1_flops / (kms["ffn1_fwd"] * 1e-3) / 1e12
+        steps = args.steps * len(sweep)
+        value = world * B * steps / total_dt
+        ks = probe_stats(probe_all)
         step_tf = value / world * flops_per_sample(args.variant) / 1e12
+        dom = ks.get("dgrad_cs")
+        pmc = load_profile_json("pmc_r2.json", "dgrad_cs") or {}
+        roofline = {"kernel": "dgrad_cs: BERT input-gradient GEMMs with fused bias-gradient column sums "
+                              "(QKV K=2304, out-proj K=768, FFN-in K=3072; gemm8 CS, 36 launches per step, "
+                              "the largest kernel group by time in profiles/r1s11_kernel_stats.md)",
+                    "bound": "mfma", "achieved": round(dom["tflops"], 1) if dom else None, "peak": PEAK_BF16,
+                    "unit": "TFLOP/s", "frac": round(dom["tflops"] / PEAK_BF16, 4) if dom else None,
+                    "traffic": pmc.get("hbm_bytes_per_launch"), "mfma_busy": pmc.get("mfma_busy"),
+                    "avg_ms": round(dom["avg_ms"], 4) if dom else None,
+                    "flops_per_launch": dom["flops_per_launch"] if dom else None}
+        f1 = ks.get("ffn1_fwd")
+        ffn1 = load_profile_json("traffic.json", "ffn1_fwd") or {}
         out = {
-            "metric": METRIC, "value": round(value, 2), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+            "metric": METRIC, "value": round(value, 2), "unit": "samples/s", "n_gpus": world, "steps": steps,
+            "warmup": args.warmup, "ms_per_step": round(total_dt / steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
-            "config": {"workload": ("PriGumbel eps=1.0 newfrac iteration (past_acc.py:194-212): pass-1 fwd + DP "
-                                    "Adam, pass-2 fwd/bwd + model Adam" if args.variant == "prigumbel" else
+            "config": {"workload": ("PriGumbel eps=%s %s iteration (past_acc.py:194-212): pass-1 fwd + DP Adam, "
+                                    "pass-2 fwd/bwd + model Adam" % (",".join(map(str, sweep)), args.eps_mode)
+                                    if args.variant == "prigumbel" else
                                     "PriConcat eps=1.0 step (main_0430.py): fwd/bwd + Adam"),
                        "global_batch": world * B, "per_gpu_batch": B, "seq_len": L, "eeg": f"{C}ch x {L}",
                        "action_dim": A, "encoder": "BERT-base 12x768 over per-step Linear(64,768) tokens",
-                       "parallelism": f"dp{world}"},
-            "roofline": {"kernel": "ffn1_fwd (BertIntermediate GEMM 65536x3072x768 + bias + GELU)", "bound": "mfma",
-                         "achieved": round(ach, 1), "peak": PEAK_BF16, "unit": "TFLOP/s",
-                         "frac": round(ach / PEAK_BF16, 4), "traffic": load_traffic("ffn1_fwd"),
-                         "avg_ms": round(kms["ffn1_fwd"], 4)},
+                       "parallelism": f"dp{world}", "process_group": {"world_size": world, "backend": backend}},
+            "roofline": roofline,
+            "roofline_ffn1": ({"kernel": "ffn1_fwd (BertIntermediate GEMM + bias + GELU)", "bound": "mfma",
+                               "achieved": round(f1["tflops"], 1), "peak": PEAK_BF16, "unit": "TFLOP/s",
+                               "frac": round(f1["tflops"] / PEAK_BF16, 4), "avg_ms": round(f1["avg_ms"], 4),
+                               "traffic": ffn1.get("hbm_bytes_per_launch")} if f1 else None),
             "step_roofline": {"achieved": round(step_tf, 1), "unit": "TFLOP/s", "frac": round(step_tf / PEAK_BF16, 4),
                               "flops_per_sample": flops_per_sample(args.variant)},
-            "kernel_ms": {k: round(v, 4) for k, v in kms.items()},
+            "kernels": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
+                        for k, v in ks.items()},
             "loss": float(loss[-1].item()),
         }
+        if len(sweep) > 1 or feawei is not None:
+            out["sweep"] = per_eps
+            out["feawei"] = feawei
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.variant, args.cpu_batch, args.cpu_iters)
         print(json.dumps(out), flush=True)

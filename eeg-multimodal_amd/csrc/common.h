@@ -173,6 +173,9 @@ DEV float wave_min(float v) {
   for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
   return v;
 }
+// torch.relu: NaN propagates (fmaxf(NaN, 0) would return 0 and hide a NaN row from the forward
+// while the backward's 0 * NaN still poisons the gradients)
+DEV float relu_nan(float v) { return v < 0.f ? 0.f : v; }
 
 // XCD-aware bijective remap of a 1-D block id (blocks b and b+8 share an XCD under the
 // observed round-robin dispatch; this makes consecutive logical tiles share one XCD's L2).

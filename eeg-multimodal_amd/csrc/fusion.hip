@@ -35,6 +35,11 @@ DEV float feat(const FusionArgs& a, int b, int j) {
   return to_f32(((const T*)a.cross)[(long)b * a.ld_cross + j - 2 * D1]);
 }
 
+DEV float gumbel_of(uint32_t word) {
+  const float u = ((float)(word >> 9) + 0.5f) * 0x1p-23f;
+  return -logf(-logf(u));
+}
+
 // laplace(0,1), gumbel_0, gumbel_1 for element (b, j)
 DEV void draws(const FusionArgs& a, int b, int j, float& n, float& g0, float& g1) {
   const long e = (long)b * D3 + j;
@@ -49,11 +54,11 @@ DEV void draws(const FusionArgs& a, int b, int j, float& n, float& g0, float& g1
   // torch Laplace.rsample: u ~ U[finfo.eps - 1, 1), n = -sign(u) log1p(-|u|)   (laplace.py:83-86)
   const float u = (float)(r.x >> 8) * (1.0f / 16777216.0f) * (2.0f - 1.1920929e-7f) + (1.1920929e-7f - 1.0f);
   n = a.noise ? a.noise[e] : -copysignf(1.f, u) * log1pf(-fabsf(u)) * (u == 0.f ? 0.f : 1.f);
-  // gumbel = -log(E), E ~ Exp(1) = -log(U), U in (0,1)
-  const float u0 = ((float)(r.y >> 8) + 0.5f) * (1.0f / 16777216.0f);
-  const float u1 = ((float)(r.z >> 8) + 0.5f) * (1.0f / 16777216.0f);
-  g0 = a.gumbels ? a.gumbels[e] : -__logf(-__logf(u0));
-  g1 = a.gumbels ? a.gumbels[(long)a.B * D3 + e] : -__logf(-__logf(u1));
+  // gumbel = -log(E), E ~ Exp(1) = -log(U).  U = (k + 1/2) 2^-23, k in [0, 2^23), lies strictly
+  // inside (0, 1): its largest value 1 - 2^-24 is an fp32 number (a 24-bit k + 1/2 would round to
+  // 2^24, U = 1, E = 0, g = inf and a NaN softmax).  Accurate logf: the fast log of 1 - 2^-24 is 0.
+  g0 = a.gumbels ? a.gumbels[e] : gumbel_of(r.y);
+  g1 = a.gumbels ? a.gumbels[(long)a.B * D3 + e] : gumbel_of(r.z);
 }
 
 DEV float row_laplace(const FusionArgs& a, int b) {

@@ -246,7 +246,7 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmArgs g) {
             float v = g.alpha * acc[i][j][r];
             if (EPI == EPI_BIAS) v += bias[r];
             else if (EPI == EPI_BIAS_GELU) v = g.aux ? v + bias[r] : gelu_f(v + bias[r]);
-            else if (EPI == EPI_BIAS_RELU) v = fmaxf(v + bias[r], 0.f);
+            else if (EPI == EPI_BIAS_RELU) v = relu_nan(v + bias[r]);
             else if (EPI == EPI_BIAS_TANH) v = tanhf(v + bias[r]);
             else if (EPI == EPI_DGELU) v *= gelu_grad(av[r]);
             else if (EPI == EPI_DRELU) v = av[r] > 0.f ? v * g.epi_scale : 0.f;
@@ -325,7 +325,7 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmArgs g) {
         else if (EPI == EPI_BIAS_GELU) { v += bias[r]; pre[r] = v; v = gelu_f(v); }
         else if (EPI == EPI_BIAS_GELU_D) { float gl; gelu_fg(v + bias[r], gl, pre[r]); v = gl; }
         else if (EPI == EPI_MUL_AUX) v *= av[r];
-        else if (EPI == EPI_BIAS_RELU) v = fmaxf(v + bias[r], 0.f);
+        else if (EPI == EPI_BIAS_RELU) v = relu_nan(v + bias[r]);
         else if (EPI == EPI_BIAS_TANH) v = tanhf(v + bias[r]);
         else if (EPI == EPI_DGELU) v *= gelu_grad(av[r]);
         else if (EPI == EPI_DRELU) v = av[r] > 0.f ? v * g.epi_scale : 0.f;
@@ -366,7 +366,7 @@ __global__ void __launch_bounds__(256) gemm_splitk_reduce(const float* __restric
   if (EPI == EPI_BIAS_GELU) { if (aux) aux[m * ldaux + n] = from_f32<TO>(v); v = gelu_f(v); }
   else if (EPI == EPI_BIAS_GELU_D) { float gl, gd; gelu_fg(v, gl, gd); aux[m * ldaux + n] = from_f32<TO>(gd); v = gl; }
   else if (EPI == EPI_MUL_AUX) v *= to_f32(aux[m * ldaux + n]);
-  else if (EPI == EPI_BIAS_RELU) v = fmaxf(v, 0.f);
+  else if (EPI == EPI_BIAS_RELU) v = relu_nan(v);
   else if (EPI == EPI_BIAS_TANH) v = tanhf(v);
   else if (EPI == EPI_DGELU) v *= gelu_grad(to_f32(aux[m * ldaux + n]));
   else if (EPI == EPI_DRELU) v = to_f32(aux[m * ldaux + n]) > 0.f ? v * epi_scale : 0.f;

@@ -189,7 +189,7 @@ DEV void big_epilogue(const BigArgs& g, f32x4 (&acc)[8][NJ], bf16* lds, int m0, 
         float v = g.alpha * acc[i][j][r];
         if (EPI == EPI_BIAS) v += bias[r];
         else if (EPI == EPI_BIAS_GELU) v = g.aux ? v + bias[r] : v;      // no aux: GELU below (packed)
-        else if (EPI == EPI_BIAS_RELU) v = fmaxf(v + bias[r], 0.f);
+        else if (EPI == EPI_BIAS_RELU) v = relu_nan(v + bias[r]);
         else if (EPI == EPI_BIAS_TANH) v = tanhf(v + bias[r]);
         else if (EPI == EPI_DGELU) v *= gelu_grad(av[r]);
         else if (EPI == EPI_DRELU) v = av[r] > 0.f ? v * g.epi_scale : 0.f;
@@ -681,7 +681,7 @@ DEV void direct_epilogue_body(const BigArgs& g, f32x4 (&acc)[8][4], const float*
           float v = g.alpha * acc[i][j][r];
           const float a = load_in ? (float)av[i][j][r] : 0.f;
           if (HAS_BIAS) v += bias[j][r];
-          if (EPI == EPI_BIAS_RELU) v = fmaxf(v, 0.f);
+          if (EPI == EPI_BIAS_RELU) v = relu_nan(v);
           else if (EPI == EPI_BIAS_TANH) v = tanhf(v);
           else if (EPI == EPI_DGELU) v *= gelu_grad(a);
           else if (EPI == EPI_DRELU) v = a > 0.f ? v * g.epi_scale : 0.f;

@@ -34,6 +34,7 @@ from .arena import ParamArena
 HID, NH, DH, FFN, NL = 768, 12, 64, 3072, 12
 DEC_FF, DEC_L = 2048, 3
 FUSED = 3 * HID
+EPS_MODES = ("newfrac", "new")    # past_acc.py:132 1/ln((e^eps-w)/(1-w)) | model.py:57 ln(...)
 SPLITK_WS = 24 << 20          # fp32 elements of split-K slab workspace (96 MB)
 VARIANTS = {"concat": _lib.FUSE_CONCAT, "priconcat": _lib.FUSE_PRICONCAT,
             "priconcat_lap": _lib.FUSE_PRICONCAT_LAP, "prigumbel": _lib.FUSE_PRIGUMBEL}
@@ -95,6 +96,10 @@ class FusionEngine:
         self.cfg = cfg
         self.dt = cfg.dtype
         self.code = F32 if cfg.dtype == torch.float32 else BF16
+        if cfg.variant not in VARIANTS:
+            raise ValueError(f"eegfusion: unknown variant {cfg.variant!r} (one of {sorted(VARIANTS)})")
+        if cfg.eps_mode not in EPS_MODES:
+            raise ValueError(f"eegfusion: eps_mode must be one of {EPS_MODES}, got {cfg.eps_mode!r}")
         self.variant = VARIANTS[cfg.variant]
         self.ws = Workspace(arena.device)
         self.rng_counter = 0
@@ -163,7 +168,7 @@ class FusionEngine:
         ev = self._ev_start(tag)
         self.gemm(x, w, out, M, N, K, 1, 1, lda or K, K, out.shape[-1], epi=epi, bias=b, aux=aux,
                   ldaux=(aux.shape[-1] if aux is not None else 0))
-        self._ev_end(tag, ev)
+        self._ev_end(tag, ev, 2.0 * M * N * K)
         return out
 
     def _ev_start(self, tag):
@@ -173,14 +178,16 @@ class FusionEngine:
         ev.record()
         return ev
 
-    def _ev_end(self, tag, ev):
+    def _ev_end(self, tag, ev, flops=0.0):
+        """probe[tag] gets (start, end, algorithmic FLOPs) of the launch just enqueued: HIP events on
+        the launch stream (torch's current stream, where every eegf_* call is enqueued)"""
         if ev is not None:
             e2 = torch.cuda.Event(enable_timing=True)
             e2.record()
-            self.probe[tag].append((ev, e2))
+            self.probe[tag].append((ev, e2, flops))
 
     def dgrad(self, dy, w, out, M, ldd=None, ldo=None, epi=_lib.EPI_NONE, aux=None, scale=1.0, beta=0.0,
-              bias_grad=None):
+              bias_grad=None, tag=None):
         """out = dy W (* act'(aux)) (+ beta out).  bias_grad: fp32 tensor that receives += dy.sum(0) —
         fused into the GEMM (per-256-row-tile column sums of dy, eegf_gemm_acs) when the shape takes
         the 256x256 path, else a separate column reduction."""
@@ -190,8 +197,10 @@ class FusionEngine:
             tiles = _lib.lib().eegf_gemm_colsum_tiles(_code(dy), _code(out), 1, M, K, N)
             if tiles > 0 and (ldd or N) == N:
                 part = self._part("acs", tiles * N)
+                ev = self._ev_start(tag)
                 call("eegf_gemm_acs", _code(dy), _code(out), 1, 0, epi, M, K, N, P(dy), N, P(w), K, P(out), ldo or K,
                      None, P(aux), ldaux, 1.0, float(beta), float(scale), P(part), _stream())
+                self._ev_end(tag, ev, 2.0 * M * N * K)
                 self.colsum(part, N, tiles, N, bias_grad)
                 return out
             self.colsum(dy, ldd or N, M, N, bias_grad)
@@ -309,6 +318,11 @@ class FusionEngine:
             call("eegf_key_bias", B * L, P(mask), P(kbias), _stream())
             t["ids"] = ids
         sv.B, sv.L = B, L
+        if save and L % 256:
+            # eegf_attn_bwd handles L % 256 == 0 only: refuse before any gradient is written
+            raise ValueError(f"eegfusion: sequence length {L} is not a multiple of 256 (backward unsupported)")
+        if L % 128:
+            raise ValueError(f"eegfusion: sequence length {L} is not a multiple of 128")
         R = B * L
         t["kbias"] = kbias
         e = "bert.embeddings."
@@ -337,7 +351,7 @@ class FusionEngine:
             ev = self._ev_start("attn_fwd")
             call("eegf_attn_fwd", self.code, B, NH, L, P(qkv), 3 * HID, P(kbias), scale, float(adrop), self.cfg.seed,
                  sv.rng + 12 + 3 * i, P(ctx), HID, P(lse), P(bits), _stream())
-            self._ev_end("attn_fwd", ev)
+            self._ev_end("attn_fwd", ev, 4.0 * B * NH * L * L * DH)
             ao = self.ws.get("ao", R * HID, self.dt).view(R, HID)
             self.linear(ctx, self.W(pre + "attention.output.dense.weight"), self.F(pre + "attention.output.dense.bias"),
                         ao, R)
@@ -426,7 +440,17 @@ class FusionEngine:
         t["dec"] = dl
         cross = x
 
-        # ---------------- fusion + privacy stage (fp32)
+        # ---------------- fusion + privacy stage + head (fp32)
+        logits, fh = self.fuse_head_fwd(pooled, vis, cross, hard, sv.rng)
+        t.update(fh)
+        return logits, sv
+
+    def fuse_head_fwd(self, pooled, vis, cross, hard: bool, rng: int):
+        """concat + min-max + privacy stage (one kernel) and the fc head over the three encoder
+        outputs [B, 768] fp32 (model.py:46-63, past_acc.py:119-138, main_0430.py:116-122).
+        Returns logits [B, 2] and the state the backward needs."""
+        cfg = self.cfg
+        B = pooled.shape[0]
         g = self.eh(B, FUSED)
         xn = self._f32(B, FUSED)
         amin = torch.empty(B, dtype=torch.int32, device=self.a.device)
@@ -436,19 +460,16 @@ class FusionEngine:
         eps_a = math.exp(cfg.eps)
         call("eegf_fusion_fwd", F32, B, self.variant, P(pooled), HID, P(vis), HID, P(cross), HID,
              P(self.F("DP")) if "DP" in self.a.offsets else None, P(inj.get("noise")), P(inj.get("gumbels")),
-             P(inj.get("row_noise")), int(hard), 0 if cfg.eps_mode == "newfrac" else 1, eps_a, 1.0 / cfg.eps,
-             self.cfg.seed, sv.rng + 200, P(g), P(xn), P(amin), P(amax), P(rng_), _stream())
-        t["fuse"] = dict(g=g, xn=xn, amin=amin, amax=amax, range=rng_, inj=inj, cross=cross)
-
-        # ---------------- head (fp32)
+             P(inj.get("row_noise")), int(hard), EPS_MODES.index(cfg.eps_mode), eps_a, 1.0 / cfg.eps,
+             self.cfg.seed, rng + 200, P(g), P(xn), P(amin), P(amax), P(rng_), _stream())
         z1 = self.eh(B, FUSED)
         self.linear(g, self.F("fc_layers.0.weight"), self.F("fc_layers.0.bias"), z1, B, epi=_lib.EPI_BIAS_RELU)
         z2 = self.eh(B, HID)
         self.linear(z1, self.F("fc_layers.2.weight"), self.F("fc_layers.2.bias"), z2, B, epi=_lib.EPI_BIAS_TANH)
         logits = self.eh(B, 2)
         self.linear(z2, self.F("classifier.weight"), self.F("classifier.bias"), logits, B)
-        t["head"] = dict(z1=z1, z2=z2)
-        return logits, sv
+        return logits, dict(fuse=dict(g=g, xn=xn, amin=amin, amax=amax, range=rng_, inj=inj),
+                            head=dict(z1=z1, z2=z2))
 
     def _f32(self, *shape):
         return torch.empty(*shape, dtype=torch.float32, device=self.a.device)
@@ -472,36 +493,7 @@ class FusionEngine:
         pdrop = cfg.hidden_dropout if sv.training else 0.0
         adrop = cfg.attn_dropout if sv.training else 0.0
         ddrop = cfg.dec_dropout if sv.training else 0.0
-        dlogits = dlogits.float().contiguous()
-        hd = t["head"]
-        fz = t["fuse"]
-        g = fz["g"]
-
-        # ---------------- head (fp32)
-        self.wgrad(dlogits, hd["z2"], "classifier.weight", B)
-        self.bgrad(dlogits, "classifier.bias", B)
-        dz2 = self.eh(B, HID)
-        self.dgrad(dlogits, self.F("classifier.weight"), dz2, B, epi=_lib.EPI_DTANH, aux=hd["z2"])
-        self.wgrad(dz2, hd["z1"], "fc_layers.2.weight", B)
-        self.bgrad(dz2, "fc_layers.2.bias", B)
-        dz1 = self.eh(B, FUSED)
-        self.dgrad(dz2, self.F("fc_layers.2.weight"), dz1, B, epi=_lib.EPI_DRELU, aux=hd["z1"])
-        self.wgrad(dz1, g, "fc_layers.0.weight", B)
-        self.bgrad(dz1, "fc_layers.0.bias", B)
-        dg = self.eh(B, FUSED)
-        self.dgrad(dz1, self.F("fc_layers.0.weight"), dg, B)
-
-        # ---------------- fusion / privacy stage
-        dpooled, dvis, dcross = self.eh(B, HID), self.eh(B, HID), self.eh(B, HID)
-        has_dp = "DP" in self.a.offsets and self.variant == _lib.FUSE_PRIGUMBEL and self.need("DP")
-        ddp = self._f32(B, FUSED) if has_dp else None
-        inj = fz["inj"]
-        call("eegf_fusion_bwd", F32, B, self.variant, P(dg), P(fz["xn"]), P(fz["amin"]), P(fz["amax"]),
-             P(fz["range"]), P(self.F("DP")) if "DP" in self.a.offsets else None, P(inj.get("noise")),
-             P(inj.get("gumbels")), int(sv.hard), 0 if cfg.eps_mode == "newfrac" else 1, math.exp(cfg.eps),
-             self.cfg.seed, sv.rng + 200, P(dpooled), HID, P(dvis), HID, P(dcross), HID, P(ddp), _stream())
-        if has_dp:
-            self.bgrad(ddp, "DP", B, FUSED)
+        dpooled, dvis, dcross = self.fuse_head_bwd(t, dlogits, sv.hard, sv.rng)
         if head_only:
             return
 
@@ -622,17 +614,19 @@ class FusionEngine:
             self.ln_bwd(dh, *s["ln2"], pre + "output.LayerNorm", R, dfo, da, pdrop, 1, sv.rng + 11 + 3 * i)
             self.wgrad(dfo, s["ffact"], pre + "output.dense.weight", R)
             self.dgrad(dfo, self.W(pre + "output.dense.weight"), dffp, R, epi=_lib.EPI_MUL_AUX, aux=s["ffgd"],
-                       bias_grad=self.gbias(pre + "output.dense.bias"))
+                       bias_grad=self.gbias(pre + "output.dense.bias"), tag="dgrad_ffn2")
             self.wgrad(dffp, s["a1"], pre + "intermediate.dense.weight", R)
             self.dgrad(dffp, self.W(pre + "intermediate.dense.weight"), da, R, beta=1.0,
-                       bias_grad=self.gbias(pre + "intermediate.dense.bias"))
+                       bias_grad=self.gbias(pre + "intermediate.dense.bias"), tag="dgrad_cs")
             self.ln_bwd(da, *s["ln1"], pre + "attention.output.LayerNorm", R, dao, dhn, pdrop, 1, sv.rng + 10 + 3 * i)
             self.wgrad(dao, s["ctx"], pre + "attention.output.dense.weight", R)
             self.dgrad(dao, self.W(pre + "attention.output.dense.weight"), dctx, R,
-                       bias_grad=self.gbias(pre + "attention.output.dense.bias"))
+                       bias_grad=self.gbias(pre + "attention.output.dense.bias"), tag="dgrad_cs")
+            ev = self._ev_start("attn_bwd")
             call("eegf_attn_bwd", self.code, B, NH, L, P(s["qkv"]), 3 * HID, P(t["kbias"]), scale, float(adrop),
                  self.cfg.seed, sv.rng + 12 + 3 * i, P(s["ctx"]), P(dctx), HID, P(s["lse"]), P(s["bits"]), P(dqkv),
                  P(dq_ws), _stream())
+            self._ev_end("attn_bwd", ev, 2.5 * 4.0 * B * NH * L * L * DH)
             qn = pre + "attention.self.query.weight"
             if self.need(qn):
                 gq = self.a.span(qn, 3, self.a.grad).view(3 * HID, HID)
@@ -640,7 +634,7 @@ class FusionEngine:
             bn = pre + "attention.self.query.bias"
             gb = self.a.span(bn, 3, self.a.grad) if self.need(bn) else None
             if i > lowest or lowest == 0:
-                self.dgrad(dqkv, self.Wspan(qn, 3).view(3 * HID, HID), dhn, R, beta=1.0, bias_grad=gb)
+                self.dgrad(dqkv, self.Wspan(qn, 3).view(3 * HID, HID), dhn, R, beta=1.0, bias_grad=gb, tag="dgrad_cs")
             elif gb is not None:
                 self.bgrad(dqkv, bn, R, width=3 * HID, out=gb)
             self._ready(lambda n, pre=pre: n.startswith(pre))
@@ -663,6 +657,39 @@ class FusionEngine:
         elif self.need(e + "word_embeddings.weight"):
             call("eegf_embed_scatter_add", self.code, R, HID, P(t["ids"]), P(demb),
                  P(self.G(e + "word_embeddings.weight")), _stream())
+
+    def fuse_head_bwd(self, t: dict, dlogits: torch.Tensor, hard: bool, rng: int):
+        """Backward of fuse_head_fwd: head weight / bias gradients and the DP gradient (PriGumbel)
+        into the arena; returns dL/d(pooled, vis, cross) [B, 768] fp32."""
+        cfg = self.cfg
+        dlogits = dlogits.float().contiguous()
+        B = dlogits.shape[0]
+        hd = t["head"]
+        fz = t["fuse"]
+        g = fz["g"]
+        self.wgrad(dlogits, hd["z2"], "classifier.weight", B)
+        self.bgrad(dlogits, "classifier.bias", B)
+        dz2 = self.eh(B, HID)
+        self.dgrad(dlogits, self.F("classifier.weight"), dz2, B, epi=_lib.EPI_DTANH, aux=hd["z2"])
+        self.wgrad(dz2, hd["z1"], "fc_layers.2.weight", B)
+        self.bgrad(dz2, "fc_layers.2.bias", B)
+        dz1 = self.eh(B, FUSED)
+        self.dgrad(dz2, self.F("fc_layers.2.weight"), dz1, B, epi=_lib.EPI_DRELU, aux=hd["z1"])
+        self.wgrad(dz1, g, "fc_layers.0.weight", B)
+        self.bgrad(dz1, "fc_layers.0.bias", B)
+        dg = self.eh(B, FUSED)
+        self.dgrad(dz1, self.F("fc_layers.0.weight"), dg, B)
+        dpooled, dvis, dcross = self.eh(B, HID), self.eh(B, HID), self.eh(B, HID)
+        has_dp = "DP" in self.a.offsets and self.variant == _lib.FUSE_PRIGUMBEL and self.need("DP")
+        ddp = self._f32(B, FUSED) if has_dp else None
+        inj = fz["inj"]
+        call("eegf_fusion_bwd", F32, B, self.variant, P(dg), P(fz["xn"]), P(fz["amin"]), P(fz["amax"]),
+             P(fz["range"]), P(self.F("DP")) if "DP" in self.a.offsets else None, P(inj.get("noise")),
+             P(inj.get("gumbels")), int(hard), EPS_MODES.index(cfg.eps_mode), math.exp(cfg.eps),
+             self.cfg.seed, rng + 200, P(dpooled), HID, P(dvis), HID, P(dcross), HID, P(ddp), _stream())
+        if has_dp:
+            self.bgrad(ddp, "DP", B, FUSED)
+        return dpooled, dvis, dcross
 
     def _ready(self, pred):
         """Report weight matrices matching pred as final.  Vectors (biases, LayerNorm, embeddings,

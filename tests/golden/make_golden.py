@@ -329,6 +329,114 @@ def gen_adam_two_optimizer(past_acc):
     save("two_optimizer_step", dict(lr=lr, eps=1.0, seed=SEED, B=B_W, C=C_W, T=T_W, A=A_W, dp="w_values"), out)
 
 
+def gen_adam_three_iters(past_acc):
+    """Three PriGumbel iterations of past_acc.main2's loop body (:194-212) with the reference's two
+    Adam optimizers (lr 1e-6).  After the first Adam step delta/lr is no longer ~-sign(g), so the
+    deltas of iterations 2-3 check the moment estimates; recorded for DP, the head, one BERT layer's
+    Q/K/V/out/FFN matrices (sampled positions) and the decoder's in_proj matrices (sampled)."""
+    torch.manual_seed(40)
+    gen = torch.Generator().manual_seed(41)
+    m = prepare(past_acc.ConcatModel(1.0), "W", w_values_dp())
+    eeg, act = window_inputs(gen)
+    frame, vmask, tmask = act.unsqueeze(1), torch.ones(B_W, 1, dtype=torch.long), torch.ones(B_W, T_W, dtype=torch.long)
+    labels = torch.tensor([[1], [0]])
+    lr = 1e-6
+    DP_params = [p for n, p in m.named_parameters() if "DP" in n]
+    model_params = [p for n, p in m.named_parameters() if "DP" not in n]
+    model_opt, dp_opt = torch.optim.Adam(model_params, lr=lr), torch.optim.Adam(DP_params, lr=lr)
+    before = {canon(n): p.detach().clone() for n, p in m.named_parameters()}
+    out = dict(eeg=eeg, act=act, labels=labels.view(-1))
+    for it in range(3):
+        n1, n2 = laplace_noise(gen, (B_W, 2304)), laplace_noise(gen, (B_W, 2304))
+        dp_opt.zero_grad()
+        m.noiser = InjectedNoise(n1)
+        with RecordExp() as r1:
+            loss1, _, _, _ = past_acc.cal_loss(m(frame, vmask, eeg, tmask, hard=False), labels)
+        loss1.backward()
+        dp_opt.step()
+        model_opt.zero_grad()
+        m.noiser = InjectedNoise(n2)
+        with RecordExp() as r2:
+            loss2, _, _, _ = past_acc.cal_loss(m(frame, vmask, eeg, tmask, hard=True), labels)
+        loss2.backward()
+        model_opt.step()
+        out.update({f"noise1_{it}": n1, f"noise2_{it}": n2, f"gumbels1_{it}": -torch.log(r1.draws[0]),
+                    f"gumbels2_{it}": -torch.log(r2.draws[0]), f"loss1_{it}": loss1.detach(),
+                    f"loss2_{it}": loss2.detach()})
+    full = ("DP", "classifier.weight", "classifier.bias", "fc_layers.2.bias", "bert.pooler.dense.bias",
+            "multi_head_decoder.layers.2.norm3.weight", "bert.encoder.layer.5.attention.self.query.bias",
+            "bert.encoder.layer.5.output.LayerNorm.weight")
+    sampled = tuple(f"bert.encoder.layer.5.{k}" for k in (
+        "attention.self.query.weight", "attention.self.key.weight", "attention.self.value.weight",
+        "attention.output.dense.weight", "intermediate.dense.weight", "output.dense.weight")) + (
+        "multi_head_decoder.layers.0.self_attn.in_proj_weight", "multi_head_decoder.layers.0.multihead_attn.in_proj_weight",
+        "eeg_encoder.weight", "fc_layers.0.weight")
+    for n, p in m.named_parameters():
+        cn = canon(n)
+        d = ((p.detach() - before[cn]) / lr).reshape(-1)
+        if cn in full:
+            out["delta:" + cn] = d
+        elif cn in sampled:
+            pos = sample_positions(cn, d.numel())
+            out["dpos:" + cn] = pos
+            out["dval:" + cn] = d[torch.from_numpy(pos)]
+    save("three_iterations", dict(lr=lr, eps=1.0, seed=SEED, B=B_W, C=C_W, T=T_W, A=A_W, dp="w_values", iters=3), out)
+
+
+def gen_priconcat_lap_full(main_0430):
+    """PriConcat with DP_guarantee('feature_all_lap') honoured (the build's honor_dp_mode=True, SURVEY
+    App. A.2): the reference's ConcatModel.forward (main_0430.py:108-123) with its DP_guarantee call
+    routed to dp_mode='feature_all_lap' (main_0430.py:76-85); the per-row Laplace draw is taken under
+    a fixed seed and recorded by re-drawing under the same seed."""
+    torch.manual_seed(42)
+    gen = torch.Generator().manual_seed(43)
+    args = types.SimpleNamespace(EPSILON=1.0)
+    m = prepare(main_0430.ConcatModel(args, dp_mode="feature_all_lap"), "W")
+    eeg, act = window_inputs(gen)
+    labels = torch.tensor([1, 0])
+    orig = main_0430.DP_guarantee
+
+    def honoured(feature, EPSILON, dp_mode=None):
+        torch.manual_seed(77)
+        return orig(feature, EPSILON, dp_mode="feature_all_lap")
+
+    main_0430.DP_guarantee = honoured
+    try:
+        logits = m(act.unsqueeze(1), torch.ones(B_W, 1, dtype=torch.long), eeg, torch.ones(B_W, T_W, dtype=torch.long))
+    finally:
+        main_0430.DP_guarantee = orig
+    torch.manual_seed(77)
+    row_noise = torch.distributions.laplace.Laplace(torch.tensor([0.0]), torch.tensor([1.0])).sample([B_W]).view(-1)
+    loss = nn.functional.cross_entropy(logits, labels)
+    loss.backward()
+    cfg = dict(contract="W", variant="priconcat_lap", eps=1.0, honor_dp_mode=True, seed=SEED, B=B_W, C=C_W, T=T_W,
+               A=A_W)
+    save("full_priconcat_lap", cfg, dict(eeg=eeg, act=act, labels=labels, row_noise=row_noise, logits=logits.detach(),
+                                         loss=loss.detach(), **grad_record(m)))
+
+
+def gen_feawei_features():
+    """The live feature pass of the feawei initialisation: past_acc_feawei.ConcatModel.forward
+    (:103-124) returns the min-max normalised fused feature; main2 (:127-148) stacks the batches
+    into a float64 matrix whose column mean (:156) feeds the DP init.  Two batches of B=2."""
+    import past_acc_feawei
+    torch.manual_seed(44)
+    gen = torch.Generator().manual_seed(45)
+    m = prepare(past_acc_feawei.ConcatModel(), "W")
+    weight = np.empty((0, 2304))
+    out = {}
+    for i in range(2):
+        eeg, act = window_inputs(gen)
+        with torch.no_grad():
+            feature = m(act.unsqueeze(1), torch.ones(B_W, 1, dtype=torch.long), eeg,
+                        torch.ones(B_W, T_W, dtype=torch.long), hard=False)
+        weight = np.vstack((weight, feature.detach().cpu().numpy()))
+        out[f"eeg{i}"], out[f"act{i}"] = eeg, act
+    out["features"] = weight
+    out["mean_values"] = np.mean(weight, axis=0)
+    save("feawei_features", dict(contract="W", seed=SEED, B=B_W, batches=2, C=C_W, T=T_W, A=A_W), out)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
     past_acc, main_0430, ref_model = import_reference()
@@ -339,3 +447,7 @@ if __name__ == "__main__":
     gen_priconcat_full(main_0430)
     gen_concat_tokens(ref_model)
     gen_adam_two_optimizer(past_acc)
+    # round 2 (appended so the fixtures above are regenerated bit-identically)
+    gen_adam_three_iters(past_acc)
+    gen_priconcat_lap_full(main_0430)
+    gen_feawei_features()

@@ -89,3 +89,75 @@ def test_full_concat_tokens():
     loss.backward()
     assert rel_err(logits.detach(), fx["logits"]) < 2e-5
     check_grads(_grads(p), fx, 1e-4)
+
+
+def test_full_priconcat_lap():
+    """PriConcat with DP_guarantee('feature_all_lap') honoured (make_golden.gen_priconcat_lap_full)."""
+    cfg, fx = load("full_priconcat_lap")
+    p = det_params("W", "priconcat")
+    pc = O.PathConfig(contract="W", variant="priconcat", eps=cfg["eps"], honor_dp_mode=True)
+    logits = O.forward(p, _window_batch(fx), pc, row_noise=torch.from_numpy(fx["row_noise"]))
+    loss = torch.nn.functional.cross_entropy(logits, torch.from_numpy(fx["labels"]))
+    loss.backward()
+    assert rel_err(logits.detach(), fx["logits"]) < 2e-5
+    check_grads(_grads(p), fx, 1e-4)
+
+
+def test_feawei_feature_pass():
+    """The live feature pass of past_acc_feawei.py:103-124 (normalised fused features) and the
+    float64 column mean of main2's stacked matrix (:141-156)."""
+    cfg, fx = load("feawei_features")
+    p = det_params("W", "prigumbel")
+    pc = O.PathConfig(contract="W", variant="prigumbel")
+    feats = []
+    with torch.no_grad():
+        for i in range(cfg["batches"]):
+            pooled, img, cross = O.encoders(p, dict(eeg=torch.from_numpy(fx[f"eeg{i}"]),
+                                                    act=torch.from_numpy(fx[f"act{i}"])), pc)
+            feats.append(O.minmax(torch.cat((pooled, img, cross), 1)))
+    f = torch.cat(feats).double().numpy()
+    assert rel_err(f, fx["features"]) < 2e-5
+    assert rel_err(f.mean(0), fx["mean_values"]) < 2e-5
+
+
+def _two_pass_iteration(p, batch, labels, n1, g1, n2, g2, dp_opt, model_opt):
+    """past_acc.py:194-212 on the oracle: pass 1 (hard=False) -> DP Adam, pass 2 (hard=True) -> model Adam."""
+    dp_opt.zero_grad()
+    O.cal_loss(O.forward(p, batch, O.PathConfig(contract="W", variant="prigumbel", hard=False), noise=n1,
+                         gumbels=g1), labels)[0].backward()
+    dp_opt.step()
+    model_opt.zero_grad()
+    loss2, _ = O.cal_loss(O.forward(p, batch, O.PathConfig(contract="W", variant="prigumbel", hard=True), noise=n2,
+                                    gumbels=g2), labels)
+    loss2.backward()
+    model_opt.step()
+    return loss2
+
+
+def test_three_iterations():
+    """Three two-optimizer iterations: oracle + torch Adam reproduce the reference's parameter deltas."""
+    cfg, fx = load("three_iterations")
+    p = det_params("W", "prigumbel", w_values_dp())
+    before = {k: v.detach().clone() for k, v in p.items()}
+    dp_opt = torch.optim.Adam([p["DP"]], lr=cfg["lr"])
+    model_opt = torch.optim.Adam([v for k, v in p.items() if k != "DP"], lr=cfg["lr"])
+    batch = _window_batch(fx)
+    labels = torch.from_numpy(fx["labels"])
+    for it in range(cfg["iters"]):
+        t = {k: torch.from_numpy(fx[f"{k}_{it}"]) for k in ("noise1", "gumbels1", "noise2", "gumbels2")}
+        loss2 = _two_pass_iteration(p, batch, labels, t["noise1"], t["gumbels1"], t["noise2"], t["gumbels2"],
+                                    dp_opt, model_opt)
+        assert abs(loss2.item() - float(fx[f"loss2_{it}"])) < 1e-5 * max(1.0, abs(float(fx[f"loss2_{it}"])))
+    n_checked = 0
+    for key in fx:
+        if not key.startswith(("delta:", "dval:")):
+            continue
+        n = key.split(":", 1)[1]
+        d = ((p[n].detach() - before[n]) / cfg["lr"]).reshape(-1).numpy()
+        if key.startswith("dval:"):
+            d = d[fx["dpos:" + n]]
+        ref = fx[key]
+        big = np.abs(ref) > 0.05
+        assert big.any() and np.abs(d[big] - ref[big]).max() < 2e-3, (n, np.abs(d[big] - ref[big]).max())
+        n_checked += 1
+    assert n_checked >= 16
