@@ -11,8 +11,10 @@ persistent attention.  The B <= 4 parity tests never reach them.  Here:
   * B = 256 and B = 512 (configs[2]/[4] per-GPU sizes), PriGumbel with dropout on: everything finite,
     bf16 vs fp32 engine on the same inputs and the same Philox streams: cosine >= 0.99 on the
     logits, the DP gradient and the 12 fused QKV weight gradients;
-  * B = 256 training: the pass-2 loss strictly decreases over 5 PriGumbelTrainer iterations at lr 1e-4
-    (draws fixed per step so the objective is one function), parameters and gradients finite.
+  * B = 256 training: the pass-2 loss strictly decreases over 5 PriGumbelTrainer iterations at lr 2e-5
+    (draws fixed per step so the objective is one function), parameters and gradients finite.  At lr
+    1e-4 (measured r2a) Adam's first, sign-like step of 1e-4 on all 117 M parameters overshoots:
+    0.712 -> 0.783, then 0.629, 0.563, 0.532.
 """
 import pytest
 import torch
@@ -122,7 +124,7 @@ def test_b256_training_loss_decreases_and_stays_finite():
     batch = {"eeg": torch.randn(B, 64, 256, generator=g, device=DEV),
              "act": torch.randn(B, 32, generator=g, device=DEV) * 0.5}
     labels = (torch.rand(B, generator=g, device=DEV) < 0.66).long()
-    tr = PriGumbelTrainer(m.engine, lr=1e-4)
+    tr = PriGumbelTrainer(m.engine, lr=2e-5)
     losses = []
     for _ in range(5):
         m.engine.rng_counter = 0          # same noise / Gumbel / dropout draws every iteration
