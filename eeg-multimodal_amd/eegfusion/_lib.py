@@ -57,8 +57,15 @@ SIGNATURES: dict[str, list] = {
     "eegf_window_tokens": [i32, i32, i32, i32, vp, vp, vp],
     "eegf_embed_gather": [i32, i64, i32, vp, vp, vp, vp],
     "eegf_embed_scatter_add": [i32, i64, i32, vp, vp, vp, vp],
+    # DP-SGD (dpsgd.hip)
+    "eegf_ghost_norm_workspace": [i32, i32],
+    "eegf_ghost_norm": [i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, f32, vp, vp],
+    "eegf_seg_sqnorm": [i32, i32, i32, i32, vp, i64, vp, i64, vp, vp, f32, vp, vp],
+    "eegf_row_sqnorm": [i32, i32, i32, vp, i64, i32, vp, i64, vp, vp],
+    "eegf_dp_clip_rows": [i32, i32, vp, f32, vp, vp, vp],
+    "eegf_dp_noise": [i64, vp, f32, f32, u64, u64, vp],
 }
-RESTYPE_LONG = {"eegf_ln_bwd_partial_rows", "eegf_attn_bwd_workspace"}
+RESTYPE_LONG = {"eegf_ln_bwd_partial_rows", "eegf_attn_bwd_workspace", "eegf_ghost_norm_workspace"}
 
 
 def register(name: str, argtypes: list) -> None:

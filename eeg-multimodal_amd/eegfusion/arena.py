@@ -8,11 +8,13 @@ matrix with no copy.  Offsets are 64-element (256 B) aligned.
 """
 from __future__ import annotations
 
+import weakref
 from collections import OrderedDict
 
 import torch
 
 ALIGN = 64
+_LIVE: "weakref.WeakSet[ParamArena]" = weakref.WeakSet()
 
 
 class ParamArena:
@@ -38,6 +40,21 @@ class ParamArena:
         self.master = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
         self.grad = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
         self.shadow = None              # bf16 copy (allocated on demand)
+        self.shadow_version = -1
+        _LIVE.add(self)
+
+    @staticmethod
+    def owner(t: torch.Tensor) -> "ParamArena | None":
+        """The live arena whose master buffer holds tensor t (a parameter view), if any."""
+        p = t.untyped_storage().data_ptr()
+        for a in list(_LIVE):
+            if a.master.untyped_storage().data_ptr() == p:
+                return a
+        return None
+
+    def invalidate_shadow(self) -> None:
+        """The master was written outside torch's version counter (a raw-pointer optimizer step): the
+        bf16 compute shadow is re-cast before the next forward."""
         self.shadow_version = -1
 
     @staticmethod

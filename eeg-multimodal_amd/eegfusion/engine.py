@@ -114,6 +114,10 @@ class FusionEngine:
         self.defer: list | None = None
         self._defer_k = 0
         self._parts: set[int] = set()
+        # DP-SGD norm pass (eegfusion/dpsgd.py): when set to {"out": fp32 [B], "B": B, "T": L}, every
+        # gradient site of a needed parameter adds the squared per-sample norms of its gradient to out
+        # instead of accumulating the gradient (dpsgd.hip; opacus GradSampleModule semantics)
+        self.psn: dict | None = None
 
     # ------------------------------------------------------------------ parameter access
     def _refresh_shadow(self):
@@ -193,6 +197,9 @@ class FusionEngine:
         the 256x256 path, else a separate column reduction."""
         N, K = w.shape
         ldaux = aux.shape[-1] if aux is not None else 0
+        if bias_grad is not None and self.psn is not None:
+            self._psn_bias(dy, M, N, ldd or N)
+            bias_grad = None
         if bias_grad is not None:
             tiles = _lib.lib().eegf_gemm_colsum_tiles(_code(dy), _code(out), 1, M, K, N)
             if tiles > 0 and (ldd or N) == N:
@@ -216,6 +223,9 @@ class FusionEngine:
             return
         g = self.G(name)
         N, K = g.shape
+        if self.psn is not None:
+            self._psn_linear(dy, x, M, N, K, ldd or N, ldx or K)
+            return
         self.gemm(dy, x, g, N, K, M, 0, 0, ldd or N, ldx or K, K, beta=1.0)
 
     def bgrad(self, dy, name, rows, width=None, ld=None, period=1, out=None):
@@ -223,7 +233,43 @@ class FusionEngine:
             return
         o = out if out is not None else self.G(name)
         width = width or o.shape[-1]
+        if self.psn is not None:
+            if period != 1:
+                raise NotImplementedError(f"eegfusion DP-SGD: per-sample norms of {name} (periodic sum)")
+            self._psn_bias(dy, rows, width, ld or width)
+            return
         self.colsum(dy, ld or width, rows, width, o, period)
+
+    # ---------------------------------------------------- DP-SGD per-sample gradient norms (dpsgd.hip)
+    def _psn_rows(self, M):
+        """rows per sample of a gradient site with M rows: 1 (head / pooler / decoder) or T (BERT)"""
+        ps = self.psn
+        if M == ps["B"]:
+            return 1
+        if M == ps["B"] * ps["T"]:
+            return ps["T"]
+        raise RuntimeError(f"eegfusion DP-SGD: a gradient site with {M} rows (batch {ps['B']}, T {ps['T']})")
+
+    def _psn_linear(self, dy, x, M, N, K, ldd, ldx):
+        """squared per-sample norms of the weight gradient dy^T x (dy [M, N], x [M, K])"""
+        ps, T = self.psn, self._psn_rows(M)
+        if _code(dy) != _code(x):
+            raise RuntimeError("eegfusion DP-SGD: mixed operand dtypes at a weight-gradient site")
+        if T == 1:
+            call("eegf_row_sqnorm", _code(dy), ps["B"], N, P(dy), ldd, K, P(x), ldx, P(ps["out"]), _stream())
+            return
+        n = _lib.lib().eegf_ghost_norm_workspace(ps["B"], T)
+        ws = self.ws.get("ghost", n, torch.float32)
+        call("eegf_ghost_norm", _code(dy), ps["B"], T, K, N, P(x), ldx, P(dy), ldd, P(ws), n, 1.0, P(ps["out"]),
+             _stream())
+
+    def _psn_bias(self, dy, M, W, ld, ln=None):
+        """squared per-sample norms of a bias gradient dy.sum(0) (dy [M, W]); ln = (s, mean, rstd) adds
+        the LayerNorm gamma term sum_t dy_t * xhat_t"""
+        ps, T = self.psn, self._psn_rows(M)
+        xs, mean, rstd = ln if ln is not None else (None, None, None)
+        call("eegf_seg_sqnorm", _code(dy), ps["B"], T, W, P(dy), ld, P(xs), W, P(mean), P(rstd), 1.0, P(ps["out"]),
+             _stream())
 
     def colsum(self, src, ld, rows, width, dst, period=1):
         """dst += column sums of src (rows x width, row stride ld); deferred to the end of the backward
@@ -280,6 +326,12 @@ class FusionEngine:
         part = self._part("ln_part", 2 * nb * HID)
         call("eegf_ln_bwd", _code(dy), rows, HID, P(dy), P(s), P(mean), P(rstd), P(self.F(pre + ".weight")), float(p),
              int(mode if p > 0 else 0), self.cfg.seed, rng, P(dx), P(dr), P(part), P(part[nb * HID:]), _stream())
+        if self.psn is not None:
+            if self.need(pre + ".weight") or self.need(pre + ".bias"):
+                if mode == 2 and p > 0:
+                    raise NotImplementedError("eegfusion DP-SGD: per-sample norms of a post-LN-dropout LayerNorm")
+                self._psn_bias(dy, rows, HID, HID, ln=(s, mean, rstd))
+            return
         self.bgrad(part[: nb * HID], pre + ".weight", nb, HID)
         self.bgrad(part[nb * HID:], pre + ".bias", nb, HID)
 
@@ -628,7 +680,9 @@ class FusionEngine:
                  P(dq_ws), _stream())
             self._ev_end("attn_bwd", ev, 2.5 * 4.0 * B * NH * L * L * DH)
             qn = pre + "attention.self.query.weight"
-            if self.need(qn):
+            if self.need(qn) and self.psn is not None:
+                self._psn_linear(dqkv, s["h"], R, 3 * HID, HID, 3 * HID, HID)
+            elif self.need(qn):
                 gq = self.a.span(qn, 3, self.a.grad).view(3 * HID, HID)
                 self.gemm(dqkv, s["h"], gq, 3 * HID, HID, R, 0, 0, 3 * HID, HID, HID, beta=1.0)
             bn = pre + "attention.self.query.bias"

@@ -131,6 +131,25 @@ class _PathFunction(torch.autograd.Function):
         return (None, None, None) + (None,) * (len(ctx.needs_input_grad) - 3)
 
 
+class _EmptyBatch(torch.autograd.Function):
+    """logits [0, 2] for an empty batch; its backward sets zero gradients on the trainable params"""
+
+    @staticmethod
+    def forward(ctx, model, *params):
+        ctx.model = model
+        return torch.zeros(0, 2, device=model.arena.device)
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        m = ctx.model
+        for n, p in m.named_parameters():
+            if p.requires_grad and p.grad is None:
+                g = m.arena.gview(n)
+                g.zero_()
+                p.grad = g
+        return (None,) * (len(ctx.needs_input_grad))
+
+
 class FusionModel(nn.Module):
     """Common body of ConcatModel / PriConcat / PriGumbel / TICA_LapDropout."""
 
@@ -159,6 +178,7 @@ class FusionModel(nn.Module):
                                  hidden_dropout=dropout, attn_dropout=dropout, dec_dropout=dropout,
                                  eeg_channels=eeg_channels, act_dim=act_dim, seed=seed)
         self._build_arena(torch.device("cpu"))
+        self._dp = None                      # DP-SGD state (eegfusion.dpsgd.GradSampleModule)
 
     # ------------------------------------------------------------------ arena binding
     def _build_arena(self, device):
@@ -210,6 +230,10 @@ class FusionModel(nn.Module):
         self._check_device(*batch.values())
         self._engine.cfg.eps = float(self.eps)
         params = [p for p in self.parameters() if p.requires_grad]
+        if next(iter(batch.values())).shape[0] == 0:
+            # an empty batch (DP-SGD Poisson sampling draws them): no launches; the backward leaves
+            # zero gradients so the private step adds noise only (opacus semantics)
+            return _EmptyBatch.apply(self, *params)
         if torch.is_grad_enabled() and params:
             keys = tuple(batch)
             return _PathFunction.apply(self, keys, bool(hard), *batch.values(), *params)
@@ -221,8 +245,14 @@ class FusionModel(nn.Module):
         names = dict(self.named_parameters())
         in_graph = eng.graph_params()
         need = {n for n, p in names.items() if p.requires_grad and n in in_graph}
-        eng.needs_grad = need
         a = self._arena
+        if self._dp is not None:
+            from .dpsgd import private_backward
+            private_backward(self, saved, dlogits, need)      # overwrites: sum_b c_b grad_b
+            for n in need:
+                names[n].grad = a.gview(n)
+            return
+        eng.needs_grad = need
         # grad routing: overwrite (zero first) params whose .grad is None, accumulate into our views
         for n in need:
             p = names[n]
@@ -250,9 +280,9 @@ class FusionModel(nn.Module):
                     .contiguous().float()}
         # token ids / mask arrive as [B, L], or [B, 1, L] when a pickle holds [1, L] per sample
         # (the shape data.py:25's comment names); both mean the same sequence
-        B = title_input.shape[0]
-        return {"title_input": title_input.reshape(B, -1).contiguous().long(),
-                "text_mask": text_mask.reshape(B, -1).contiguous().long(),
+        B, L = title_input.shape[0], title_input.shape[-1]
+        return {"title_input": title_input.reshape(B, L).contiguous().long(),
+                "text_mask": text_mask.reshape(B, L).contiguous().long(),
                 "frame_input": frame_input.contiguous().float()}
 
     def extra_repr(self):

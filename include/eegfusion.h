@@ -215,6 +215,32 @@ int eegf_embed_gather(int dtype, long rows, int width, const long long* ids, con
 int eegf_embed_scatter_add(int dtype, long rows, int width, const long long* ids, const void* d,
                            float* table_grad, hipStream_t stream);
 
+/* ---- DP-SGD: per-sample clipping + Gaussian noise (opacus make_private_with_epsilon as used by
+ * main_0430.py:143-162 and python/src/custom_models/base_train.py:322-348; opacus's GradSampleModule
+ * + DPOptimizer.pre_step), without materialising per-sample gradients.  out[s] accumulates the
+ * squared per-sample gradient norm of sample s; beta scales the previous value (0 or 1). */
+/* fp32 partial-sum elements eegf_ghost_norm needs: S * (T/64)(T/64 + 1)/2 */
+long eegf_ghost_norm_workspace(int S, int T);
+/* Token-sequence Linear (T rows per sample, T % 64 == 0): out[s] = beta*out[s] + ||DY_s^T X_s||_F^2
+ * = sum_{t,u} (x_t.x_u)(dy_t.dy_u) (the two Gram matrices on the MFMA, tile by tile).  X [S*T, Dx],
+ * DY [S*T, Dy] row-major with leading dimensions; Dx, Dy % 32 == 0. */
+int eegf_ghost_norm(int dtype, int S, int T, int Dx, int Dy, const void* X, long ldx, const void* DY, long ldy,
+                    float* ws, long ws_elems, float beta, float* out, hipStream_t stream);
+/* Per-sample column sums over T rows: out[s] = beta*out[s] + sum_c (sum_t dy[t,c])^2 (a bias) and, with
+ * LayerNorm statistics (xs = pre-LN sum, mean, rstd; nullable), + sum_c (sum_t dy[t,c] xhat[t,c])^2
+ * (LN gamma).  T = 1 gives per-row norms. */
+int eegf_seg_sqnorm(int dtype, int S, int T, int W, const void* dy, long ldd, const void* xs, long ldx,
+                    const float* mean, const float* rstd, float beta, float* out, hipStream_t stream);
+/* One row per sample (head / pooler / visual Linear): out[s] += ||a_s||^2 * (b ? ||b_s||^2 : 1). */
+int eegf_row_sqnorm(int dtype, int S, int Wa, const void* a, long lda, int Wb, const void* b, long ldb, float* out,
+                    hipStream_t stream);
+/* c_s = min(1, max_norm / (sqrt(psn_s) + 1e-6)); dlogits[s, :] *= c_s; clip[s] = c_s (nullable). */
+int eegf_dp_clip_rows(int S, int ncls, const float* psn, float max_norm, float* dlogits, float* clip,
+                      hipStream_t stream);
+/* grad[i] = (grad[i] + std * N(0,1)) * scale (Philox4x32-10 (seed, offset) + Box-Muller). */
+int eegf_dp_noise(long n, float* grad, float std, float scale, unsigned long long seed, unsigned long long offset,
+                  hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif
