@@ -294,6 +294,119 @@ __global__ __launch_bounds__(256) void feawei_kernel(int D, const float* colsum,
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// PriGumbel-v1 (train_val.py:95-158): after fc1 + ReLU + fc2 the 768-wide feature x goes through
+//   gumbel_dropout: logits_j = (w_j, 1 - w_j) (raw w, no sigmoid), m_j = gumbel_softmax(logits_j,
+//     tau, hard)[1] with ONE Gumbel pair per feature shared by the whole batch (the [768, 2] call,
+//     dim -1); hard = straight-through one-hot of the argmax (first index on ties);
+//     res = x * m / (1 - w)                                                     :95-101
+//   Lap_noise: row min-max of res, + one Laplace(0, 1/eps) draw per row          :114-123
+// and the loss adds max_j((1 - w_j) e^eps + w_j) (loss_function :80-93).  Draws: Philox(seed, offset,
+// counter j) words y, z for the feature's pair, the row draw as row_laplace; or injected.
+constexpr int V1D = 768, V1PER = V1D / 256;
+
+struct V1Vals { float m, dmdw; };
+
+DEV V1Vals v1_mask(const FusionArgs& a, int j) {
+  float g0, g1;
+  if (a.gumbels) {
+    g0 = a.gumbels[2 * j];
+    g1 = a.gumbels[2 * j + 1];
+  } else {
+    const u32x4s r = philox4x32((uint32_t)j, 0x76316731u, (uint32_t)a.offset, (uint32_t)(a.offset >> 32),
+                                (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
+    g0 = gumbel_of(r.y);
+    g1 = gumbel_of(r.z);
+  }
+  const float w = a.DP[j];
+  const float z0 = (w + g0) / a.tau, z1 = ((1.0f - w) + g1) / a.tau;
+  const float mz = fmaxf(z0, z1);
+  const float e0 = __expf(z0 - mz), e1 = __expf(z1 - mz), sm = e0 + e1;
+  const float s0 = e0 / sm, s1 = e1 / sm;
+  V1Vals v;
+  v.m = a.hard ? (((s0 >= s1 ? 0.f : 1.f) - s1) + s1) : s1;
+  v.dmdw = -2.0f * s0 * s1 / a.tau;          // d s1 / d w (the straight-through estimator keeps it)
+  return v;
+}
+
+// one workgroup per row; a.pooled = x [B, 768] fp32 (row stride ld_pooled), a.DP = w [768]
+__global__ void __launch_bounds__(256) v1_fwd_kernel(FusionArgs a) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const float* x = (const float*)a.pooled + (long)b * a.ld_pooled;
+  float r[V1PER];
+  float vmin = 3.4e38f, vmax = -3.4e38f;
+  int imin = 0x7fffffff, imax = 0x7fffffff;
+#pragma unroll
+  for (int k = 0; k < V1PER; ++k) {
+    const int j = tid + 256 * k;
+    const V1Vals v = v1_mask(a, j);
+    r[k] = x[j] * v.m / (1.0f - a.DP[j]);
+    if (r[k] < vmin) { vmin = r[k]; imin = j; }
+    if (r[k] > vmax) { vmax = r[k]; imax = j; }
+  }
+  block_minmax(vmin, imin, vmax, imax);
+  const float R = vmax - vmin;
+  if (tid == 0) { a.amin[b] = imin; a.amax[b] = imax; a.range[b] = R; }
+  const float rn = row_laplace(a, b);
+  float* out = (float*)a.out + (long)b * V1D;
+#pragma unroll
+  for (int k = 0; k < V1PER; ++k) {
+    const int j = tid + 256 * k;
+    const float xn = (r[k] - vmin) / R;
+    a.xn[(long)b * V1D + j] = xn;
+    out[j] = xn + rn;
+  }
+}
+
+__global__ void __launch_bounds__(256) v1_bwd_kernel(FusionArgs a) {
+  __shared__ float red[4];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const float* dout = (const float*)a.dout + (long)b * V1D;
+  const float* x = (const float*)a.pooled + (long)b * a.ld_pooled;
+  float d[V1PER], xn[V1PER];
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int k = 0; k < V1PER; ++k) {
+    const int j = tid + 256 * k;
+    d[k] = dout[j];
+    xn[k] = a.xn[(long)b * V1D + j];
+    s1 += d[k] * (xn[k] - 1.0f);
+    s2 += d[k] * xn[k];
+  }
+  s1 = block_sum(s1, red);
+  s2 = block_sum(s2, red);
+  const float R = a.range[b];
+  const int imin = a.amin[b], imax = a.amax[b];
+  float* dx = (float*)a.d_pooled + (long)b * a.ld_pooled;
+#pragma unroll
+  for (int k = 0; k < V1PER; ++k) {
+    const int j = tid + 256 * k;
+    float dr = d[k] / R;
+    if (j == imin) dr += s1 / R;
+    if (j == imax) dr -= s2 / R;
+    const V1Vals v = v1_mask(a, j);
+    const float iw = 1.0f / (1.0f - a.DP[j]);
+    dx[j] = dr * v.m * iw;
+    if (a.ddp_rows) a.ddp_rows[(long)b * V1D + j] = dr * x[j] * (v.dmdw * iw + v.m * iw * iw);
+  }
+}
+
+// loss_w = max_j((1 - w_j) a + w_j), a = e^eps (first index on ties, torch.max); dw[j*] += dscale (1 - a)
+__global__ void __launch_bounds__(256) v1_wloss_kernel(int D, const float* __restrict__ w, float eps_a, float dscale,
+                                                       float* __restrict__ loss, float* __restrict__ dw) {
+  float vmax = -3.4e38f, vmin = 3.4e38f;
+  int imax = 0x7fffffff, imin = 0x7fffffff;
+  for (int j = threadIdx.x; j < D; j += 256) {
+    const float v = (1.0f - w[j]) * eps_a + w[j];
+    if (v > vmax) { vmax = v; imax = j; }
+  }
+  block_minmax(vmin, imin, vmax, imax);
+  if (threadIdx.x == 0) {
+    if (loss) *loss = vmax;
+    if (dw) dw[imax] += dscale * (1.0f - eps_a);
+  }
+}
+
 }  // namespace
 
 extern "C" int eegf_fusion_fwd(int dtype, int B, int variant, const void* pooled, long ld_pooled, const void* img,
@@ -349,6 +462,40 @@ extern "C" int eegf_cross_entropy(int dtype, int B, int C, const void* logits, c
     hipLaunchKernelGGL(ce_kernel<bf16>, dim3(1), dim3(256), 0, stream, (const bf16*)logits, labels, B, C, reduction,
                        dscale, loss, correct, (bf16*)dlogits);
   else return EEGF_ERR_ARG;
+  return (int)hipGetLastError();
+}
+
+extern "C" int eegf_v1_gate_fwd(int B, const float* x, long ldx, const float* w, const float* gumbels,
+                                const float* row_noise, float tau, int hard, float lap_scale, unsigned long long seed,
+                                unsigned long long offset, float* out, float* xn, int* amin, int* amax, float* range,
+                                hipStream_t stream) {
+  if (B <= 0 || !x || !w || !out || !xn || !amin || !amax || !range || !(tau > 0.f) || ldx < V1D) return EEGF_ERR_ARG;
+  FusionArgs a{};
+  a.pooled = x; a.ld_pooled = ldx; a.DP = w; a.gumbels = gumbels; a.row_noise = row_noise; a.B = B; a.hard = hard;
+  a.tau = tau; a.lap_scale = lap_scale; a.seed = seed; a.offset = offset; a.out = out; a.xn = xn; a.amin = amin;
+  a.amax = amax; a.range = range;
+  hipLaunchKernelGGL(v1_fwd_kernel, dim3(B), dim3(256), 0, stream, a);
+  return (int)hipGetLastError();
+}
+
+extern "C" int eegf_v1_gate_bwd(int B, const float* dout, const float* x, long ldx, const float* w,
+                                const float* gumbels, const float* xn, const int* amin, const int* amax,
+                                const float* range, float tau, int hard, unsigned long long seed,
+                                unsigned long long offset, float* dx, float* dw_rows, hipStream_t stream) {
+  if (B <= 0 || !dout || !x || !w || !xn || !amin || !amax || !range || !dx || !(tau > 0.f) || ldx < V1D)
+    return EEGF_ERR_ARG;
+  FusionArgs a{};
+  a.dout = dout; a.pooled = x; a.ld_pooled = ldx; a.DP = w; a.gumbels = gumbels; a.xn = const_cast<float*>(xn);
+  a.amin = const_cast<int*>(amin); a.amax = const_cast<int*>(amax); a.range = const_cast<float*>(range); a.B = B;
+  a.hard = hard; a.tau = tau; a.seed = seed; a.offset = offset; a.d_pooled = dx; a.ddp_rows = dw_rows;
+  hipLaunchKernelGGL(v1_bwd_kernel, dim3(B), dim3(256), 0, stream, a);
+  return (int)hipGetLastError();
+}
+
+extern "C" int eegf_v1_wloss(int D, const float* w, float eps_a, float dscale, float* loss, float* dw,
+                             hipStream_t stream) {
+  if (D <= 0 || !w) return EEGF_ERR_ARG;
+  hipLaunchKernelGGL(v1_wloss_kernel, dim3(1), dim3(256), 0, stream, D, w, eps_a, dscale, loss, dw);
   return (int)hipGetLastError();
 }
 

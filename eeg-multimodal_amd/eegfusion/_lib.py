@@ -57,6 +57,9 @@ SIGNATURES: dict[str, list] = {
     "eegf_window_tokens": [i32, i32, i32, i32, vp, vp, vp],
     "eegf_embed_gather": [i32, i64, i32, vp, vp, vp, vp],
     "eegf_embed_scatter_add": [i32, i64, i32, vp, vp, vp, vp],
+    "eegf_v1_gate_fwd": [i32, vp, i64, vp, vp, vp, f32, i32, f32, u64, u64, vp, vp, vp, vp, vp, vp],
+    "eegf_v1_gate_bwd": [i32, vp, vp, i64, vp, vp, vp, vp, vp, vp, f32, i32, u64, u64, vp, vp, vp],
+    "eegf_v1_wloss": [i32, vp, f32, f32, vp, vp, vp],
     # DP-SGD (dpsgd.hip)
     "eegf_ghost_norm_workspace": [i32, i32],
     "eegf_ghost_norm": [i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, f32, vp, vp],

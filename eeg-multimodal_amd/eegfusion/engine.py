@@ -37,7 +37,9 @@ FUSED = 3 * HID
 EPS_MODES = ("newfrac", "new")    # past_acc.py:132 1/ln((e^eps-w)/(1-w)) | model.py:57 ln(...)
 SPLITK_WS = 24 << 20          # fp32 elements of split-K slab workspace (96 MB)
 VARIANTS = {"concat": _lib.FUSE_CONCAT, "priconcat": _lib.FUSE_PRICONCAT,
-            "priconcat_lap": _lib.FUSE_PRICONCAT_LAP, "prigumbel": _lib.FUSE_PRIGUMBEL}
+            "priconcat_lap": _lib.FUSE_PRICONCAT_LAP, "prigumbel": _lib.FUSE_PRIGUMBEL,
+            # PriGumbel-v1 (train_val.py:125-158): plain concat into fc1+ReLU, fc2, the v1 gate on 768
+            "prigumbel_v1": _lib.FUSE_PRICONCAT}
 
 
 def P(t):
@@ -57,6 +59,7 @@ class EngineConfig:
     eeg_channels: int = 64
     act_dim: int = 32
     seed: int = 980616
+    tau: float = 1.0               # PriGumbel-v1 gumbel_softmax temperature (train_val.py:95)
 
 
 @dataclass
@@ -101,6 +104,7 @@ class FusionEngine:
         if cfg.eps_mode not in EPS_MODES:
             raise ValueError(f"eegfusion: eps_mode must be one of {EPS_MODES}, got {cfg.eps_mode!r}")
         self.variant = VARIANTS[cfg.variant]
+        self.v1 = cfg.variant == "prigumbel_v1"
         self.ws = Workspace(arena.device)
         self.rng_counter = 0
         self.injected = None        # parity hook: dict(noise=..., gumbels=..., row_noise=...)
@@ -503,6 +507,8 @@ class FusionEngine:
         Returns logits [B, 2] and the state the backward needs."""
         cfg = self.cfg
         B = pooled.shape[0]
+        if self.v1:
+            return self._v1_head_fwd(pooled, vis, cross, hard, rng)
         g = self.eh(B, FUSED)
         xn = self._f32(B, FUSED)
         amin = torch.empty(B, dtype=torch.int32, device=self.a.device)
@@ -718,6 +724,8 @@ class FusionEngine:
         cfg = self.cfg
         dlogits = dlogits.float().contiguous()
         B = dlogits.shape[0]
+        if self.v1:
+            return self._v1_head_bwd(t, dlogits, hard, rng)
         hd = t["head"]
         fz = t["fuse"]
         g = fz["g"]
@@ -744,6 +752,68 @@ class FusionEngine:
         if has_dp:
             self.bgrad(ddp, "DP", B, FUSED)
         return dpooled, dvis, dcross
+
+    # ------------------------------------------------------------- PriGumbel-v1 head
+    def _v1_head_fwd(self, pooled, vis, cross, hard, rng):
+        """train_val.py:152-157: feature_concat -> relu(fc1) -> fc2 -> gumbel_dropout(w, tau) ->
+        Lap_noise (row min-max + Laplace(0, 1/eps)) -> classifier (768 -> 2)."""
+        cfg = self.cfg
+        B = pooled.shape[0]
+        inj = self.injected or {}
+        g = self.eh(B, FUSED)
+        call("eegf_fusion_fwd", F32, B, _lib.FUSE_PRICONCAT, P(pooled), HID, P(vis), HID, P(cross), HID, None, None,
+             None, None, 0, 0, math.exp(cfg.eps), 1.0 / cfg.eps, self.cfg.seed, rng + 200, P(g), None, None, None,
+             None, _stream())
+        z1 = self.eh(B, FUSED)
+        self.linear(g, self.F("fc1.weight"), self.F("fc1.bias"), z1, B, epi=_lib.EPI_BIAS_RELU)
+        x = self.eh(B, HID)
+        self.linear(z1, self.F("fc2.weight"), self.F("fc2.bias"), x, B)
+        out, xn = self.eh(B, HID), self._f32(B, HID)
+        amin = torch.empty(B, dtype=torch.int32, device=self.a.device)
+        amax = torch.empty_like(amin)
+        rg = self._f32(B)
+        call("eegf_v1_gate_fwd", B, P(x), HID, P(self.F("w")), P(inj.get("v1_gumbels")), P(inj.get("row_noise")),
+             float(cfg.tau), int(hard), 1.0 / cfg.eps, self.cfg.seed, rng + 200, P(out), P(xn), P(amin), P(amax),
+             P(rg), _stream())
+        logits = self.eh(B, 2)
+        self.linear(out, self.F("classifier.weight"), self.F("classifier.bias"), logits, B)
+        return logits, dict(fuse=dict(g=g, xn=xn, amin=amin, amax=amax, range=rg, inj=inj),
+                            head=dict(z1=z1, x=x, out=out))
+
+    def _v1_head_bwd(self, t, dlogits, hard, rng):
+        cfg = self.cfg
+        B = dlogits.shape[0]
+        hd, fz = t["head"], t["fuse"]
+        self.wgrad(dlogits, hd["out"], "classifier.weight", B)
+        self.bgrad(dlogits, "classifier.bias", B)
+        dout = self.eh(B, HID)
+        self.dgrad(dlogits, self.F("classifier.weight"), dout, B)
+        dx = self.eh(B, HID)
+        dw = self._f32(B, HID) if self.need("w") else None
+        call("eegf_v1_gate_bwd", B, P(dout), P(hd["x"]), HID, P(self.F("w")), P(fz["inj"].get("v1_gumbels")),
+             P(fz["xn"]), P(fz["amin"]), P(fz["amax"]), P(fz["range"]), float(cfg.tau), int(hard), self.cfg.seed,
+             rng + 200, P(dx), P(dw), _stream())
+        if dw is not None:
+            self.bgrad(dw, "w", B, HID)
+        self.wgrad(dx, hd["z1"], "fc2.weight", B)
+        self.bgrad(dx, "fc2.bias", B)
+        dz1 = self.eh(B, FUSED)
+        self.dgrad(dx, self.F("fc2.weight"), dz1, B, epi=_lib.EPI_DRELU, aux=hd["z1"])
+        self.wgrad(dz1, fz["g"], "fc1.weight", B)
+        self.bgrad(dz1, "fc1.bias", B)
+        dg = self.eh(B, FUSED)
+        self.dgrad(dz1, self.F("fc1.weight"), dg, B)
+        dpooled, dvis, dcross = self.eh(B, HID), self.eh(B, HID), self.eh(B, HID)
+        call("eegf_fusion_bwd", F32, B, _lib.FUSE_PRICONCAT, P(dg), None, None, None, None, None, None, None, 0, 0,
+             math.exp(cfg.eps), self.cfg.seed, rng + 200, P(dpooled), HID, P(dvis), HID, P(dcross), HID, None,
+             _stream())
+        return dpooled, dvis, dcross
+
+    def v1_wloss(self, dscale: float, loss: torch.Tensor | None = None):
+        """loss_function's max_j((1 - w_j) e^eps + w_j) term (train_val.py:88-90): value into `loss`
+        (nullable) and dscale * d/dw into the arena gradient of w."""
+        call("eegf_v1_wloss", HID, P(self.F("w")), math.exp(self.cfg.eps), float(dscale), P(loss),
+             P(self.G("w")) if self.need("w") else None, _stream())
 
     def _ready(self, pred):
         """Report weight matrices matching pred as final.  Vectors (biases, LayerNorm, embeddings,

@@ -155,7 +155,8 @@ class FusionModel(nn.Module):
 
     def __init__(self, variant: str, contract: str = "T", eps: float = 1.0, eps_mode: str = "newfrac",
                  dtype: torch.dtype = torch.float32, eeg_channels: int = 64, act_dim: int = 32, frame_dim: int = 512,
-                 with_dp: bool = True, dp_init: torch.Tensor | None = None, dropout: float = 0.1, seed: int = 980616):
+                 with_dp: bool = True, dp_init: torch.Tensor | None = None, dropout: float = 0.1, seed: int = 980616,
+                 tau: float = 1.0):
         super().__init__()
         self._variant, self._contract = variant, contract
         self.bert = _bert()
@@ -167,16 +168,26 @@ class FusionModel(nn.Module):
             self.visual_encoder = nn.Linear(frame_dim, HID)
         self.multi_head_decoderlayer = nn.TransformerDecoderLayer(d_model=HID, nhead=12)
         self.multi_head_decoder = nn.TransformerDecoder(self.multi_head_decoderlayer, num_layers=DEC_L)
-        self.dropout = nn.Dropout(0.1)
-        self.fc_layers = nn.Sequential(nn.Linear(FUSED, FUSED), nn.ReLU(), nn.Linear(FUSED, HID), nn.Tanh())
-        self.classifier = nn.Linear(HID, 2)
+        if variant == "prigumbel_v1":
+            # train_val.py:125-142 registration order: classifier (first assigned at :134), w, dropout,
+            # fc1, fc2; no fc_layers, no DP
+            self.classifier = nn.Linear(HID, 2)
+            self.w = nn.Parameter(torch.rand(HID))
+            self.dropout = GumbelSoftmaxDropout(tau)
+            self.fc1 = nn.Linear(FUSED, FUSED)
+            self.fc2 = nn.Linear(FUSED, HID)
+            with_dp = False
+        else:
+            self.dropout = nn.Dropout(0.1)
+            self.fc_layers = nn.Sequential(nn.Linear(FUSED, FUSED), nn.ReLU(), nn.Linear(FUSED, HID), nn.Tanh())
+            self.classifier = nn.Linear(HID, 2)
         if with_dp:
             self.DP = nn.Parameter(torch.zeros(1, FUSED) if dp_init is None else dp_init.reshape(1, FUSED).float())
         self.noiser = torch.distributions.laplace.Laplace(torch.tensor([0.0]), torch.tensor([1.0]))
         self.eps = torch.tensor(eps)
         self._cfg = EngineConfig(contract=contract, variant=variant, dtype=dtype, eps=float(eps), eps_mode=eps_mode,
                                  hidden_dropout=dropout, attn_dropout=dropout, dec_dropout=dropout,
-                                 eeg_channels=eeg_channels, act_dim=act_dim, seed=seed)
+                                 eeg_channels=eeg_channels, act_dim=act_dim, seed=seed, tau=float(tau))
         self._build_arena(torch.device("cpu"))
         self._dp = None                      # DP-SGD state (eegfusion.dpsgd.GradSampleModule)
 
@@ -351,6 +362,37 @@ class TICA_LapDropout(FusionModel):
     def forward(self, eeg_txt_input, eeg_txt_mask, act_img_input, act_img_mask, epsilon, hard):
         self.eps = torch.tensor(float(epsilon))
         return self._run(self._token_batch(act_img_input, act_img_mask, eeg_txt_input, eeg_txt_mask), hard)
+
+
+class GumbelSoftmaxDropout(nn.Module):
+    """train_val.py:103-112 holder (no parameters): tau; soft masks in train mode, hard in eval.  The
+    computation is the engine's v1 gate (eegf_v1_gate_fwd / bwd)."""
+
+    def __init__(self, tau):
+        super().__init__()
+        self.tau = tau
+
+    def forward(self, *a, **k):  # pragma: no cover - never called
+        raise RuntimeError("GumbelSoftmaxDropout runs inside the engine; call the top-level model")
+
+
+class PriGumbelV1Model(FusionModel):
+    """train_val.py:125-158 — ConcatModel(tau, epsilon); forward(frame_input, vedio_mask, title_input,
+    text_mask): concat -> relu(fc1) -> fc2 -> Gumbel-softmax feature dropout x*m/(1-w) (soft in train
+    mode, hard in eval, one draw per feature per forward) -> row min-max + Laplace(0, 1/eps) ->
+    classifier."""
+
+    def __init__(self, tau: float = 0.01, epsilon: float = 1.0, contract: str = "T", **kw):
+        super().__init__("prigumbel_v1", contract=contract, eps=float(epsilon), tau=float(tau), **kw)
+        self.epsilon = epsilon
+
+    def forward(self, frame_input, vedio_mask, title_input, text_mask):
+        self._engine.cfg.tau = float(self.dropout.tau)
+        return self._run(self._token_batch(frame_input, vedio_mask, title_input, text_mask), not self.training)
+
+    def forward_window(self, eeg, act, hard=None):
+        self._engine.cfg.tau = float(self.dropout.tau)
+        return super().forward_window(eeg, act, (not self.training) if hard is None else hard)
 
 
 def load_bert_weights(model: FusionModel, path: str):

@@ -209,3 +209,39 @@ class SinglePassTrainer:
         self.reduce.finish(0, e.a.numel)
         self.opt.step()
         return self.loss, self.correct
+
+
+class PriGumbelV1Trainer:
+    """PriGumbel-v1 step (train_val.py:204-215): Adam over every parameter in the graph,
+    loss = alpha * CE(mean) + max_j((1 - w_j) e^eps + w_j) (loss_function :80-93); the CE gradient
+    scaled by alpha in the loss kernel, the privacy term's gradient added by eegf_v1_wloss."""
+
+    def __init__(self, engine: FusionEngine, alpha: float, lr: float = 1e-5, reducer: GradReducer | None = None):
+        self.e, self.alpha = engine, float(alpha)
+        self.params = engine.graph_params()
+        self.opt = FlatAdam(engine, (0, engine.a.numel), lr=lr, names=self.params)
+        self.reduce = reducer or GradReducer()
+        dev = engine.a.device
+        self.loss = torch.zeros(2, dtype=torch.float32, device=dev)     # [alpha * CE, privacy term]
+        self.correct = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    def step(self, batch, labels, training: bool = True):
+        e = self.e
+        logits, sv = e.forward(batch, hard=not training, training=training, save=True)
+        dl = torch.empty_like(logits)
+        call("eegf_cross_entropy", _lib.F32, logits.shape[0], 2, logits.data_ptr(), labels.data_ptr(), 0, self.alpha,
+             self.loss.data_ptr(), self.correct.data_ptr(), dl.data_ptr(), _s())
+        self.opt.zero_grad()
+        e.needs_grad = self.params
+        self.reduce.begin(e.a, self.params)
+        e.grad_ready = self.reduce.ready
+        try:
+            e.backward(sv, dl)
+        finally:
+            e.grad_ready = None
+        e.v1_wloss(1.0, self.loss[1:])     # before finish(): w is all-reduced (sum / N) with the vectors
+        e.needs_grad = None
+        self.reduce.finish(0, e.a.numel)
+        self.opt.step()
+        self.loss[:1].mul_(self.alpha)
+        return self.loss, self.correct

@@ -183,6 +183,24 @@ int eegf_cross_entropy(int dtype, int B, int C, const void* logits, const long l
                        int reduction, float dscale, float* loss, int* correct, void* dlogits,
                        hipStream_t stream);
 
+/* PriGumbel-v1 gate (train_val.py:95-123, the model of :125-158): x [B,768] fp32 (fc2 output, row
+ * stride ldx), w [768] (raw, no sigmoid); m_j = F.gumbel_softmax((w_j, 1-w_j), tau, hard)[1] with one
+ * Gumbel pair per feature for the whole batch (gumbels [768,2] = -log Exp(1) injected, or Philox);
+ * res = x m / (1 - w); out = row min-max(res) + row Laplace(0, lap_scale) (row_noise [B] injected or
+ * Philox).  Saves xn, argmin/argmax/range for the backward. */
+int eegf_v1_gate_fwd(int B, const float* x, long ldx, const float* w, const float* gumbels, const float* row_noise,
+                     float tau, int hard, float lap_scale, unsigned long long seed, unsigned long long offset,
+                     float* out, float* xn, int* amin, int* amax, float* range, hipStream_t stream);
+/* Backward: dx [B,768] (row stride ldx); dw_rows [B,768] per-row dL/dw (nullable; reduce with
+ * eegf_colsum), the straight-through estimator for hard masks. */
+int eegf_v1_gate_bwd(int B, const float* dout, const float* x, long ldx, const float* w, const float* gumbels,
+                     const float* xn, const int* amin, const int* amax, const float* range, float tau, int hard,
+                     unsigned long long seed, unsigned long long offset, float* dx, float* dw_rows,
+                     hipStream_t stream);
+/* loss_function's privacy term (train_val.py:88-90): loss = max_j((1-w_j) eps_a + w_j) (nullable);
+ * dw[argmax] += dscale (1 - eps_a) (nullable; first index on ties). */
+int eegf_v1_wloss(int D, const float* w, float eps_a, float dscale, float* loss, float* dw, hipStream_t stream);
+
 /* feawei DP initialisation (past_acc.py:98-103 with k = 1, zscore = 1; past_acc_feawei.py:153-163
  * with k = 5, zscore = 0): colsum [D] = column sums over `count` rows of the normalised features
  * (eegf_colsum with beta = 1 across batches); z = (m - mean m) / std m (population std) or z = m;

@@ -54,6 +54,7 @@ class PathConfig:
     eps_mode: str = "newfrac"    # "newfrac": 1/ln((e^eps-w)/(1-w)) (past_acc.py:132); "new": ln(...) (model.py:57)
     hard: bool = False
     honor_dp_mode: bool = False  # PriConcat: apply DP_guarantee('feature_all_lap') (main_0430.py:76-85)
+    tau: float = 1.0             # PriGumbel-v1 gumbel_softmax temperature (train_val.py:95)
 
 
 _DROP = None
@@ -216,6 +217,28 @@ def head(p, f):
     return _lin(h, p, "classifier")
 
 
+# --------------------------------------------------------------- PriGumbel-v1 (train_val.py)
+def gumbel_dropout_v1(x, w, gumbels, tau, hard):
+    """train_val.py:95-101: logits [768, 2] = (w, 1 - w) (raw w), F.gumbel_softmax over dim -1 with
+    the -log Exp(1) draws [768, 2] supplied; mask = column 1; x * mask / (1 - w)."""
+    logits = torch.stack((w, 1 - w), dim=1)
+    mask = gumbel_softmax_injected(logits, gumbels, hard, tau=tau, dim=-1)[:, 1]
+    return x * mask / (1.0 - w)
+
+
+def head_v1(p, f, gumbels, row_noise, tau, hard):
+    """train_val.py:153-157: relu(fc1) -> fc2 -> gumbel dropout -> Lap_noise (:114-123: row min-max +
+    one Laplace(0, 1/eps) draw per row) -> classifier."""
+    x = _lin(torch.relu(_lin(f, p, "fc1")), p, "fc2")
+    res = gumbel_dropout_v1(x, p["w"], gumbels, tau, hard)
+    return _lin(minmax(res) + row_noise.view(-1, 1), p, "classifier")
+
+
+def loss_v1(logits, labels, w, alpha, eps):
+    """train_val.py:80-93: alpha * CE(mean) + max_j((1 - w_j) e^eps + w_j)."""
+    return alpha * F.cross_entropy(logits, labels) + ((1 - w) * math.exp(eps) + w).max(dim=0)[0]
+
+
 # ------------------------------------------------------------------------- feawei init
 def feawei_dp_init(features, k=1.0, zscore=True, base=(0.4, 0.5, 0.3)):
     """DP initialisation from a feature pass, numpy as in the reference:
@@ -257,6 +280,9 @@ def encoders(p, batch, cfg: PathConfig):
 def forward(p, batch, cfg: PathConfig, noise=None, gumbels=None, row_noise=None, return_feature=False):
     pooled, img, cross = encoders(p, batch, cfg)
     f = torch.cat((pooled, img, cross), dim=1)                     # [B,2304]: EEG || action || cross
+    if cfg.variant == "prigumbel_v1":
+        logits = head_v1(p, f, gumbels, row_noise, cfg.tau, cfg.hard)
+        return (logits, f, None) if return_feature else logits
     if cfg.variant == "priconcat":
         g = dp_guarantee(f, row_noise, cfg.honor_dp_mode)
     elif cfg.variant == "concat":
@@ -318,6 +344,15 @@ def param_shapes(contract: str = "W", variant: str = "prigumbel", eeg_channels=6
         for n in ("norm1", "norm2", "norm3"):
             s[pre + n + ".weight"] = (HID,)
             s[pre + n + ".bias"] = (HID,)
+    if variant == "prigumbel_v1":
+        s["classifier.weight"] = (2, HID)
+        s["classifier.bias"] = (2,)
+        s["w"] = (HID,)
+        s["fc1.weight"] = (FUSED, FUSED)
+        s["fc1.bias"] = (FUSED,)
+        s["fc2.weight"] = (HID, FUSED)
+        s["fc2.bias"] = (HID,)
+        return s
     s["fc_layers.0.weight"] = (FUSED, FUSED)
     s["fc_layers.0.bias"] = (FUSED,)
     s["fc_layers.2.weight"] = (HID, FUSED)

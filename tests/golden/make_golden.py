@@ -437,6 +437,53 @@ def gen_feawei_features():
     save("feawei_features", dict(contract="W", seed=SEED, B=B_W, batches=2, C=C_W, T=T_W, A=A_W), out)
 
 
+def gen_prigumbel_v1():
+    """PriGumbel-v1 (train_val.py:125-158) through the reference's own forward and loss_function
+    (:80-93): Gumbel draws recorded from its F.gumbel_softmax call ([768, 2], one pair per feature),
+    the per-row Laplace draws of Lap_noise recorded from Laplace.sample.  w set to a spread of values
+    in (0.05, 0.95) (the reference initialises torch.rand(768)).  Cases: train mode (soft mask) and
+    eval mode (hard, straight-through), tau 0.5 / 0.01, eps 1, alpha 0.2 (the 'good results' run,
+    train_val.py:547-549)."""
+    import train_val
+    from torch.distributions.laplace import Laplace
+    out = {}
+    cases = [(0.5, False), (0.01, True), (0.01, False)]
+    for ci, (tau, hard) in enumerate(cases):
+        torch.manual_seed(50 + ci)
+        gen = torch.Generator().manual_seed(60 + ci)
+        m = prepare(train_val.ConcatModel(tau, 1.0), "W")
+        with torch.no_grad():
+            m.w.copy_(torch.from_numpy((0.05 + 0.9 * (np.arange(768) % 97) / 96.0).astype(np.float32)))
+        if hard:
+            m.eval()
+        eeg, act = window_inputs(gen)
+        labels = torch.tensor([[1], [0]])
+        lap = []
+        orig = Laplace.sample
+
+        def rec(self, shape=torch.Size()):
+            r = orig(self, shape)
+            lap.append(r.detach().clone())
+            return r
+
+        Laplace.sample = rec
+        try:
+            with RecordExp() as re_:
+                logits = m(act.unsqueeze(1), torch.ones(B_W, 1, dtype=torch.long), eeg,
+                           torch.ones(B_W, T_W, dtype=torch.long))
+        finally:
+            Laplace.sample = orig
+        loss, _, _, _ = train_val.loss_function(logits, labels, m, 0.2, 1.0)
+        loss.backward()
+        pre = f"c{ci}:"
+        out.update({pre + "eeg": eeg, pre + "act": act, pre + "labels": labels.view(-1),
+                    pre + "w": m.w.detach().clone(), pre + "gumbels": -torch.log(re_.draws[0]),
+                    pre + "row_noise": lap[0].view(-1), pre + "logits": logits.detach(), pre + "loss": loss.detach()})
+        out.update({pre + k: v for k, v in grad_record(m).items()})
+    save("prigumbel_v1", dict(cases=[dict(tau=t, hard=h, eps=1.0, alpha=0.2) for t, h in cases], contract="W",
+                              seed=SEED, B=B_W, C=C_W, T=T_W, A=A_W), out)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
     past_acc, main_0430, ref_model = import_reference()
@@ -451,3 +498,4 @@ if __name__ == "__main__":
     gen_adam_three_iters(past_acc)
     gen_priconcat_lap_full(main_0430)
     gen_feawei_features()
+    gen_prigumbel_v1()

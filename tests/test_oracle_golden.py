@@ -161,3 +161,28 @@ def test_three_iterations():
         assert big.any() and np.abs(d[big] - ref[big]).max() < 2e-3, (n, np.abs(d[big] - ref[big]).max())
         n_checked += 1
     assert n_checked >= 16
+
+
+def _case(fx, ci):
+    pre = f"c{ci}:"
+    return {k[len(pre):]: v for k, v in fx.items() if k.startswith(pre)}
+
+
+@pytest.mark.parametrize("ci", [0, 1, 2])
+def test_prigumbel_v1(ci):
+    """train_val.py PriGumbel-v1: the reference's forward + loss_function with its recorded Gumbel
+    ([768, 2]) and per-row Laplace draws (make_golden.gen_prigumbel_v1)."""
+    cfg, fx = load("prigumbel_v1")
+    c = cfg["cases"][ci]
+    f = _case(fx, ci)
+    p = det_params("W", "prigumbel_v1")
+    with torch.no_grad():
+        p["w"].copy_(torch.from_numpy(f["w"]))
+    pc = O.PathConfig(contract="W", variant="prigumbel_v1", eps=c["eps"], hard=c["hard"], tau=c["tau"])
+    logits = O.forward(p, _window_batch(f), pc, gumbels=torch.from_numpy(f["gumbels"]),
+                       row_noise=torch.from_numpy(f["row_noise"]))
+    loss = O.loss_v1(logits, torch.from_numpy(f["labels"]), p["w"], c["alpha"], c["eps"])
+    loss.backward()
+    assert rel_err(logits.detach(), f["logits"]) < 2e-5
+    assert abs(loss.item() - float(f["loss"])) < 1e-5
+    check_grads(_grads(p), f, 1e-4)
