@@ -1,0 +1,152 @@
+"""Per-kernel PMC table (MFMA busy, VALU/MFMA instruction mix, LDS conflicts, HBM bytes) from
+rocprofv3 counter passes over the same bench command.
+
+usage: python tools/pmc_table.py <tag> <steps traced> <pass_dir> [<pass_dir> ...]
+
+Each <pass_dir> holds one `rocprofv3 --kernel-trace --pmc ... --output-format csv` run
+(`*counter_collection.csv` and `*kernel_trace.csv`).  Launches are grouped by (kernel, grid), so
+GEMM shapes that share a kernel symbol stay apart.  Per group and per launch:
+
+  mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)
+              (BUSY counts SIMD cycles, 32 per v_mfma_f32_32x32x16_bf16; GRBM_GUI_ACTIVE is summed
+              over the 8 XCDs — MI355X_MICROARCH.md, cycle constants and DVFS notes)
+  hbm_bytes = 2 x FETCH_SIZE x 1024 + WRITE_SIZE x 1024   (gfx950: FETCH_SIZE counts half the bytes of
+              16-B-per-lane streaming reads — MI355X_MICROARCH.md §HBM)
+  clock_ghz = GRBM_GUI_ACTIVE / 8 / duration
+
+Writes profiles/<tag>_pmc_table.md and profiles/pmc_<tag>.json (read by bench.py: roofline traffic and
+mfma_busy of the named kernel groups).
+"""
+import csv
+import json
+import sys
+from collections import defaultdict
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+N_SIMD = 1024
+
+# bench.py roofline groups -> kernel-name fragments (mangled or demangled) + grid filters
+GROUPS = {
+    "dgrad_cs": ("gemm8_kernelILb1ELb0ELi0EDF16bLi4ELb1E",),
+    "ffn1_fwd": ("gemm8_kernelILb1ELb1ELi2EDF16bLi4E", "gemm8_kernelILb1ELb1ELi8EDF16bLi4E"),
+    "attn_fwd": ("attn_fwd256_kernel",),
+    "attn_bwd": ("attn_bwd_kernel", "attn_bwd256_kernel"),
+}
+
+
+def short(name):
+    return name if len(name) < 96 else name[:93] + "..."
+
+
+def read_pass(d):
+    d = Path(d)
+    cc = next(d.rglob("*counter_collection.csv"), None)
+    kt = next(d.rglob("*kernel_trace.csv"), None)
+    dur = {}
+    if kt is not None:
+        for r in csv.DictReader(open(kt)):
+            dur[r["Dispatch_Id"]] = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
+    per = defaultdict(dict)          # dispatch -> {counter: value, _name, _grid}
+    if cc is None:
+        return per, dur
+    for r in csv.DictReader(open(cc)):
+        k = r["Dispatch_Id"]
+        e = per[k]
+        e["_name"] = r["Kernel_Name"]
+        e["_grid"] = r.get("Grid_Size", "")
+        e[r["Counter_Name"]] = e.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        if "Start_Timestamp" in r and r.get("End_Timestamp"):
+            dur.setdefault(k, float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
+    return per, dur
+
+
+def main():
+    tag, steps, dirs = sys.argv[1], float(sys.argv[2]), sys.argv[3:]
+    agg = defaultdict(lambda: defaultdict(float))     # (name, grid) -> counter sums
+    cnt = defaultdict(lambda: defaultdict(int))       # (name, grid) -> launches seen per counter
+    tsum = defaultdict(float)
+    tn = defaultdict(int)
+    for d in dirs:
+        per, dur = read_pass(d)
+        for k, e in per.items():
+            key = (e["_name"], e["_grid"])
+            for c, v in e.items():
+                if not c.startswith("_"):
+                    agg[key][c] += v
+                    cnt[key][c] += 1
+            if k in dur:
+                tsum[key] += dur[k]
+                tn[key] += 1
+
+    def avg(key, c):
+        n = cnt[key].get(c, 0)
+        return agg[key][c] / n if n else None
+
+    rows = []
+    for key in agg:
+        if not tn[key]:
+            continue
+        t_ns = tsum[key] / tn[key]
+        launches = max(cnt[key].values()) / max(1, len(dirs))
+        gui = avg(key, "GRBM_GUI_ACTIVE")
+        busy = avg(key, "SQ_VALU_MFMA_BUSY_CYCLES")
+        fetch, write = avg(key, "FETCH_SIZE"), avg(key, "WRITE_SIZE")
+        hbm = 2 * fetch * 1024 + write * 1024 if fetch is not None and write is not None else None
+        cyc = gui / 8 if gui else None
+        rows.append({
+            "kernel": key[0], "grid": key[1], "avg_us": t_ns / 1e3,
+            "ms_per_step": tsum[key] / tn[key] * (tn[key] / len(dirs)) / steps / 1e6 if tn[key] else None,
+            "launches_per_step": tn[key] / len(dirs) / steps,
+            "mfma_busy": busy / (N_SIMD * cyc) if busy is not None and cyc else None,
+            "clock_ghz": cyc / t_ns if cyc else None,
+            "valu_insts": avg(key, "SQ_INSTS_VALU"), "mfma_insts": avg(key, "SQ_INSTS_MFMA"),
+            "lds_conflict_frac": (avg(key, "SQ_LDS_BANK_CONFLICT") / avg(key, "SQ_LDS_IDX_ACTIVE")
+                                  if avg(key, "SQ_LDS_IDX_ACTIVE") else None),
+            "hbm_bytes": hbm, "hbm_gbs": hbm / t_ns if hbm is not None else None,
+            "fetch_kb": fetch, "write_kb": write,
+            "l2_hit": (avg(key, "TCC_HIT_sum") / (avg(key, "TCC_HIT_sum") + avg(key, "TCC_MISS_sum"))
+                       if avg(key, "TCC_HIT_sum") is not None and avg(key, "TCC_MISS_sum") else None),
+        })
+    rows.sort(key=lambda r: -(r["ms_per_step"] or 0))
+
+    def f(v, fmt):
+        return "—" if v is None else format(v, fmt)
+
+    out = [f"# rocprofv3 PMC table — {tag}", "",
+           f"bench.py PriGumbel B=256 bf16, {steps:g} iterations traced per pass; passes: "
+           + ", ".join(Path(d).name for d in dirs), "",
+           "mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (1024 x GRBM_GUI_ACTIVE/8); HBM = 2 x FETCH_SIZE + WRITE_SIZE; "
+           "clock = GRBM_GUI_ACTIVE/8 / duration (durations are from the profiled passes)", "",
+           "| ms/step | launches/step | avg us | mfma_busy | clock GHz | VALU/MFMA insts | LDS conflict | HBM MB/launch "
+           "| HBM GB/s | L2 hit | kernel (grid) |",
+           "|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|---|"]
+    for r in rows[:20]:
+        mix = (r["valu_insts"] / r["mfma_insts"]) if r["valu_insts"] and r["mfma_insts"] else None
+        out.append(f"| {f(r['ms_per_step'], '.3f')} | {r['launches_per_step']:.1f} | {r['avg_us']:.1f} | "
+                   f"{f(r['mfma_busy'], '.3f')} | {f(r['clock_ghz'], '.2f')} | {f(mix, '.2f')} | "
+                   f"{f(r['lds_conflict_frac'], '.3f')} | {f(r['hbm_bytes'] and r['hbm_bytes'] / 1e6, '.1f')} | "
+                   f"{f(r['hbm_gbs'], '.0f')} | {f(r['l2_hit'], '.3f')} | `{short(r['kernel'])}` ({r['grid']}) |")
+    (ROOT / "profiles" / f"{tag}_pmc_table.md").write_text("\n".join(out) + "\n")
+    print("\n".join(out))
+
+    groups = {}
+    for g, frags in GROUPS.items():
+        sel = [r for r in rows if any(fr in r["kernel"] for fr in frags)]
+        if not sel:
+            continue
+        w = sum(r["launches_per_step"] for r in sel)
+
+        def wavg(field):
+            vs = [(r[field], r["launches_per_step"]) for r in sel if r[field] is not None]
+            return sum(v * n for v, n in vs) / sum(n for _, n in vs) if vs else None
+
+        groups[g] = {"launches_per_step": w, "avg_us": wavg("avg_us"), "mfma_busy": wavg("mfma_busy"),
+                     "hbm_bytes_per_launch": wavg("hbm_bytes"), "clock_ghz": wavg("clock_ghz"),
+                     "lds_conflict_frac": wavg("lds_conflict_frac"), "round": tag}
+    (ROOT / "profiles" / f"pmc_{tag}.json").write_text(json.dumps(groups, indent=1) + "\n")
+    print(json.dumps(groups, indent=1))
+
+
+if __name__ == "__main__":
+    main()
