@@ -40,6 +40,20 @@ HID, L, C, A = 768, 256, 64, 32
 F_PER_SAMPLE = 46.03e9            # forward GEMM+attention FLOPs per sample, contract W
 PEAK_BF16 = 2500.0                # TFLOP/s dense bf16 MFMA (MI355X_MICROARCH.md)
 METRIC = "samples/sec at batch 256, 64ch×256 EEG + 32-d action, 1/2/4/8 GPUs"
+PMC_FILE = "pmc_r2.json"          # profiles/: tools/pmc_table.py output (HBM bytes, MFMA busy per group)
+# probed kernel groups (HIP events around each launch on the launch stream, engine.probe)
+KERNEL_GROUPS = {
+    "ffn1_fwd": "BertIntermediate GEMM + bias + GELU (+GELU' saved in pass 2), 65536x3072x768",
+    "qkv_fwd": "fused Q|K|V projection GEMM + bias, 65536x2304x768",
+    "ffn2_fwd": "BertOutput GEMM + bias, 65536x768x3072",
+    "attn_fwd": "fused self-attention forward (QK^T, softmax, dropout, PV), 256x12 heads x 256^2 x 64",
+    "attn_bwd": "fused self-attention backward (dQ, dK, dV)",
+    "dgrad_qkv": "input gradient through the Q|K|V projection, 65536x768x2304",
+    "dgrad_ffn1": "input gradient through BertIntermediate, 65536x768x3072",
+    "dgrad_out": "input gradient through the attention output projection, 65536x768x768",
+    "dgrad_ffn2": "input gradient through BertOutput with the GELU' product, 65536x3072x768",
+    "wgrad": "weight gradients (split-K over 65536 tokens) with the bias gradients fused (row sums)",
+}
 
 
 def parse_args(argv=None):
@@ -262,7 +276,7 @@ def main():
         torch.cuda.synchronize()
         feawei = {"samples": acc.count, "seconds": round(time.perf_counter() - t0, 3), "k": 1.0, "zscore": True}
 
-    tags = ("ffn1_fwd", "qkv_fwd", "ffn2_fwd", "attn_fwd", "attn_bwd", "dgrad_cs", "dgrad_ffn2")
+    tags = tuple(KERNEL_GROUPS)
     total_dt, per_eps, loss = 0.0, [], None
     probe_all = {t: [] for t in tags}
     for eps in sweep:
@@ -300,11 +314,13 @@ def main():
         value = world * B * steps / total_dt
         ks = probe_stats(probe_all)
         step_tf = value / world * flops_per_sample(args.variant) / 1e12
-        dom = ks.get("dgrad_cs")
-        pmc = load_profile_json("pmc_r2.json", "dgrad_cs") or {}
-        roofline = {"kernel": "dgrad_cs: BERT input-gradient GEMMs with fused bias-gradient column sums "
-                              "(QKV K=2304, out-proj K=768, FFN-in K=3072; gemm8 CS, 36 launches per step, "
-                              "the largest kernel group by time in profiles/r1s11_kernel_stats.md)",
+        # the dominant kernel group: largest total time among the probed groups of this run
+        dom_tag = max(ks, key=lambda t: ks[t]["avg_ms"] * ks[t]["launches"]) if ks else None
+        dom = ks.get(dom_tag)
+        pmc = load_profile_json(PMC_FILE, dom_tag) or {}
+        roofline = {"kernel": f"{dom_tag}: {KERNEL_GROUPS.get(dom_tag, '')} (the largest probed kernel group by "
+                              f"time in this run: {dom['avg_ms'] * dom['launches'] / steps:.2f} ms per step)"
+                              if dom else None,
                     "bound": "mfma", "achieved": round(dom["tflops"], 1) if dom else None, "peak": PEAK_BF16,
                     "unit": "TFLOP/s", "frac": round(dom["tflops"] / PEAK_BF16, 4) if dom else None,
                     "traffic": pmc.get("hbm_bytes_per_launch"), "mfma_busy": pmc.get("mfma_busy"),

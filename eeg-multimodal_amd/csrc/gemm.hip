@@ -457,6 +457,8 @@ int eegf_gemm_big(int a_kc, int b_kc, int epi, int out_f32, int M, int N, int K,
                   const void* B, long ldb, void* C, long ldc, const float* bias, void* aux, long ldaux, float alpha,
                   float beta, float epi_scale, void* workspace, long ws_bytes, float* a_colsum, hipStream_t stream);
 int eegf_gemm_big_colsum_tiles(int M, int N, int K);
+int eegf_gemm_big_wgrad_bias(int M, int N, int K, const void* A, long lda, const void* B, long ldb, float* C, long ldc,
+                             float beta, float* db, void* workspace, long ws_bytes, hipStream_t stream);
 
 static int lds_epi_enabled() {
   static const int on = [] { const char* e = getenv("EEGF_GEMM_LDS_EPI"); return (e && e[0] == '0') ? 0 : 1; }();
@@ -556,4 +558,12 @@ extern "C" int eegf_gemm_acs(int dtype, int out_dtype, int a_kcontig, int b_kcon
   if (!a_colsum || eegf_gemm_colsum_tiles(dtype, out_dtype, a_kcontig, M, N, K) == 0) return EEGF_ERR_ARG;
   return gemm_impl(dtype, out_dtype, a_kcontig, b_kcontig, epi, M, N, K, 1, A, lda, 0, B, ldb, 0, C, ldc, 0, bias, 0,
                    aux, ldaux, 0, alpha, beta, epi_scale, nullptr, 0, a_colsum, stream);
+}
+
+extern "C" int eegf_gemm_wgrad_bias(int dtype, int M, int N, int K, const void* dY, long ldd, const void* X, long ldx,
+                                    float* dW, long ldw, float beta, float* db, void* workspace, long ws_bytes,
+                                    hipStream_t stream) {
+  if (dtype != EEGF_BF16 || !big_enabled() || !dY || !X || !dW || !db || M <= 0 || N <= 0 || K <= 0) return EEGF_ERR_ARG;
+  const int st = eegf_gemm_big_wgrad_bias(M, N, K, dY, ldd, X, ldx, dW, ldw, beta, db, workspace, ws_bytes, stream);
+  return st == 1 ? EEGF_ERR_ARG : st;
 }

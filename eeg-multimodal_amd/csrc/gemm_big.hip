@@ -37,6 +37,7 @@ struct BigArgs {
   int ksplit;            // >0: split-K slice length; C = fp32 slabs [blockIdx.y][M][N]
   float* colsum_part;    // AKC only: [tiles_m][K] partial column sums of A (nullable)
   int prio;              // 1: waves 4-7 run at s_setprio 1 for the whole kernel (eegf_tune key 3)
+  float* rowsum_part;    // gemm4w RS only: [splits][M] sums over this split's K of each row of a k-major A
 };
 int g_big_prio = [] { const char* e = getenv("EEGF_GEMM_PRIO"); return e ? atoi(e) : 0; }();
 
@@ -920,7 +921,11 @@ DEV bf16x8 rd_col_off(const bf16* t, int o0, int o1) {
 // against a ones operand (A^T fragments by transpose reads), parks its 32 partials in
 // red[k & 1][w]; wave 0 folds the previous K-tile's 4 partials (fixed order) into ks[K] after the
 // K-tile barrier.  The ring is 4 deep then (128 KB + red 1 KB + ks 12 KB).
-template <bool AKC, bool BKC, int EPI, typename TO, bool CS = false>
+// RS (weight gradients, A = dY k-major): the same kernel also sums every A row over K (the bias
+// gradient dY.sum(0) of the nn.Linear whose weight gradient this is): in workgroups of tile column 0,
+// wave (wm, wn) sums its row blocks s = 4 wn .. 4 wn + 3 from the A fragments it already holds,
+// partials -> rowsum_part[split][M].
+template <bool AKC, bool BKC, int EPI, typename TO, bool CS = false, bool RS = false>
 __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
   constexpr int NSLOT4 = CS ? 4 : ::NSLOT4;
   constexpr int LDS4 = CS ? (NSLOT4 * SLOT4 + 512 + CS_KMAX * 2) : NSLOT4 * SLOT4;
@@ -1056,6 +1061,13 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
   };
 
   f32x4 acc[8][8];           // defined by the first K-tile's MFMAs (mma16_acc0)
+  // RS: per-lane fp32 partial row sums (row 16 s + (lane & 15), k-block lane >> 4) of the wave's 4 row
+  // blocks, summed on the VALU from the A fragments already in registers (16 VALU per fragment, in the
+  // MFMA shadows).  An MFMA against a ones operand would need 8+ more VGPRs: at 256 VGPRs + 256 AGPRs
+  // the compiler then shuttles the asm-pinned accumulators through v_accvgpr_read/write, which the
+  // hazard recognizer cannot time against the opaque asm MFMAs (wrong results, measured).
+  const bool do_rs = RS && tn == 0;
+  float rsv[4] = {0.f, 0.f, 0.f, 0.f};
 
   // prologue: K-tiles 0 .. NSLOT4-1 staged; 0 and 1 retired
   for (int kt = 0; kt < NSLOT4; ++kt)
@@ -1126,6 +1138,19 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
       __builtin_amdgcn_sched_barrier(0);
       mma(s, 6);
       mma(s, 7);
+      // RS: row sums of this K-tile's A rows 16 s .. (lane & 15 -> row, every D column the same sum);
+      // compiler-visible MFMA (hazards against the VALU reads at the end are the compiler's)
+      if constexpr (RS) {
+        if (do_rs && (s >> 2) == wn) {
+          const u32x4 w = __builtin_bit_cast(u32x4, fa[H][s]);
+          float v = rsv[s & 3];
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            v += __builtin_bit_cast(float, w[q] << 16) + __builtin_bit_cast(float, w[q] & 0xFFFF0000u);
+          rsv[s & 3] = v;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
     // K-tile k + 2 retired (its fragments are read in the next K-tile); younger: k + 3 .. k + NSLOT4
     if (!TAIL) vm_wait_tiles(NSLOT4 - 2);
@@ -1164,6 +1189,16 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
   if (CS && do_cs) {                     // every K-tile folded in the loop (fold(k) in K-tile k)
     __syncthreads();
     for (int k = tid; k < g.K; k += NT4) g.colsum_part[(long)tm * g.K + k] = ks[k];
+  }
+  if (RS && do_rs) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {      // fold the 4 k-blocks (lane groups 16 apart), fixed order
+      float v = rsv[j];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      const int m = m0 + wm * 128 + 16 * (4 * wn + j) + lane;
+      if (lane < 16 && m < g.M) g.rowsum_part[(long)blockIdx.y * g.M + m] = v;
+    }
   }
   __syncthreads();
   big_epilogue<EPI, TO, 8, NT4>(g, acc, lds, m0, n0, tid, lane, wm, wn);
@@ -1254,7 +1289,62 @@ __global__ void __launch_bounds__(256) big_splitk_reduce(const float* __restrict
   *(f32x4*)c = o;
 }
 
+// db[m] += sum over splits of part[s][m] (fixed order: bitwise reproducible)
+__global__ void __launch_bounds__(256) rowsum_reduce(const float* __restrict__ part, int splits, int M, float* db) {
+  const int m = blockIdx.x * 256 + threadIdx.x;
+  if (m >= M) return;
+  float v = 0.f;
+  for (int s = 0; s < splits; ++s) v += part[(long)s * M + m];
+  db[m] += v;
+}
+
+// split count of the weight-gradient GEMM (fp32 slabs over K = tokens): the count that fills whole
+// waves of the CUs best with >= 2048-deep slices and slabs (+ extra fp32 elements per slab) within
+// ws_bytes: e.g. 36 tiles x 7 = 252 workgroups, 27 x 9 = 243, 9 x 28 = 252
+int wgrad_splits(int M, int N, int K, long ws_bytes, long extra) {
+  const int tiles = ((M + TM - 1) / TM) * ((N + TN - 1) / TN);
+  int splits = 1;
+  double best = 0.0;
+  for (int s = 1; s <= 64; ++s) {
+    if (K / s < 2048 || (long)s * ((long)M * N + extra) * 4 > ws_bytes) break;
+    const int wg = tiles * s, waves = (wg + 255) / 256;
+    const double eff = (double)wg / (waves * 256.0) * (wg >= 192 ? 1.0 : wg / 192.0);
+    if (eff > best + 1e-3) { best = eff; splits = s; }
+  }
+  return splits;
+}
+
 }  // namespace
+
+// Weight gradient with the bias gradient fused (gemm.hip eegf_gemm_wgrad_bias): C[M][N] = A^T B + beta C
+// over K tokens (A [K][M], B [K][N] bf16, both k-major), db[M] += A.sum(0), on the 4-wave kernel with
+// fp32 split-K slabs followed by the fixed-order slab and row-sum reductions.  Returns 1 when the shape
+// is not eligible (the caller then runs the plain GEMM and a column reduction).
+int eegf_gemm_big_wgrad_bias(int M, int N, int K, const void* A, long lda, const void* B, long ldb, float* C, long ldc,
+                             float beta, float* db, void* workspace, long ws_bytes, hipStream_t stream) {
+  if (K % BK != 0 || M % 8 != 0 || N % 8 != 0 || M < 256 || N < 256 || K < 4096) return 1;
+  if (lda % 8 || ldb % 8 || ldc % 4 || !workspace) return 1;
+  if ((((uintptr_t)A | (uintptr_t)B) & 15) != 0) return 1;
+  int splits = wgrad_splits(M, N, K, ws_bytes, M);
+  if ((splits > 1 ? (long)splits * ((long)M * N + M) : (long)M) * 4 > ws_bytes) return 1;
+  int ks = (K / splits + BK - 1) / BK * BK;
+  splits = (K + ks - 1) / ks;
+  float* slabs = (float*)workspace;
+  float* part = slabs + (splits > 1 ? (long)splits * M * N : 0);
+  BigArgs a{(const bf16*)A, (const bf16*)B, splits > 1 ? (void*)slabs : (void*)C, nullptr, nullptr, lda, ldb, ldc, 0,
+            M, N, K, 1.0f, beta, 1.0f, splits > 1 ? ks : 0, nullptr, 0, part};
+  const int tiles = ((M + TM - 1) / TM) * ((N + TN - 1) / TN);
+  hipLaunchKernelGGL((gemm4w_kernel<false, false, EPI_NONE, float, false, true>), dim3(tiles, splits), dim3(NT4), 0,
+                     stream, a);
+  if (splits > 1) {
+    const long MN = (long)M * N;
+    hipLaunchKernelGGL(big_splitk_reduce, dim3((unsigned)((MN / 4 + 255) / 256)), dim3(256), 0, stream,
+                       (const float*)slabs, splits, MN, N, C, ldc, beta);
+  }
+  hipLaunchKernelGGL(rowsum_reduce, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, stream, (const float*)part, splits,
+                     M, db);
+  return (int)hipGetLastError();
+}
 
 // Internal entry used by eegf_gemm (gemm.hip).  Returns 1 if the shape is not eligible.
 //   bf16 out: token-sized forward / input-gradient GEMMs (A K-contiguous), any beta;
@@ -1271,17 +1361,7 @@ int eegf_gemm_big(int a_kc, int b_kc, int epi, int out_f32, int M, int N, int K,
   if (a_colsum && (!a_kc || out_f32)) return 1;
   if (out_f32) {
     if (a_kc || b_kc || epi != EPI_NONE || M < 256 || N < 256 || K < 4096 || ldc % 4) return 1;
-    const int tiles = ((M + TM - 1) / TM) * ((N + TN - 1) / TN);
-    // pick the split count that fills whole waves of the 256 CUs best (>= 2048-deep slices, slabs
-    // within the workspace): e.g. 36 tiles x 7 = 252 workgroups, 27 x 9 = 243, 9 x 28 = 252
-    int splits = 1;
-    double best = 0.0;
-    for (int s = 1; s <= 64; ++s) {
-      if (K / s < 2048 || (long)s * M * N * 4 > ws_bytes) break;
-      const int wg = tiles * s, waves = (wg + 255) / 256;
-      const double eff = (double)wg / (waves * 256.0) * (wg >= 192 ? 1.0 : wg / 192.0);
-      if (eff > best + 1e-3) { best = eff; splits = s; }
-    }
+    int splits = wgrad_splits(M, N, K, ws_bytes, 0);
     if (splits == 1) return launch_big<false, false, EPI_NONE, float>(a, 1, stream);
     int ks = (K / splits + BK - 1) / BK * BK;
     splits = (K + ks - 1) / ks;

@@ -27,6 +27,7 @@ SIGNATURES: dict[str, list] = {
                   vp, i64, i64, vp, i64, i64, vp, i64, i64,
                   vp, i64, vp, i64, i64, f32, f32, f32, vp, i64, vp],
     "eegf_gemm_colsum_tiles": [i32, i32, i32, i32, i32, i32],
+    "eegf_gemm_wgrad_bias": [i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, f32, vp, vp, i64, vp],
     "eegf_gemm_acs": [i32, i32, i32, i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, vp, vp, i64, f32, f32, f32,
                       vp, vp],
     "eegf_tune": [i32, i32],

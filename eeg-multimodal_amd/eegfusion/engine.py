@@ -215,22 +215,48 @@ class FusionEngine:
                 self.colsum(part, N, tiles, N, bias_grad)
                 return out
             self.colsum(dy, ldd or N, M, N, bias_grad)
-        return self.gemm(dy, w, out, M, K, N, 1, 0, ldd or N, K, ldo or K, epi=epi, aux=aux, ldaux=ldaux,
-                         scale=scale, beta=beta)
+        ev = self._ev_start(tag)
+        self.gemm(dy, w, out, M, K, N, 1, 0, ldd or N, K, ldo or K, epi=epi, aux=aux, ldaux=ldaux, scale=scale,
+                  beta=beta)
+        self._ev_end(tag, ev, 2.0 * M * N * K)
+        return out
 
     def gbias(self, name):
         """gradient view to accumulate a bias gradient into, or None when not needed"""
         return self.G(name) if self.need(name) else None
 
-    def wgrad(self, dy, x, name, M, ldd=None, ldx=None):
-        if not self.need(name):
+    def wgrad(self, dy, x, name, M, ldd=None, ldx=None, bias=None, gw=None, gb=None):
+        """weight gradient g[N, K] += dy^T x over M rows; with `bias` (a parameter name) or `gb` (its
+        gradient view) the bias gradient dy.sum(0) is produced too — on the weight-gradient kernel
+        itself (eegf_gemm_wgrad_bias: row sums of the k-major dy by the MFMA) when the shape takes it,
+        else by a column reduction."""
+        if gb is None and bias is not None:
+            gb = self.gbias(bias)
+        if gw is None and not self.need(name):
+            if gb is not None:
+                self.bgrad(dy, bias, M, width=gb.numel(), ld=ldd, out=gb)
             return
-        g = self.G(name)
+        g = gw if gw is not None else self.G(name)
         N, K = g.shape
         if self.psn is not None:
             self._psn_linear(dy, x, M, N, K, ldd or N, ldx or K)
+            if gb is not None:
+                self._psn_bias(dy, M, N, ldd or N)
             return
+        ev = self._ev_start("wgrad" if M >= 4096 else None)
+        if gb is not None and _code(dy) == BF16 and _code(x) == BF16:
+            ws = self.ws.get("splitk", SPLITK_WS, torch.float32)
+            st = _lib.lib().eegf_gemm_wgrad_bias(BF16, N, K, M, P(dy), ldd or N, P(x), ldx or K, P(g), K, 1.0,
+                                                 P(gb), P(ws), ws.numel() * 4, _stream())
+            if st != 0 and st != _lib.ERR_ARG:
+                raise RuntimeError(f"eegf_gemm_wgrad_bias failed with status {st} (hipError)")
+            if st == 0:
+                self._ev_end("wgrad" if M >= 4096 else None, ev, 2.0 * M * N * K)
+                return
         self.gemm(dy, x, g, N, K, M, 0, 0, ldd or N, ldx or K, K, beta=1.0)
+        self._ev_end("wgrad" if M >= 4096 else None, ev, 2.0 * M * N * K)
+        if gb is not None:
+            self.colsum(dy, ldd or N, M, N, gb)
 
     def bgrad(self, dy, name, rows, width=None, ld=None, period=1, out=None):
         if out is None and not self.need(name):
@@ -670,33 +696,31 @@ class FusionEngine:
             s = t["layers"][i]
             dhn = self.ws.get(f"b_dh{i % 2}", R * HID, self.dt).view(R, HID)
             self.ln_bwd(dh, *s["ln2"], pre + "output.LayerNorm", R, dfo, da, pdrop, 1, sv.rng + 11 + 3 * i)
-            self.wgrad(dfo, s["ffact"], pre + "output.dense.weight", R)
+            # bias gradients ride on the weight-gradient GEMMs (eegf_gemm_wgrad_bias)
+            self.wgrad(dfo, s["ffact"], pre + "output.dense.weight", R, bias=pre + "output.dense.bias")
             self.dgrad(dfo, self.W(pre + "output.dense.weight"), dffp, R, epi=_lib.EPI_MUL_AUX, aux=s["ffgd"],
-                       bias_grad=self.gbias(pre + "output.dense.bias"), tag="dgrad_ffn2")
-            self.wgrad(dffp, s["a1"], pre + "intermediate.dense.weight", R)
-            self.dgrad(dffp, self.W(pre + "intermediate.dense.weight"), da, R, beta=1.0,
-                       bias_grad=self.gbias(pre + "intermediate.dense.bias"), tag="dgrad_cs")
+                       tag="dgrad_ffn2")
+            self.wgrad(dffp, s["a1"], pre + "intermediate.dense.weight", R, bias=pre + "intermediate.dense.bias")
+            self.dgrad(dffp, self.W(pre + "intermediate.dense.weight"), da, R, beta=1.0, tag="dgrad_ffn1")
             self.ln_bwd(da, *s["ln1"], pre + "attention.output.LayerNorm", R, dao, dhn, pdrop, 1, sv.rng + 10 + 3 * i)
-            self.wgrad(dao, s["ctx"], pre + "attention.output.dense.weight", R)
-            self.dgrad(dao, self.W(pre + "attention.output.dense.weight"), dctx, R,
-                       bias_grad=self.gbias(pre + "attention.output.dense.bias"), tag="dgrad_cs")
+            self.wgrad(dao, s["ctx"], pre + "attention.output.dense.weight", R,
+                       bias=pre + "attention.output.dense.bias")
+            self.dgrad(dao, self.W(pre + "attention.output.dense.weight"), dctx, R, tag="dgrad_out")
             ev = self._ev_start("attn_bwd")
             call("eegf_attn_bwd", self.code, B, NH, L, P(s["qkv"]), 3 * HID, P(t["kbias"]), scale, float(adrop),
                  self.cfg.seed, sv.rng + 12 + 3 * i, P(s["ctx"]), P(dctx), HID, P(s["lse"]), P(s["bits"]), P(dqkv),
                  P(dq_ws), _stream())
             self._ev_end("attn_bwd", ev, 2.5 * 4.0 * B * NH * L * L * DH)
             qn = pre + "attention.self.query.weight"
-            if self.need(qn) and self.psn is not None:
-                self._psn_linear(dqkv, s["h"], R, 3 * HID, HID, 3 * HID, HID)
-            elif self.need(qn):
-                gq = self.a.span(qn, 3, self.a.grad).view(3 * HID, HID)
-                self.gemm(dqkv, s["h"], gq, 3 * HID, HID, R, 0, 0, 3 * HID, HID, HID, beta=1.0)
             bn = pre + "attention.self.query.bias"
             gb = self.a.span(bn, 3, self.a.grad) if self.need(bn) else None
-            if i > lowest or lowest == 0:
-                self.dgrad(dqkv, self.Wspan(qn, 3).view(3 * HID, HID), dhn, R, beta=1.0, bias_grad=gb, tag="dgrad_cs")
+            if self.need(qn):
+                gq = self.a.span(qn, 3, self.a.grad).view(3 * HID, HID)
+                self.wgrad(dqkv, s["h"], qn, R, ldd=3 * HID, gw=gq, gb=gb)
             elif gb is not None:
                 self.bgrad(dqkv, bn, R, width=3 * HID, out=gb)
+            if i > lowest or lowest == 0:
+                self.dgrad(dqkv, self.Wspan(qn, 3).view(3 * HID, HID), dhn, R, beta=1.0, tag="dgrad_qkv")
             self._ready(lambda n, pre=pre: n.startswith(pre))
             dh = dhn
         if lowest > 0:

@@ -76,6 +76,17 @@ int eegf_gemm_colsum_tiles(int dtype, int out_dtype, int a_kcontig, int M, int N
 /* eegf_gemm (batch 1, no split-K) that also writes the column sums of A over each 256-row tile:
  * a_colsum [ceil(M/256)][K] fp32.  For an input-gradient GEMM (A = dY) these are the partial bias
  * gradients (nn.Linear bias.grad = dY.sum(0)), reduced with eegf_colsum over ceil(M/256) rows. */
+/* Weight gradient of an nn.Linear with its bias gradient fused (autograd of F.linear, the weight and
+ * bias grads of every BERT projection, modeling_bert.py:139-351): dW [M][N] = dY^T X + beta dW over
+ * K tokens, db [M] += dY.sum(0).  dY [K][M] (row stride ldd) and X [K][N] (ldx) bf16; dW, db fp32.
+ * The row sums ride on the weight-gradient kernel (4 MFMAs per K-tile against a ones operand in the
+ * workgroups of tile column 0) and are reduced in a fixed order.  workspace: fp32 split-K slabs
+ * (splits x (M*N + M) floats).  EEGF_ERR_ARG when the shape is not eligible (bf16, M, N >= 256,
+ * K >= 4096, K % 64 == 0, 8-aligned dims, 16-B aligned dY / X, workspace too small): run eegf_gemm and
+ * eegf_colsum instead. */
+int eegf_gemm_wgrad_bias(int dtype, int M, int N, int K, const void* dY, long ldd, const void* X, long ldx,
+                         float* dW, long ldw, float beta, float* db, void* workspace, long ws_bytes,
+                         hipStream_t stream);
 int eegf_gemm_acs(int dtype, int out_dtype, int a_kcontig, int b_kcontig, int epi, int M, int N, int K,
                   const void* A, long lda, const void* B, long ldb, void* C, long ldc, const float* bias,
                   void* aux, long ldaux, float alpha, float beta, float epi_scale, float* a_colsum,

@@ -443,3 +443,51 @@ def test_gemm_big_4wave_wgrad(M, N, K):
         assert err <= 2e-3, err
     finally:
         _tune(1, old)
+
+
+@pytest.mark.parametrize("M,N,K,ws_mb", [(2304, 768, 65536, 96), (3072, 768, 65536, 96), (768, 3072, 65536, 96),
+                                         (768, 768, 4096, 96), (2312, 776, 8192, 96), (768, 768, 8192, 2)])
+def test_gemm_wgrad_bias(M, N, K, ws_mb):
+    """eegf_gemm_wgrad_bias: weight gradient dY^T X (+ dW, beta 1) with the bias gradient dY.sum(0)
+    summed by the same kernel (ones-operand MFMAs in tile column 0), split-K slabs (ws 96 MB) and one
+    slice (ws 2 MB), ragged M / N, fixed-order reductions (bitwise repeatable)."""
+    from eegfusion import _lib
+    torch.manual_seed(5)
+    dy = torch.randn(K, M, device="cuda").to(torch.bfloat16)           # [tokens, out features]
+    x = torch.randn(K, N, device="cuda").to(torch.bfloat16)            # [tokens, in features]
+    dw0 = torch.randn(M, N, device="cuda")
+    db0 = torch.randn(M, device="cuda")
+    ws = torch.empty(ws_mb << 18, device="cuda")
+    outs = []
+    for _ in range(2):
+        dw, db = dw0.clone(), db0.clone()
+        _lib.call("eegf_gemm_wgrad_bias", _lib.BF16, M, N, K, dy.data_ptr(), M, x.data_ptr(), N, dw.data_ptr(), N,
+                  1.0, db.data_ptr(), ws.data_ptr(), ws.numel() * 4, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        outs.append((dw, db))
+    ref = dy.double().t() @ x.double() + dw0.double()
+    err_w = ((outs[0][0].double() - ref).abs().max() / ref.abs().max()).item()
+    assert err_w < 2e-5, err_w                        # fp32 accumulation of exact bf16 products
+    bref = dy.double().sum(0) + db0.double()
+    err_b = ((outs[0][1].double() - bref).abs().max() / bref.abs().max()).item()
+    assert err_b < 2e-5, err_b
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+def test_gemm_wgrad_bias_ineligible():
+    """shapes off the 4-wave path return EEGF_ERR_ARG without launching (the engine then runs the
+    plain GEMM and a column reduction)."""
+    from eegfusion import _lib
+    dy = torch.zeros(2048, 768, device="cuda", dtype=torch.bfloat16)
+    x = torch.zeros(2048, 768, device="cuda", dtype=torch.bfloat16)
+    dw = torch.zeros(768, 768, device="cuda")
+    db = torch.zeros(768, device="cuda")
+    ws = torch.empty(1 << 20, device="cuda")
+    st = _lib.lib().eegf_gemm_wgrad_bias(_lib.BF16, 768, 768, 2048, dy.data_ptr(), 768, x.data_ptr(), 768,
+                                         dw.data_ptr(), 768, 1.0, db.data_ptr(), ws.data_ptr(), ws.numel() * 4,
+                                         torch.cuda.current_stream().cuda_stream)
+    assert st == _lib.ERR_ARG                           # K = 2048 tokens < 4096
+    st = _lib.lib().eegf_gemm_wgrad_bias(_lib.F32, 768, 768, 8192, dy.data_ptr(), 768, x.data_ptr(), 768,
+                                         dw.data_ptr(), 768, 1.0, db.data_ptr(), ws.data_ptr(), ws.numel() * 4,
+                                         torch.cuda.current_stream().cuda_stream)
+    assert st == _lib.ERR_ARG

@@ -27,9 +27,15 @@ ROOT = Path(__file__).resolve().parents[1]
 N_SIMD = 1024
 
 # bench.py roofline groups -> kernel-name fragments (mangled or demangled) + grid filters
-GROUPS = {
+GROUPS = {     # bf16 instantiations appear mangled in rocprofv3's CSV (DF16b), the others demangled
     "dgrad_cs": ("gemm8_kernelILb1ELb0ELi0EDF16bLi4ELb1E",),
     "ffn1_fwd": ("gemm8_kernelILb1ELb1ELi2EDF16bLi4E", "gemm8_kernelILb1ELb1ELi8EDF16bLi4E"),
+    "qkv_fwd": ("gemm8_kernelILb1ELb1ELi1EDF16bLi4E",),
+    "ffn2_fwd": ("gemm4w_kernelILb1ELb1ELi1EDF16bLb0E",),
+    "dgrad_qkv_ffn1": ("gemm4w_kernelILb1ELb0ELi0EDF16bLb0ELb0E",),
+    "dgrad_out": ("gemm8_kernelILb1ELb0ELi0EDF16bLi4ELb0E",),
+    "dgrad_ffn2": ("gemm8_kernelILb1ELb0ELi9EDF16bLi4E",),
+    "wgrad": ("gemm4w_kernel<false, false, 0, float, false", "gemm4w_kernelILb0ELb0ELi0EfLb0E"),
     "attn_fwd": ("attn_fwd256_kernel",),
     "attn_bwd": ("attn_bwd_kernel", "attn_bwd256_kernel"),
 }
