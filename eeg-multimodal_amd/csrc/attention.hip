@@ -30,6 +30,7 @@ struct AttnArgs {
   int B, H, L; long ld_qkv, ld_out; float scale;
   float p; uint64_t seed, offset;   // attention-probability dropout (p = 0: off)
   uint32_t* bits;                   // dropout keep bits: written by the forward, read by the backward
+  const int* cu;                    // varlen (packed rows): sequence b = rows cu[b] .. cu[b+1]-1, L = max length
 };
 
 // Dropout mask of the probabilities P[q][key] of head (b,h): element ((b*H+h)*L + q)*L + key of
@@ -106,7 +107,28 @@ DEV void stage_rows(T* lds, int ldl, const T* g, long ld, int rows, int tid) {
   }
 }
 
-template <typename T>
+// stage_rows for a ragged tail: rows >= valid are zero-filled (valid may be <= 0: all zero)
+template <typename T, int NTHR>
+DEV void stage_rows_vl(T* lds, int ldl, const T* g, long ld, int rows, int valid, int tid) {
+  constexpr int VE = 16 / (int)sizeof(T);
+  constexpr int CPR = DH / VE;
+  for (int c = tid; c < rows * CPR; c += NTHR) {
+    const int r = c / CPR, cc = (c % CPR) * VE;
+    st16(lds + r * ldl + cc, r < valid ? ld16(g + (long)r * ld + cc) : u32x4{0u, 0u, 0u, 0u});
+  }
+}
+
+// Sequence b of the launch: first row and length.  Dense: rows b*L .., length L.  Varlen (a.cu): the
+// packed rows cu[b] .. cu[b+1]-1 (flash-attn cu_seqlens); the dropout element index keeps the padded
+// (b, h, q, key) numbering with L = the padded length, so a packed batch draws the masks of its
+// padded form.
+template <bool VL>
+DEV void attn_seq(const AttnArgs& a, int b, long& row0, int& len) {
+  if (VL) { row0 = a.cu[b]; len = a.cu[b + 1] - a.cu[b]; }
+  else { row0 = (long)b * a.L; len = a.L; }
+}
+
+template <typename T, bool VL = false>
 __global__ void __launch_bounds__(512) attn_fwd_kernel(AttnArgs a) {
   using F = typename Frag8<T>::type;
   constexpr int KT = 64, LDK = DH + pad16<T>();
@@ -115,15 +137,20 @@ __global__ void __launch_bounds__(512) attn_fwd_kernel(AttnArgs a) {
   T* Vs = lds + KT * LDK;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, li = lane & 15;
   const int b = blockIdx.z, h = blockIdx.y;
+  long row0;
+  int len;
+  attn_seq<VL>(a, b, row0, len);
+  if (VL && (int)blockIdx.x * 128 >= len) return;                   // uniform: past this sequence
   const int q = blockIdx.x * 128 + wave * 16 + li;                  // this lane's query (B/C column)
-  const T* base = (const T*)a.qkv + (long)b * a.L * a.ld_qkv;
+  const T* base = (const T*)a.qkv + row0 * a.ld_qkv;
   const T* Qg = base + h * DH;
   const T* Kg = base + 768 + h * DH;
   const T* Vg = base + 1536 + h * DH;
+  const int qr = VL ? min(q, len - 1) : q;                          // ragged tail: clamped, never stored
 
   F qf[2];
 #pragma unroll
-  for (int c = 0; c < 2; ++c) qf[c] = ld_row8(Qg + (long)q * a.ld_qkv + 32 * c + 8 * g);
+  for (int c = 0; c < 2; ++c) qf[c] = ld_row8(Qg + (long)qr * a.ld_qkv + 32 * c + 8 * g);
 
   f32x4 o[4];
 #pragma unroll
@@ -133,10 +160,15 @@ __global__ void __launch_bounds__(512) attn_fwd_kernel(AttnArgs a) {
   const uint32_t thr = thr16_of(a.p);
   const float dscale = 1.0f / (1.0f - a.p);
 
-  for (int k0 = 0; k0 < a.L; k0 += KT) {
+  for (int k0 = 0; k0 < len; k0 += KT) {
     __syncthreads();
-    stage_rows<T, 512>(Ks, LDK, Kg + (long)k0 * a.ld_qkv, a.ld_qkv, KT, tid);
-    stage_rows<T, 512>(Vs, LDK, Vg + (long)k0 * a.ld_qkv, a.ld_qkv, KT, tid);
+    if (VL && k0 + KT > len) {
+      stage_rows_vl<T, 512>(Ks, LDK, Kg + (long)k0 * a.ld_qkv, a.ld_qkv, KT, len - k0, tid);
+      stage_rows_vl<T, 512>(Vs, LDK, Vg + (long)k0 * a.ld_qkv, a.ld_qkv, KT, len - k0, tid);
+    } else {
+      stage_rows<T, 512>(Ks, LDK, Kg + (long)k0 * a.ld_qkv, a.ld_qkv, KT, tid);
+      stage_rows<T, 512>(Vs, LDK, Vg + (long)k0 * a.ld_qkv, a.ld_qkv, KT, tid);
+    }
     __syncthreads();
     f32x4 s[4];
 #pragma unroll
@@ -153,6 +185,7 @@ __global__ void __launch_bounds__(512) attn_fwd_kernel(AttnArgs a) {
       for (int r = 0; r < 4; ++r) {
         float v = s[f][r] * a.scale;
         if (kb) v += kb[k0 + 16 * f + 4 * g + r];
+        if (VL && k0 + 16 * f + 4 * g + r >= len) v = NEG;           // keys past the sequence
         s[f][r] = v;
         tmax = fmaxf(tmax, v);
       }
@@ -190,7 +223,8 @@ __global__ void __launch_bounds__(512) attn_fwd_kernel(AttnArgs a) {
   l += __shfl_xor(l, 16, 64);
   l += __shfl_xor(l, 32, 64);
   const float inv = 1.0f / l;
-  T* out = (T*)a.out + ((long)b * a.L + q) * a.ld_out + h * DH;
+  if (VL && q >= len) return;
+  T* out = (T*)a.out + (row0 + q) * a.ld_out + h * DH;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     // o[e][r]: d = 16e + 4g + r
@@ -200,7 +234,7 @@ __global__ void __launch_bounds__(512) attn_fwd_kernel(AttnArgs a) {
   if (g == 0) a.lse[((long)b * a.H + h) * a.L + q] = m + __logf(l);
 }
 
-template <typename T>
+template <typename T, bool VL = false>
 __global__ void __launch_bounds__(512) attn_bwd_kernel(AttnArgs a) {
   using F = typename Frag8<T>::type;
   constexpr int KB = 256, QC = 32, LDK = DH + pad16<T>(), LDS_ = KB + pad16<T>();
@@ -215,16 +249,22 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(AttnArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, li = lane & 15;
   const int b = blockIdx.z, h = blockIdx.y, kb0 = blockIdx.x * KB;
+  long row0;
+  int len;
+  attn_seq<VL>(a, b, row0, len);
+  if (VL && kb0 >= len) return;                                     // uniform: past this sequence
   const int kw0 = kb0 + wave * 32;                                    // this wave's 32 keys
-  const T* base = (const T*)a.qkv + (long)b * a.L * a.ld_qkv;
+  const T* base = (const T*)a.qkv + row0 * a.ld_qkv;
   const T* Qg = base + h * DH;
   const T* Kg = base + 768 + h * DH;
   const T* Vg = base + 1536 + h * DH;
-  const T* Og = (const T*)a.o + (long)b * a.L * a.ld_out + h * DH;
-  const T* dOg = (const T*)a.dout + (long)b * a.L * a.ld_out + h * DH;
+  const T* Og = (const T*)a.o + row0 * a.ld_out + h * DH;
+  const T* dOg = (const T*)a.dout + row0 * a.ld_out + h * DH;
   const float* lse = a.lse + ((long)b * a.H + h) * a.L;
   const float* kbias = a.kbias ? a.kbias + (long)b * a.L : nullptr;
-  const int nkb = a.L / KB;
+  // dQ: one key block per sequence -> plain stores; varlen always sums through dq_acc when any
+  // sequence may span two blocks (L > 256), so every row of the launch takes one path
+  const int nkb = VL ? (a.L > KB ? 2 : 1) : a.L / KB;
   const uint32_t thr = thr16_of(a.p);
   const float dscale = 1.0f / (1.0f - a.p);
 
@@ -234,12 +274,16 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(AttnArgs a) {
   for (int f = 0; f < 2; ++f)
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-      kf[f][c] = ld_row8(Kg + (long)(kw0 + 16 * f + li) * a.ld_qkv + 32 * c + 8 * g);
-      vf[f][c] = ld_row8(Vg + (long)(kw0 + 16 * f + li) * a.ld_qkv + 32 * c + 8 * g);
+      const int kr = VL ? min(kw0 + 16 * f + li, len - 1) : kw0 + 16 * f + li;
+      kf[f][c] = ld_row8(Kg + (long)kr * a.ld_qkv + 32 * c + 8 * g);
+      vf[f][c] = ld_row8(Vg + (long)kr * a.ld_qkv + 32 * c + 8 * g);
     }
   float kbv[2];
 #pragma unroll
-  for (int f = 0; f < 2; ++f) kbv[f] = kbias ? kbias[kw0 + 16 * f + li] : 0.f;
+  for (int f = 0; f < 2; ++f) {
+    kbv[f] = kbias ? kbias[kw0 + 16 * f + li] : 0.f;
+    if (VL && kw0 + 16 * f + li >= len) kbv[f] = NEG;              // keys past the sequence: p = 0
+  }
 
   f32x4 dk[2][4], dv[2][4];
 #pragma unroll
@@ -247,14 +291,21 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(AttnArgs a) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) { dk[f][e] = f32x4{0, 0, 0, 0}; dv[f][e] = f32x4{0, 0, 0, 0}; }
 
-  stage_rows<T, 512>(Ks, LDK, Kg + (long)kb0 * a.ld_qkv, a.ld_qkv, KB, tid);
+  if (VL) stage_rows_vl<T, 512>(Ks, LDK, Kg + (long)kb0 * a.ld_qkv, a.ld_qkv, KB, len - kb0, tid);
+  else stage_rows<T, 512>(Ks, LDK, Kg + (long)kb0 * a.ld_qkv, a.ld_qkv, KB, tid);
 
-  for (int q0 = 0; q0 < a.L; q0 += QC) {
+  for (int q0 = 0; q0 < len; q0 += QC) {
     __syncthreads();
-    stage_rows<T, 512>(Qs, LDK, Qg + (long)q0 * a.ld_qkv, a.ld_qkv, QC, tid);
-    stage_rows<T, 512>(dOs, LDK, dOg + (long)q0 * a.ld_out, a.ld_out, QC, tid);
-    stage_rows<T, 512>(Os, LDK, Og + (long)q0 * a.ld_out, a.ld_out, QC, tid);
-    if (tid < QC) lse_s[tid] = lse[q0 + tid];
+    if (VL) {      // rows past the sequence zero-filled: they add nothing to dK / dV
+      stage_rows_vl<T, 512>(Qs, LDK, Qg + (long)q0 * a.ld_qkv, a.ld_qkv, QC, len - q0, tid);
+      stage_rows_vl<T, 512>(dOs, LDK, dOg + (long)q0 * a.ld_out, a.ld_out, QC, len - q0, tid);
+      stage_rows_vl<T, 512>(Os, LDK, Og + (long)q0 * a.ld_out, a.ld_out, QC, len - q0, tid);
+    } else {
+      stage_rows<T, 512>(Qs, LDK, Qg + (long)q0 * a.ld_qkv, a.ld_qkv, QC, tid);
+      stage_rows<T, 512>(dOs, LDK, dOg + (long)q0 * a.ld_out, a.ld_out, QC, tid);
+      stage_rows<T, 512>(Os, LDK, Og + (long)q0 * a.ld_out, a.ld_out, QC, tid);
+    }
+    if (tid < QC) lse_s[tid] = (!VL || q0 + tid < len) ? lse[q0 + tid] : 0.f;
     __syncthreads();
     {  // D[q] = sum_d dO[q,d] O[q,d]: 16 lanes per query
       const int qq = tid >> 4, part = tid & 15;
@@ -296,7 +347,8 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(AttnArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int qi = 16 * qf + 4 * g + r;
-          const float pv = __expf(s[r] * a.scale + kbv[f] - lse_s[qi]);
+          float pv = __expf(s[r] * a.scale + kbv[f] - lse_s[qi]);
+          if (VL && q0 + qi >= len) pv = 0.f;                          // query rows past the sequence
           const float mk = (m8[f] >> (4 * qf + r)) & 1u ? dscale : 0.f;
           s[r] = pv * mk;
           dp[r] = pv * (dp[r] * mk - dd_s[qi]);
@@ -335,15 +387,16 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(AttnArgs a) {
       // acc[r]: q = q0 + 16qf + 4g + r, d = 16e + li
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const long qrow = (long)b * a.L + q0 + 16 * qf + 4 * g + r;
+        if (VL && q0 + 16 * qf + 4 * g + r >= len) continue;
+        const long qrow = row0 + q0 + 16 * qf + 4 * g + r;
         const int d = 16 * e + li;
         if (nkb == 1) ((T*)a.dqkv)[qrow * a.ld_qkv + h * DH + d] = from_f32<T>(acc[r] * a.scale);
         else atomicAdd(a.dq_acc + qrow * 768 + h * DH + d, acc[r] * a.scale);
       }
     }
   }
-  // write dK, dV: dk[f][e][r]: key = kw0 + 16f + 4g + r ... wait: rows of dK acc = keys? (see note)
-  T* dqkv = (T*)a.dqkv + (long)b * a.L * a.ld_qkv;
+  // write dK, dV: dk[f][e][r] / dv[f][e][r] hold key kw0 + 16f + 4g + r, d = 16e + li
+  T* dqkv = (T*)a.dqkv + row0 * a.ld_qkv;
 #pragma unroll
   for (int f = 0; f < 2; ++f)
 #pragma unroll
@@ -351,6 +404,7 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(AttnArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const long key = kw0 + 16 * f + 4 * g + r;
+        if (VL && key >= len) continue;
         const int d = 16 * e + li;
         dqkv[key * a.ld_qkv + 768 + h * DH + d] = from_f32<T>(dk[f][e][r] * a.scale);
         dqkv[key * a.ld_qkv + 1536 + h * DH + d] = from_f32<T>(dv[f][e][r]);
@@ -444,6 +498,61 @@ extern "C" int eegf_attn_bwd(int dtype, int B, int H, int L, const void* qkv, lo
     const long n = (long)B * L * 768;
     hipLaunchKernelGGL(dq_convert_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, dq_workspace, dqkv,
                        dtype == EEGF_BF16, (long)B * L, ld_qkv);
+  }
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Varlen (packed) self-attention for contract T pad skipping: the padded keys of
+// BertSelfAttention are masked (model.py:43, modeling_bert.py extended mask), so the packed rows of
+// each sequence give the real rows' outputs of the padded computation exactly.
+extern "C" int eegf_attn_varlen_fwd(int dtype, int B, int H, int max_len, const int* cu_seqlens, long packed_rows,
+                                    long total_rows, const void* qkv, long ld_qkv, float scale, float drop_p,
+                                    unsigned long long seed, unsigned long long offset, void* out, long ld_out,
+                                    float* lse, hipStream_t stream) {
+  if (B <= 0 || B > 65535 || H != 12 || max_len <= 0 || !cu_seqlens || !qkv || !out || !lse) return EEGF_ERR_ARG;
+  if (ld_qkv < 2304 || ld_out < 768 || drop_p < 0.f || drop_p >= 1.f || packed_rows < 0 || total_rows < packed_rows)
+    return EEGF_ERR_ARG;
+  const size_t es = dtype == EEGF_BF16 ? 2 : dtype == EEGF_F32 ? 4 : 0;
+  if (!es) return EEGF_ERR_ARG;
+  if (total_rows > packed_rows)        // rows past the packed sequences: defined zeros
+    hipMemsetAsync((char*)out + packed_rows * ld_out * es, 0, (total_rows - packed_rows) * ld_out * es, stream);
+  AttnArgs a{qkv, out, lse, nullptr, nullptr, nullptr, nullptr, nullptr, B, H, max_len, ld_qkv, ld_out, scale,
+             drop_p, seed, offset, nullptr, cu_seqlens};
+  const dim3 grid((max_len + 127) / 128, H, B);
+  if (dtype == EEGF_F32) hipLaunchKernelGGL((attn_fwd_kernel<float, true>), grid, dim3(512), 0, stream, a);
+  else hipLaunchKernelGGL((attn_fwd_kernel<bf16, true>), grid, dim3(512), 0, stream, a);
+  return (int)hipGetLastError();
+}
+
+extern "C" long eegf_attn_varlen_bwd_workspace(long total_rows, int max_len) {
+  return max_len > 256 ? total_rows * 768 : 0;
+}
+
+extern "C" int eegf_attn_varlen_bwd(int dtype, int B, int H, int max_len, const int* cu_seqlens, long packed_rows,
+                                    long total_rows, const void* qkv, long ld_qkv, float scale, float drop_p,
+                                    unsigned long long seed, unsigned long long offset, const void* out,
+                                    const void* dout, long ld_out, const float* lse, void* dqkv, float* dq_workspace,
+                                    hipStream_t stream) {
+  if (B <= 0 || B > 65535 || H != 12 || max_len <= 0 || !cu_seqlens || !qkv || !out || !dout || !lse || !dqkv)
+    return EEGF_ERR_ARG;
+  if (ld_qkv < 2304 || ld_out < 768 || drop_p < 0.f || drop_p >= 1.f || packed_rows < 0 || total_rows < packed_rows)
+    return EEGF_ERR_ARG;
+  if (max_len > 256 && !dq_workspace) return EEGF_ERR_ARG;
+  const size_t es = dtype == EEGF_BF16 ? 2 : dtype == EEGF_F32 ? 4 : 0;
+  if (!es) return EEGF_ERR_ARG;
+  if (total_rows > packed_rows)
+    hipMemsetAsync((char*)dqkv + packed_rows * ld_qkv * es, 0, (total_rows - packed_rows) * ld_qkv * es, stream);
+  if (max_len > 256) hipMemsetAsync(dq_workspace, 0, sizeof(float) * (size_t)total_rows * 768, stream);
+  AttnArgs a{qkv, nullptr, const_cast<float*>(lse), nullptr, out, dout, dqkv, dq_workspace, B, H, max_len, ld_qkv,
+             ld_out, scale, drop_p, seed, offset, nullptr, cu_seqlens};
+  const dim3 grid((max_len + 255) / 256, H, B);
+  if (dtype == EEGF_F32) hipLaunchKernelGGL((attn_bwd_kernel<float, true>), grid, dim3(512), 0, stream, a);
+  else hipLaunchKernelGGL((attn_bwd_kernel<bf16, true>), grid, dim3(512), 0, stream, a);
+  if (max_len > 256) {
+    const long n = total_rows * 768;
+    hipLaunchKernelGGL(dq_convert_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, dq_workspace, dqkv,
+                       dtype == EEGF_BF16, total_rows, ld_qkv);
   }
   return (int)hipGetLastError();
 }

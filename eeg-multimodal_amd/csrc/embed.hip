@@ -5,7 +5,9 @@
 // per (b, 64-step tile) reads the tile coalesced along time into LDS and writes it coalesced along
 // channels (cast to the compute dtype) — the input of the eeg_encoder GEMM.
 // Contract T (token ids, model.py / train.py): word-embedding gather feeding BertEmbeddings
-// (modeling_bert.py:95-105) and its scatter-add backward.
+// (modeling_bert.py:95-105) and its scatter-add backward; the varlen (pad-skipping) front-end: per-row
+// lengths of the attention mask, the packed embedding gather (word + position rows of the real
+// tokens only) and the padded <-> packed row moves around the BERT stack.
 #include "common.h"
 #include "eegfusion_internal.h"
 
@@ -46,7 +48,107 @@ __global__ void __launch_bounds__(256) scatter_add_kernel(const long long* __res
   for (int c = threadIdx.x & 63; c < width; c += 64) atomicAdd(dst + c, to_f32(d[row * width + c]));
 }
 
+// lens[b] = number of nonzero mask entries of row b; *nonprefix |= 1 when a row is not of the form
+// [1]*n + [0]*(L-n) (BertTokenizer right padding, get_embedding.py:115): the packed path needs it
+__global__ void __launch_bounds__(64) seq_lengths_kernel(const long long* __restrict__ mask, int L, int* lens,
+                                                        int* nonprefix) {
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const long long* m = mask + (long)b * L;
+  int n = 0;
+  for (int j = lane; j < L; j += 64) n += m[j] != 0;
+  n = wave_sum_i(n);
+  int bad = 0;
+  for (int j = lane; j < L; j += 64) bad |= (m[j] != 0) != (j < n);
+  bad = wave_sum_i(bad);
+  if (lane == 0) {
+    lens[b] = n;
+    if (bad) atomicOr(nonprefix, 1);
+  }
+}
+
+// packed row cu[b] + j (j < len_b) = word[ids[b, j]] + pos[j] (fp32 sum, one rounding to T);
+// ids_packed[row] = ids[b, j].  4 rows (b, j) per block, 64 threads per row.
+template <typename T>
+__global__ void __launch_bounds__(256) varlen_embed_kernel(const int* __restrict__ cu, const long long* __restrict__ ids,
+                                                           int L, int width, const float* __restrict__ word,
+                                                           const float* __restrict__ pos, T* __restrict__ out,
+                                                           long long* __restrict__ ids_packed) {
+  const int b = blockIdx.y, j = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int len = cu[b + 1] - cu[b];
+  if (j >= len || j >= L) return;
+  const long row = cu[b] + j;
+  const long long id = ids[(long)b * L + j];
+  const float* w = word + id * width;
+  const float* p = pos + (long)j * width;
+  for (int c = threadIdx.x & 63; c < width; c += 64) out[row * width + c] = from_f32<T>(w[c] + p[c]);
+  if ((threadIdx.x & 63) == 0) ids_packed[row] = id;
+}
+
+// padded [B, S, width] <-> packed rows: to_padded: dst[b*S + j] = j < len_b ? src[cu[b] + j] : 0;
+// else dst[cu[b] + j] = src[b*S + j] for j < len_b.  16-B chunks, 4 rows per block.
+__global__ void __launch_bounds__(256) varlen_rows_kernel(const int* __restrict__ cu, int S, int chunks,
+                                                          const char* __restrict__ src, long ld_src,
+                                                          char* __restrict__ dst, long ld_dst, int to_padded) {
+  const int b = blockIdx.y, j = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (j >= S) return;
+  const int len = cu[b + 1] - cu[b];
+  const long prow = (long)b * S + j, qrow = (long)cu[b] + j;
+  if (to_padded) {
+    char* d = dst + prow * ld_dst;
+    for (int c = threadIdx.x & 63; c < chunks; c += 64)
+      st16(d + 16 * c, j < len ? ld16(src + qrow * ld_src + 16 * c) : u32x4{0u, 0u, 0u, 0u});
+  } else if (j < len) {
+    char* d = dst + qrow * ld_dst;
+    for (int c = threadIdx.x & 63; c < chunks; c += 64) st16(d + 16 * c, ld16(src + prow * ld_src + 16 * c));
+  }
+}
+
 }  // namespace
+
+extern "C" int eegf_seq_lengths(int B, int L, const long long* mask, int* lens, int* nonprefix, hipStream_t stream) {
+  if (B <= 0 || L <= 0 || !mask || !lens || !nonprefix) return EEGF_ERR_ARG;
+  hipMemsetAsync(nonprefix, 0, sizeof(int), stream);
+  hipLaunchKernelGGL(seq_lengths_kernel, dim3(B), dim3(64), 0, stream, mask, L, lens, nonprefix);
+  return (int)hipGetLastError();
+}
+
+extern "C" int eegf_varlen_embed(int dtype, int B, int L, int width, const int* cu_seqlens, long packed_rows,
+                                 long total_rows, const long long* ids, const float* word, const float* pos, void* out,
+                                 long long* ids_packed, hipStream_t stream) {
+  if (B <= 0 || B > 65535 || L <= 0 || width <= 0 || !cu_seqlens || !ids || !word || !pos || !out || !ids_packed ||
+      packed_rows < 0 || total_rows < packed_rows)
+    return EEGF_ERR_ARG;
+  const size_t es = dtype == EEGF_BF16 ? 2 : dtype == EEGF_F32 ? 4 : 0;
+  if (!es) return EEGF_ERR_ARG;
+  if (total_rows > packed_rows) {      // pad rows: zero inputs, token id 0 (their gradients are zero)
+    hipMemsetAsync((char*)out + packed_rows * width * es, 0, (total_rows - packed_rows) * width * es, stream);
+    hipMemsetAsync(ids_packed + packed_rows, 0, (total_rows - packed_rows) * sizeof(long long), stream);
+  }
+  const dim3 grid((L + 3) / 4, B);
+  if (dtype == EEGF_F32)
+    hipLaunchKernelGGL(varlen_embed_kernel<float>, grid, dim3(256), 0, stream, cu_seqlens, ids, L, width, word, pos,
+                       (float*)out, ids_packed);
+  else
+    hipLaunchKernelGGL(varlen_embed_kernel<bf16>, grid, dim3(256), 0, stream, cu_seqlens, ids, L, width, word, pos,
+                       (bf16*)out, ids_packed);
+  return (int)hipGetLastError();
+}
+
+extern "C" int eegf_varlen_rows(int dtype, int B, int S, int width, const int* cu_seqlens, long packed_rows,
+                                long total_rows, const void* src, long ld_src, void* dst, long ld_dst, int to_padded,
+                                hipStream_t stream) {
+  const size_t es = dtype == EEGF_BF16 ? 2 : dtype == EEGF_F32 ? 4 : 0;
+  if (!es || B <= 0 || B > 65535 || S <= 0 || width <= 0 || (width * es) % 16 || !cu_seqlens || !src || !dst)
+    return EEGF_ERR_ARG;
+  if ((ld_src * es) % 16 || (ld_dst * es) % 16 || ((uintptr_t)src | (uintptr_t)dst) % 16) return EEGF_ERR_ARG;
+  if (!to_padded && total_rows > packed_rows)       // packed rows past the sequences: defined zeros
+    hipMemset2DAsync((char*)dst + packed_rows * ld_dst * es, ld_dst * es, 0, width * es, total_rows - packed_rows,
+                     stream);
+  const dim3 grid((S + 3) / 4, B);
+  hipLaunchKernelGGL(varlen_rows_kernel, grid, dim3(256), 0, stream, cu_seqlens, S, (int)(width * es / 16),
+                     (const char*)src, (long)(ld_src * es), (char*)dst, (long)(ld_dst * es), to_padded);
+  return (int)hipGetLastError();
+}
 
 extern "C" int eegf_window_tokens(int dtype, int B, int C, int T, const float* eeg, void* tokens, hipStream_t stream) {
   if (B <= 0 || C <= 0 || C > 128 || T <= 0 || !eeg || !tokens || B > 65535) return EEGF_ERR_ARG;

@@ -68,8 +68,77 @@ class MultiModalDataset_ti(Dataset):
         return (video_feature, mask, input_ids, attention_mask), label
 
 
+class DeviceBatchLoader:
+    """Batched loader for a map-style dataset such as MultiModalDataset_ti.
+
+    The reference collates sample by sample on the host and copies every batch to the device
+    (data.py:22-34 + DataLoader default collate, train.py:96-98).  Here the split is collated ONCE
+    (the feature files are tens of MB), staged through pinned host memory, and kept resident in HBM;
+    each batch is a device-side row gather of the epoch permutation — no per-sample Python and no
+    per-step host-to-device copy.  Batches have the structure, shapes and dtypes of
+    DataLoader(dataset, batch_size, shuffle) with the default collate, and with shuffle=True the
+    sample order is the one RandomSampler draws from the same global torch RNG state (one int64 seed
+    draw per epoch after the iterator's base-seed draw, then randperm on a CPU generator), so a seeded
+    run sees the reference's batches and leaves the global RNG where DataLoader leaves it."""
+
+    def __init__(self, dataset, batch_size, shuffle=True, device=None, drop_last=False):
+        self.batch_size, self.shuffle, self.drop_last = int(batch_size), bool(shuffle), bool(drop_last)
+        self.n = len(dataset)
+        self.device = torch.device(device) if device is not None else (
+            torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu"))
+        items = [dataset[i] for i in range(self.n)]
+        collate = torch.utils.data.default_collate
+        host = collate(items)                                   # ((f, m, ids, mask), label) stacked
+        pin = self.device.type == "cuda"
+
+        def stage(t):
+            t = t.contiguous()
+            if pin:
+                t = t.pin_memory()
+            return t.to(self.device, non_blocking=pin)
+
+        self.data = _tree_map(stage, host)
+        if pin:
+            torch.cuda.current_stream(self.device).synchronize()
+
+    def __len__(self):
+        return self.n // self.batch_size if self.drop_last else (self.n + self.batch_size - 1) // self.batch_size
+
+    def _order(self):
+        # the DataLoader iterator draws its worker base seed first (_BaseDataLoaderIter.__init__), then
+        # RandomSampler.__iter__ draws the permutation seed: consume the global RNG the same way
+        torch.empty((), dtype=torch.int64).random_()
+        if not self.shuffle:
+            return torch.arange(self.n)
+        seed = int(torch.empty((), dtype=torch.int64).random_().item())     # RandomSampler.__iter__
+        g = torch.Generator()
+        g.manual_seed(seed)
+        return torch.randperm(self.n, generator=g)
+
+    def __iter__(self):
+        order = self._order().to(self.device)
+        for i in range(len(self)):
+            idx = order[i * self.batch_size:(i + 1) * self.batch_size]
+            yield _tree_map(lambda t: t.index_select(0, idx), self.data)
+
+
+def _tree_map(fn, x):
+    if isinstance(x, (list, tuple)):
+        return type(x)(_tree_map(fn, v) for v in x) if isinstance(x, tuple) else [_tree_map(fn, v) for v in x]
+    return fn(x)
+
+
 def get_data(cfg):
-    """data.py:37-45"""
+    """data.py:37-45.  cfg.device_loader = True (optional, not in the reference) serves both splits
+    through DeviceBatchLoader instead of DataLoader (same batches, resident in HBM)."""
+    if getattr(cfg, "device_loader", False):
+        tr, va = (MultiModalDataset_ti('feature/train_EEG.csv', 'feature/action/train_clip_v2.pickle',
+                                       'feature/EEG/train_bert.pickle'),
+                  MultiModalDataset_ti('feature/test_EEG.csv', 'feature/action/test_clip_v2.pickle',
+                                       'feature/EEG/test_bert.pickle'))
+        print(len(va))
+        return (DeviceBatchLoader(tr, cfg.batch_size, shuffle=True),
+                DeviceBatchLoader(va, cfg.batch_size, shuffle=True))
     batch_size = cfg.batch_size
     if cfg.data_name == 'EEG':
         train_dataset = MultiModalDataset_ti('feature/train_EEG.csv', 'feature/action/train_clip_v2.pickle',

@@ -27,6 +27,13 @@ SIGNATURES: dict[str, list] = {
                   vp, i64, i64, vp, i64, i64, vp, i64, i64,
                   vp, i64, vp, i64, i64, f32, f32, f32, vp, i64, vp],
     "eegf_gemm_colsum_tiles": [i32, i32, i32, i32, i32, i32],
+    "eegf_seq_lengths": [i32, i32, vp, vp, vp, vp],
+    "eegf_varlen_embed": [i32, i32, i32, i32, vp, i64, i64, vp, vp, vp, vp, vp, vp],
+    "eegf_varlen_rows": [i32, i32, i32, i32, vp, i64, i64, vp, i64, vp, i64, i32, vp],
+    "eegf_attn_varlen_fwd": [i32, i32, i32, i32, vp, i64, i64, vp, i64, f32, f32, u64, u64, vp, i64, vp, vp],
+    "eegf_attn_varlen_bwd_workspace": [i64, i32],
+    "eegf_attn_varlen_bwd": [i32, i32, i32, i32, vp, i64, i64, vp, i64, f32, f32, u64, u64, vp, vp, i64, vp, vp, vp,
+                             vp],
     "eegf_gemm_wgrad_bias": [i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, f32, vp, vp, i64, vp],
     "eegf_gemm_acs": [i32, i32, i32, i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, vp, vp, i64, f32, f32, f32,
                       vp, vp],
@@ -69,7 +76,8 @@ SIGNATURES: dict[str, list] = {
     "eegf_dp_clip_rows": [i32, i32, vp, f32, vp, vp, vp],
     "eegf_dp_noise": [i64, vp, f32, f32, u64, u64, vp],
 }
-RESTYPE_LONG = {"eegf_ln_bwd_partial_rows", "eegf_attn_bwd_workspace", "eegf_ghost_norm_workspace"}
+RESTYPE_LONG = {"eegf_ln_bwd_partial_rows", "eegf_attn_bwd_workspace", "eegf_ghost_norm_workspace",
+                "eegf_attn_varlen_bwd_workspace"}
 
 
 def register(name: str, argtypes: list) -> None:

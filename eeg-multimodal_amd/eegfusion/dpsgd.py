@@ -104,6 +104,8 @@ class GradSampleModule(nn.Module):
         self._module = m
         m._dp = dict(max_grad_norm=float(max_grad_norm), loss_reduction=loss_reduction, last_norms=None,
                      last_clip=None)
+        # per-sample norms index the BERT gradient sites by B x L rows: keep contract T padded
+        m.engine.cfg.varlen = False
 
     def forward(self, *a, **k):
         return self._module(*a, **k)

@@ -25,6 +25,7 @@ import math
 import struct
 from dataclasses import dataclass, field
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -60,12 +61,15 @@ class EngineConfig:
     act_dim: int = 32
     seed: int = 980616
     tau: float = 1.0               # PriGumbel-v1 gumbel_softmax temperature (train_val.py:95)
+    varlen: bool = True            # contract T: BERT over the packed real tokens (pad skipping, 8(f)#2)
 
 
 @dataclass
 class Saved:
     B: int = 0
-    L: int = 0
+    L: int = 0                     # padded sequence length (decoder memory / pooler rows: B * L)
+    R: int = 0                     # BERT rows: B * L, or the packed token count rounded up (varlen)
+    vl: dict | None = None         # varlen plan (cu_seqlens, packed / total rows) or None
     hard: bool = False
     training: bool = True
     rng: int = 0
@@ -365,6 +369,23 @@ class FusionEngine:
         self.bgrad(part[: nb * HID], pre + ".weight", nb, HID)
         self.bgrad(part[nb * HID:], pre + ".bias", nb, HID)
 
+    def _varlen_plan(self, mask, B, L):
+        """Contract T pad skipping: per-row token counts of the attention mask (one device pass, one
+        small D2H copy), cu_seqlens, and the packed row count rounded up to the 256-row GEMM tile.
+        None (the padded path) when a mask row is not right-padded or has no token."""
+        dev = self.a.device
+        mask = mask.contiguous()
+        buf = torch.empty(B + 1, dtype=torch.int32, device=dev)
+        call("eegf_seq_lengths", B, L, P(mask), P(buf), P(buf[B:]), _stream())
+        host = buf.cpu().numpy()
+        lens = host[:B].astype(np.int64)
+        if host[B] != 0 or lens.min() <= 0:
+            return None
+        cu = np.zeros(B + 1, dtype=np.int32)
+        cu[1:] = np.cumsum(lens)
+        T = int(cu[-1])
+        return dict(cu=torch.from_numpy(cu).to(dev), T=T, rows=(T + 255) // 256 * 256, max_len=int(lens.max()))
+
     # =================================================================== forward
     def forward(self, batch: dict, hard: bool, training: bool, save: bool = True):
         """batch (device tensors): contract W: eeg [B,C,T] f32, act [B,A] f32;
@@ -392,29 +413,44 @@ class FusionEngine:
         else:
             ids = batch["title_input"]
             B, L = ids.shape
-            x = self.empty(B * L, HID)
-            call("eegf_embed_gather", self.code, B * L, HID, P(ids), P(self.F("bert.embeddings.word_embeddings.weight")),
-                 P(x), _stream())
             mask = batch["text_mask"]
             kbias = torch.empty(B, L, dtype=torch.float32, device=self.a.device)
             call("eegf_key_bias", B * L, P(mask), P(kbias), _stream())
-            t["ids"] = ids
+            # DP-SGD's per-sample norms index sites by B x L rows: it keeps the padded layout
+            vl = self._varlen_plan(mask, B, L) if cfg.varlen and self.psn is None else None
+            if vl is None:
+                x = self.empty(B * L, HID)
+                call("eegf_embed_gather", self.code, B * L, HID, P(ids),
+                     P(self.F("bert.embeddings.word_embeddings.weight")), P(x), _stream())
+                t["ids"] = ids
+            else:
+                x = self.empty(vl["rows"], HID)
+                ids_p = torch.empty(vl["rows"], dtype=torch.int64, device=self.a.device)
+                call("eegf_varlen_embed", self.code, B, L, HID, P(vl["cu"]), vl["T"], vl["rows"], P(ids),
+                     P(self.F("bert.embeddings.word_embeddings.weight")),
+                     P(self.F("bert.embeddings.position_embeddings.weight")), P(x), P(ids_p), _stream())
+                t["ids"] = ids_p
+            sv.vl = vl
         sv.B, sv.L = B, L
-        if save and L % 256:
-            # eegf_attn_bwd handles L % 256 == 0 only: refuse before any gradient is written
-            raise ValueError(f"eegfusion: sequence length {L} is not a multiple of 256 (backward unsupported)")
-        if L % 128:
-            raise ValueError(f"eegfusion: sequence length {L} is not a multiple of 128")
-        R = B * L
+        vl = sv.vl
+        if vl is None:
+            if save and L % 256:
+                # eegf_attn_bwd handles L % 256 == 0 only: refuse before any gradient is written
+                raise ValueError(f"eegfusion: sequence length {L} is not a multiple of 256 (backward unsupported)")
+            if L % 128:
+                raise ValueError(f"eegfusion: sequence length {L} is not a multiple of 128")
+        R = B * L if vl is None else vl["rows"]
+        sv.R = R
         t["kbias"] = kbias
         e = "bert.embeddings."
         h = self.empty(R, HID)
         # without save (the PriGumbel DP pass: no full backward) the LN residual sums / statistics and
         # the FFN pre-activations are not stored
         s0, m0, r0 = (self.empty(R, HID), self._f32(R), self._f32(R)) if save else (None, None, None)
+        # position rows: the LN table add (dense) or already in the packed gather (varlen)
         self.ln_fwd(x, None, e + "LayerNorm", R, h, s0, m0, r0, 1e-12, pdrop, 2, sv.rng + 1,
-                    table=self.F(e + "position_embeddings.weight"), period=L,
-                    table2=self.F(e + "token_type_embeddings.weight"))
+                    table=self.F(e + "position_embeddings.weight") if vl is None else None,
+                    period=L if vl is None else 1, table2=self.F(e + "token_type_embeddings.weight"))
         t["emb"] = (s0, m0, r0)
         scale = DH ** -0.5
 
@@ -431,8 +467,12 @@ class FusionEngine:
             # storing the keep bits in the forward and reading them back)
             bits = None
             ev = self._ev_start("attn_fwd")
-            call("eegf_attn_fwd", self.code, B, NH, L, P(qkv), 3 * HID, P(kbias), scale, float(adrop), self.cfg.seed,
-                 sv.rng + 12 + 3 * i, P(ctx), HID, P(lse), P(bits), _stream())
+            if vl is None:
+                call("eegf_attn_fwd", self.code, B, NH, L, P(qkv), 3 * HID, P(kbias), scale, float(adrop),
+                     self.cfg.seed, sv.rng + 12 + 3 * i, P(ctx), HID, P(lse), P(bits), _stream())
+            else:
+                call("eegf_attn_varlen_fwd", self.code, B, NH, L, P(vl["cu"]), vl["T"], R, P(qkv), 3 * HID, scale,
+                     float(adrop), self.cfg.seed, sv.rng + 12 + 3 * i, P(ctx), HID, P(lse), _stream())
             self._ev_end("attn_fwd", ev, 4.0 * B * NH * L * L * DH)
             ao = self.ws.get("ao", R * HID, self.dt).view(R, HID)
             self.linear(ctx, self.W(pre + "attention.output.dense.weight"), self.F(pre + "attention.output.dense.bias"),
@@ -457,6 +497,11 @@ class FusionEngine:
                                    ln2=(s2, m2, r2)))
             h = h2
         t["layers"] = layers
+        if vl is not None:        # decoder memory / pooler input: the padded [B, L] layout, zero pad rows
+            hp = self.empty(B * L, HID)
+            call("eegf_varlen_rows", self.code, B, L, HID, P(vl["cu"]), vl["T"], R, P(h), HID, P(hp), HID, 1,
+                 _stream())
+            h = hp
         t["mem"] = h
         pooled = self.eh(B, HID)                 # fp32 out of the bf16 pooler GEMM (+ tanh)
         self.linear(h, self.W("bert.pooler.dense.weight"), self.F("bert.pooler.dense.bias"), pooled, B, lda=L * HID,
@@ -573,7 +618,7 @@ class FusionEngine:
         cfg = self.cfg
         t = sv.t
         B, L = sv.B, sv.L
-        R = B * L
+        R, vl = sv.R or B * L, sv.vl
         pdrop = cfg.hidden_dropout if sv.training else 0.0
         adrop = cfg.attn_dropout if sv.training else 0.0
         ddrop = cfg.dec_dropout if sv.training else 0.0
@@ -583,7 +628,7 @@ class FusionEngine:
 
         # ---------------- decoder backward (fp32; memory gradient in the encoder dtype)
         mem = t["mem"]
-        dmem = self.empty(R, HID)
+        dmem = self.empty(B * L, HID)
         dx3 = dcross
         scale = DH ** -0.5
         for d in reversed(range(DEC_L)):
@@ -680,13 +725,18 @@ class FusionEngine:
 
         # ---------------- BERT encoder backward
         dh = dmem
+        if vl is not None:        # padded memory gradient -> the packed rows (zeros past the tokens)
+            dh = self.empty(R, HID)
+            call("eegf_varlen_rows", self.code, B, L, HID, P(vl["cu"]), vl["T"], R, P(dmem), HID, P(dh), HID, 0,
+                 _stream())
         dfo = self.ws.get("b_dfo", R * HID, self.dt).view(R, HID)
         da = self.ws.get("b_da", R * HID, self.dt).view(R, HID)
         dffp = self.ws.get("b_dffp", R * FFN, self.dt).view(R, FFN)
         dao = self.ws.get("b_dao", R * HID, self.dt).view(R, HID)
         dctx = self.ws.get("b_dctx", R * HID, self.dt).view(R, HID)
         dqkv = self.ws.get("b_dqkv", R * 3 * HID, self.dt).view(R, 3 * HID)
-        dq_ws_n = _lib.lib().eegf_attn_bwd_workspace(B, L)
+        dq_ws_n = (_lib.lib().eegf_attn_bwd_workspace(B, L) if vl is None
+                   else _lib.lib().eegf_attn_varlen_bwd_workspace(R, L))
         dq_ws = self.ws.get("b_dqws", dq_ws_n, torch.float32) if dq_ws_n > 0 else None
         lowest = self._lowest_needed_layer()
         for i in reversed(range(NL)):
@@ -707,9 +757,14 @@ class FusionEngine:
                        bias=pre + "attention.output.dense.bias")
             self.dgrad(dao, self.W(pre + "attention.output.dense.weight"), dctx, R, tag="dgrad_out")
             ev = self._ev_start("attn_bwd")
-            call("eegf_attn_bwd", self.code, B, NH, L, P(s["qkv"]), 3 * HID, P(t["kbias"]), scale, float(adrop),
-                 self.cfg.seed, sv.rng + 12 + 3 * i, P(s["ctx"]), P(dctx), HID, P(s["lse"]), P(s["bits"]), P(dqkv),
-                 P(dq_ws), _stream())
+            if vl is None:
+                call("eegf_attn_bwd", self.code, B, NH, L, P(s["qkv"]), 3 * HID, P(t["kbias"]), scale, float(adrop),
+                     self.cfg.seed, sv.rng + 12 + 3 * i, P(s["ctx"]), P(dctx), HID, P(s["lse"]), P(s["bits"]),
+                     P(dqkv), P(dq_ws), _stream())
+            else:
+                call("eegf_attn_varlen_bwd", self.code, B, NH, L, P(vl["cu"]), vl["T"], R, P(s["qkv"]), 3 * HID,
+                     scale, float(adrop), self.cfg.seed, sv.rng + 12 + 3 * i, P(s["ctx"]), P(dctx), HID, P(s["lse"]),
+                     P(dqkv), P(dq_ws), _stream())
             self._ev_end("attn_bwd", ev, 2.5 * 4.0 * B * NH * L * L * DH)
             qn = pre + "attention.self.query.weight"
             bn = pre + "attention.self.query.bias"
@@ -730,7 +785,12 @@ class FusionEngine:
         demb = self.ws.get("b_demb", R * HID, self.dt).view(R, HID)
         self.ln_bwd(dh, *t["emb"], e + "LayerNorm", R, demb, None, pdrop, 2, sv.rng + 1)
         if self.need(e + "position_embeddings.weight"):
-            self.bgrad(demb, e + "position_embeddings.weight", R, width=HID, period=L,
+            dpos = demb
+            if vl is not None:    # position j of every sequence: the padded layout's period-L column sums
+                dpos = self.empty(B * L, HID)
+                call("eegf_varlen_rows", self.code, B, L, HID, P(vl["cu"]), vl["T"], R, P(demb), HID, P(dpos), HID,
+                     1, _stream())
+            self.bgrad(dpos, e + "position_embeddings.weight", B * L, width=HID, period=L,
                        out=self.G(e + "position_embeddings.weight")[:L])
         if self.need(e + "token_type_embeddings.weight"):
             self.bgrad(demb, e + "token_type_embeddings.weight", R, width=HID,

@@ -92,6 +92,39 @@ int eegf_gemm_acs(int dtype, int out_dtype, int a_kcontig, int b_kcontig, int ep
                   void* aux, long ldaux, float alpha, float beta, float epi_scale, float* a_colsum,
                   hipStream_t stream);
 
+/* ---- contract T pad skipping (varlen BERT).  The reference runs BERT over the
+ * padded 512 tokens (get_embedding.py:115) with the padded keys masked (model.py:37-43); the packed
+ * rows of the real tokens give the same outputs.  cu_seqlens [B+1] int32 (device): sequence b owns
+ * packed rows cu[b] .. cu[b+1]-1; packed_rows = cu[B]; total_rows >= packed_rows rounds the row count
+ * up for the GEMM tiles (rows past packed_rows are written as zeros). */
+/* lens[b] = nonzero entries of mask row b ([B, L] int64 attention_mask); *nonprefix = 1 when some row
+ * is not [1]*n + [0]*(L-n) (then the packed path does not apply). */
+int eegf_seq_lengths(int B, int L, const long long* mask, int* lens, int* nonprefix, hipStream_t stream);
+/* BertEmbeddings word + position rows of the real tokens (modeling_bert.py:95-105, position_ids =
+ * arange): out[cu[b]+j] = word[ids[b,j]] + pos[j] (fp32 sum, one rounding), ids_packed[cu[b]+j] =
+ * ids[b,j]; the token-type row is added by eegf_ln_fwd (table2). */
+int eegf_varlen_embed(int dtype, int B, int L, int width, const int* cu_seqlens, long packed_rows,
+                      long total_rows, const long long* ids, const float* word, const float* pos, void* out,
+                      long long* ids_packed, hipStream_t stream);
+/* padded [B, S, width] (row stride ld) <-> packed rows: to_padded = 1 writes every padded row (zeros
+ * past each sequence: the decoder memory / pooler input); 0 writes the packed rows (and zeros rows
+ * packed_rows .. total_rows-1).  16-B aligned rows. */
+int eegf_varlen_rows(int dtype, int B, int S, int width, const int* cu_seqlens, long packed_rows, long total_rows,
+                     const void* src, long ld_src, void* dst, long ld_dst, int to_padded, hipStream_t stream);
+/* Packed self-attention (BertSelfAttention over each sequence's real tokens, no key bias): as
+ * eegf_attn_fwd with the rows of sequence b at cu[b] ..; max_len = the padded length L of the batch
+ * (>= every sequence length): LSE is [B, 12, max_len] and the dropout element numbering is the padded
+ * ((b*12 + h)*L + q)*L + key, so a packed batch draws exactly its padded form's masks. */
+int eegf_attn_varlen_fwd(int dtype, int B, int H, int max_len, const int* cu_seqlens, long packed_rows,
+                         long total_rows, const void* qkv, long ld_qkv, float scale, float drop_p,
+                         unsigned long long seed, unsigned long long offset, void* out, long ld_out, float* lse,
+                         hipStream_t stream);
+long eegf_attn_varlen_bwd_workspace(long total_rows, int max_len);
+int eegf_attn_varlen_bwd(int dtype, int B, int H, int max_len, const int* cu_seqlens, long packed_rows,
+                         long total_rows, const void* qkv, long ld_qkv, float scale, float drop_p,
+                         unsigned long long seed, unsigned long long offset, const void* out, const void* dout,
+                         long ld_out, const float* lse, void* dqkv, float* dq_workspace, hipStream_t stream);
+
 /* fusion variants (eegf_fusion_fwd/bwd) */
 #define FUSE_CONCAT 0        /* model.py ConcatModel.feature: minmax(cat)            model.py:46-50      */
 #define FUSE_PRICONCAT 1     /* main_0430 ConcatModel: DP_guarantee(dp_mode=None)=id main_0430.py:118    */

@@ -82,3 +82,24 @@ def test_get_data_signature(tmp_path, monkeypatch):
     monkeypatch.chdir(tmp_path)
     tr, va = get_data(types.SimpleNamespace(batch_size=2, data_name="EEG"))
     assert len(tr.dataset) == 5 and len(va.dataset) == 5
+
+
+def test_device_batch_loader_matches_dataloader(tmp_path):
+    """DeviceBatchLoader (collated once, resident, device-side gathers) serves the batches the
+    reference's DataLoader(shuffle=True) serves from the same global seed: same structure, shapes,
+    dtypes, values and sample order (RandomSampler's RNG draw), last partial batch included."""
+    from data import DeviceBatchLoader, MultiModalDataset_ti
+    _write_split(tmp_path, n=5)
+    ds = MultiModalDataset_ti(tmp_path / "x_EEG.csv", tmp_path / "action" / "x_clip_v2.pickle",
+                              tmp_path / "EEG" / "x_bert.pickle")
+    for shuffle in (True, False):
+        torch.manual_seed(980616)
+        ref = [b for _ in range(2) for b in torch.utils.data.DataLoader(ds, batch_size=2, shuffle=shuffle)]
+        torch.manual_seed(980616)
+        dl = DeviceBatchLoader(ds, batch_size=2, shuffle=shuffle, device="cpu")
+        got = [b for _ in range(2) for b in dl]
+        assert len(dl) == 3 and len(got) == len(ref) == 6
+        for (xr, yr), (xg, yg) in zip(ref, got):
+            assert type(xr) is type(xg) and len(xr) == len(xg) == 4
+            for a, b in zip(list(xr) + [yr], list(xg) + [yg]):
+                assert a.shape == b.shape and a.dtype == b.dtype and torch.equal(a, b)
