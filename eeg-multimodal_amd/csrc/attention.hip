@@ -507,7 +507,8 @@ extern "C" int eegf_attn_bwd(int dtype, int B, int H, int L, const void* qkv, lo
 // BertSelfAttention are masked (model.py:43, modeling_bert.py extended mask), so the packed rows of
 // each sequence give the real rows' outputs of the padded computation exactly.
 extern "C" int eegf_attn_varlen_fwd(int dtype, int B, int H, int max_len, const int* cu_seqlens, long packed_rows,
-                                    long total_rows, const void* qkv, long ld_qkv, float scale, float drop_p,
+                                    long total_rows, const void* qkv, long ld_qkv, const float* key_bias,
+                                    float scale, float drop_p,
                                     unsigned long long seed, unsigned long long offset, void* out, long ld_out,
                                     float* lse, hipStream_t stream) {
   if (B <= 0 || B > 65535 || H != 12 || max_len <= 0 || !cu_seqlens || !qkv || !out || !lse) return EEGF_ERR_ARG;
@@ -517,7 +518,7 @@ extern "C" int eegf_attn_varlen_fwd(int dtype, int B, int H, int max_len, const 
   if (!es) return EEGF_ERR_ARG;
   if (total_rows > packed_rows)        // rows past the packed sequences: defined zeros
     hipMemsetAsync((char*)out + packed_rows * ld_out * es, 0, (total_rows - packed_rows) * ld_out * es, stream);
-  AttnArgs a{qkv, out, lse, nullptr, nullptr, nullptr, nullptr, nullptr, B, H, max_len, ld_qkv, ld_out, scale,
+  AttnArgs a{qkv, out, lse, key_bias, nullptr, nullptr, nullptr, nullptr, B, H, max_len, ld_qkv, ld_out, scale,
              drop_p, seed, offset, nullptr, cu_seqlens};
   const dim3 grid((max_len + 127) / 128, H, B);
   if (dtype == EEGF_F32) hipLaunchKernelGGL((attn_fwd_kernel<float, true>), grid, dim3(512), 0, stream, a);
@@ -530,7 +531,8 @@ extern "C" long eegf_attn_varlen_bwd_workspace(long total_rows, int max_len) {
 }
 
 extern "C" int eegf_attn_varlen_bwd(int dtype, int B, int H, int max_len, const int* cu_seqlens, long packed_rows,
-                                    long total_rows, const void* qkv, long ld_qkv, float scale, float drop_p,
+                                    long total_rows, const void* qkv, long ld_qkv, const float* key_bias,
+                                    float scale, float drop_p,
                                     unsigned long long seed, unsigned long long offset, const void* out,
                                     const void* dout, long ld_out, const float* lse, void* dqkv, float* dq_workspace,
                                     hipStream_t stream) {
@@ -544,7 +546,7 @@ extern "C" int eegf_attn_varlen_bwd(int dtype, int B, int H, int max_len, const 
   if (total_rows > packed_rows)
     hipMemsetAsync((char*)dqkv + packed_rows * ld_qkv * es, 0, (total_rows - packed_rows) * ld_qkv * es, stream);
   if (max_len > 256) hipMemsetAsync(dq_workspace, 0, sizeof(float) * (size_t)total_rows * 768, stream);
-  AttnArgs a{qkv, nullptr, const_cast<float*>(lse), nullptr, out, dout, dqkv, dq_workspace, B, H, max_len, ld_qkv,
+  AttnArgs a{qkv, nullptr, const_cast<float*>(lse), key_bias, out, dout, dqkv, dq_workspace, B, H, max_len, ld_qkv,
              ld_out, scale, drop_p, seed, offset, nullptr, cu_seqlens};
   const dim3 grid((max_len + 255) / 256, H, B);
   if (dtype == EEGF_F32) hipLaunchKernelGGL((attn_bwd_kernel<float, true>), grid, dim3(512), 0, stream, a);
@@ -554,5 +556,126 @@ extern "C" int eegf_attn_varlen_bwd(int dtype, int B, int H, int max_len, const 
     hipLaunchKernelGGL(dq_convert_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, dq_workspace, dqkv,
                        dtype == EEGF_BF16, total_rows, ld_qkv);
   }
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Self-attention over a handful of tokens (S <= 8): the TransformerEncoder of TISC_LapDropout runs
+// its 12-head attention over the 2 tokens [mean(EEG sequence), action] of each sample
+// (custom_models/models.py:227-228, :258-260; F.multi_head_attention_forward).  One wave per
+// (sample n, head h), lane = head dimension d: q_i . k_j by wave reductions, softmax over j, the
+// attention-weight dropout (Philox element ((n*12 + h)*S + i)*S + j, drop_mask1), ctx_i = sum_j p~_ij v_j.
+// Rows of sample n are n*S .. n*S + S-1 of qkv [N*S, 3*768] / out [N*S, 768].  probs (undropped
+// softmax, [N, 12, S, S] fp32) is saved for the backward.
+namespace {
+constexpr int SMAX = 8;
+
+template <typename T>
+__global__ void __launch_bounds__(64) attn_small_fwd_kernel(int S, const T* __restrict__ qkv, long ld, float scale,
+                                                            float p, uint64_t seed, uint64_t offset, T* __restrict__ out,
+                                                            long ldo, float* __restrict__ probs) {
+  const int n = blockIdx.x, h = blockIdx.y, d = threadIdx.x;
+  float q[SMAX], k[SMAX], v[SMAX];
+  for (int i = 0; i < S; ++i) {
+    const T* r = qkv + ((long)n * S + i) * ld + h * DH + d;
+    q[i] = to_f32(r[0]) * scale;
+    k[i] = to_f32(r[768]);
+    v[i] = to_f32(r[1536]);
+  }
+  const float dscale = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;
+  for (int i = 0; i < S; ++i) {
+    float sc[SMAX], mx = -INFINITY;
+    for (int j = 0; j < S; ++j) {
+      sc[j] = wave_sum(q[i] * k[j]);
+      mx = fmaxf(mx, sc[j]);
+    }
+    float den = 0.f;
+    for (int j = 0; j < S; ++j) { sc[j] = expf(sc[j] - mx); den += sc[j]; }
+    float o = 0.f;
+    for (int j = 0; j < S; ++j) {
+      const float pij = sc[j] / den;
+      const long e = (((long)n * 12 + h) * S + i) * S + j;
+      if (d == 0) probs[e] = pij;
+      const float m = p > 0.f ? drop_mask1(seed, offset, (uint64_t)e, p) : dscale;
+      o += pij * m * v[j];
+    }
+    out[((long)n * S + i) * ldo + h * DH + d] = from_f32<T>(o);
+  }
+}
+
+// dV_j = sum_i p~_ij dctx_i; dp~_ij = dctx_i . v_j; dp_ij = m_ij dp~_ij; ds_ij = p_ij (dp_ij - sum_k p_ik dp_ik);
+// dq_i = scale sum_j ds_ij k_j; dk_j = scale sum_i ds_ij q_i
+template <typename T>
+__global__ void __launch_bounds__(64) attn_small_bwd_kernel(int S, const T* __restrict__ qkv, long ld,
+                                                            const float* __restrict__ probs, const T* __restrict__ dout,
+                                                            long ldo, float scale, float p, uint64_t seed,
+                                                            uint64_t offset, T* __restrict__ dqkv, long ldd) {
+  const int n = blockIdx.x, h = blockIdx.y, d = threadIdx.x;
+  float q[SMAX], k[SMAX], v[SMAX], g[SMAX], dq[SMAX], dk[SMAX], dv[SMAX];
+  for (int i = 0; i < S; ++i) {
+    const T* r = qkv + ((long)n * S + i) * ld + h * DH + d;
+    q[i] = to_f32(r[0]);
+    k[i] = to_f32(r[768]);
+    v[i] = to_f32(r[1536]);
+    g[i] = to_f32(dout[((long)n * S + i) * ldo + h * DH + d]);
+    dq[i] = dk[i] = dv[i] = 0.f;
+  }
+  const float dscale = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;
+  for (int i = 0; i < S; ++i) {
+    float pr[SMAX], dp[SMAX], sdot = 0.f;
+    for (int j = 0; j < S; ++j) {
+      const long e = (((long)n * 12 + h) * S + i) * S + j;
+      pr[j] = probs[e];
+      const float m = p > 0.f ? drop_mask1(seed, offset, (uint64_t)e, p) : dscale;
+      dv[j] += pr[j] * m * g[i];
+      dp[j] = m * wave_sum(g[i] * v[j]);
+      sdot += pr[j] * dp[j];
+    }
+    for (int j = 0; j < S; ++j) {
+      const float ds = pr[j] * (dp[j] - sdot) * scale;
+      dq[i] += ds * k[j];
+      dk[j] += ds * q[i];
+    }
+  }
+  for (int i = 0; i < S; ++i) {
+    T* r = dqkv + ((long)n * S + i) * ldd + h * DH + d;
+    r[0] = from_f32<T>(dq[i]);
+    r[768] = from_f32<T>(dk[i]);
+    r[1536] = from_f32<T>(dv[i]);
+  }
+}
+}  // namespace
+
+extern "C" int eegf_attn_small_fwd(int dtype, int N, int S, const void* qkv, long ld_qkv, float scale, float drop_p,
+                                   unsigned long long seed, unsigned long long offset, void* out, long ld_out,
+                                   float* probs, hipStream_t stream) {
+  if (N <= 0 || N > 65535 || S <= 0 || S > SMAX || !qkv || !out || !probs || ld_qkv < 2304 || ld_out < 768 ||
+      drop_p < 0.f || drop_p >= 1.f)
+    return EEGF_ERR_ARG;
+  const dim3 grid(N, 12);
+  if (dtype == EEGF_F32)
+    hipLaunchKernelGGL(attn_small_fwd_kernel<float>, grid, dim3(64), 0, stream, S, (const float*)qkv, ld_qkv, scale,
+                       drop_p, seed, offset, (float*)out, ld_out, probs);
+  else if (dtype == EEGF_BF16)
+    hipLaunchKernelGGL(attn_small_fwd_kernel<bf16>, grid, dim3(64), 0, stream, S, (const bf16*)qkv, ld_qkv, scale,
+                       drop_p, seed, offset, (bf16*)out, ld_out, probs);
+  else return EEGF_ERR_ARG;
+  return (int)hipGetLastError();
+}
+
+extern "C" int eegf_attn_small_bwd(int dtype, int N, int S, const void* qkv, long ld_qkv, const float* probs,
+                                   const void* dout, long ld_out, float scale, float drop_p, unsigned long long seed,
+                                   unsigned long long offset, void* dqkv, long ld_dqkv, hipStream_t stream) {
+  if (N <= 0 || N > 65535 || S <= 0 || S > SMAX || !qkv || !probs || !dout || !dqkv || ld_qkv < 2304 ||
+      ld_out < 768 || ld_dqkv < 2304 || drop_p < 0.f || drop_p >= 1.f)
+    return EEGF_ERR_ARG;
+  const dim3 grid(N, 12);
+  if (dtype == EEGF_F32)
+    hipLaunchKernelGGL(attn_small_bwd_kernel<float>, grid, dim3(64), 0, stream, S, (const float*)qkv, ld_qkv, probs,
+                       (const float*)dout, ld_out, scale, drop_p, seed, offset, (float*)dqkv, ld_dqkv);
+  else if (dtype == EEGF_BF16)
+    hipLaunchKernelGGL(attn_small_bwd_kernel<bf16>, grid, dim3(64), 0, stream, S, (const bf16*)qkv, ld_qkv, probs,
+                       (const bf16*)dout, ld_out, scale, drop_p, seed, offset, (bf16*)dqkv, ld_dqkv);
+  else return EEGF_ERR_ARG;
   return (int)hipGetLastError();
 }

@@ -58,3 +58,58 @@ extern "C" int eegf_dropout(int dtype, long n, int group, float p, unsigned long
   else return EEGF_ERR_ARG;
   return (int)hipGetLastError();
 }
+
+// Mean over the L rows of each sequence (TTCA's decoder output .mean(dim=1), TISC's
+// eeg_txt_semantics_embedding.mean(dim=1) and its encoder's .mean(dim=0): custom_models/models.py:109,
+// :253, :260): out[b] (fp32, row stride ld_out) = (1/L) sum_l x[b*L + l] (row stride ld_x);
+// backward: dx[b*L + l] = beta dx[b*L + l] + dmean[b] / L.  One block per (b, 256-column slab),
+// fixed summation order.
+namespace {
+template <typename T>
+__global__ void __launch_bounds__(256) seq_mean_kernel(int L, int width, const T* __restrict__ x, long ldx,
+                                                       float* __restrict__ out, long ldo) {
+  const int b = blockIdx.x, c = blockIdx.y * 256 + threadIdx.x;
+  if (c >= width) return;
+  float s = 0.f;
+  for (int l = 0; l < L; ++l) s += to_f32(x[((long)b * L + l) * ldx + c]);
+  out[(long)b * ldo + c] = s / (float)L;
+}
+template <typename T>
+__global__ void __launch_bounds__(256) seq_mean_bwd_kernel(int L, int width, const float* __restrict__ dmean, long ldm,
+                                                           T* __restrict__ dx, long ldx, float beta) {
+  const int b = blockIdx.x, c = blockIdx.y * 256 + threadIdx.x;
+  if (c >= width) return;
+  const float g = dmean[(long)b * ldm + c] / (float)L;
+  for (int l = 0; l < L; ++l) {
+    T* p = dx + ((long)b * L + l) * ldx + c;
+    *p = from_f32<T>(beta != 0.f ? beta * to_f32(*p) + g : g);
+  }
+}
+}  // namespace
+
+extern "C" int eegf_seq_mean(int dtype, int B, int L, int width, const void* x, long ld_x, float* out, long ld_out,
+                             hipStream_t stream) {
+  if (B <= 0 || B > 65535 || L <= 0 || width <= 0 || !x || !out || ld_x < width || ld_out < width) return EEGF_ERR_ARG;
+  const dim3 grid(B, (width + 255) / 256);
+  if (dtype == EEGF_F32)
+    hipLaunchKernelGGL(seq_mean_kernel<float>, grid, dim3(256), 0, stream, L, width, (const float*)x, ld_x, out, ld_out);
+  else if (dtype == EEGF_BF16)
+    hipLaunchKernelGGL(seq_mean_kernel<bf16>, grid, dim3(256), 0, stream, L, width, (const bf16*)x, ld_x, out, ld_out);
+  else return EEGF_ERR_ARG;
+  return (int)hipGetLastError();
+}
+
+extern "C" int eegf_seq_mean_bwd(int dtype, int B, int L, int width, const float* dmean, long ld_dmean, void* dx,
+                                 long ld_dx, float beta, hipStream_t stream) {
+  if (B <= 0 || B > 65535 || L <= 0 || width <= 0 || !dmean || !dx || ld_dx < width || ld_dmean < width)
+    return EEGF_ERR_ARG;
+  const dim3 grid(B, (width + 255) / 256);
+  if (dtype == EEGF_F32)
+    hipLaunchKernelGGL(seq_mean_bwd_kernel<float>, grid, dim3(256), 0, stream, L, width, dmean, ld_dmean, (float*)dx,
+                       ld_dx, beta);
+  else if (dtype == EEGF_BF16)
+    hipLaunchKernelGGL(seq_mean_bwd_kernel<bf16>, grid, dim3(256), 0, stream, L, width, dmean, ld_dmean, (bf16*)dx,
+                       ld_dx, beta);
+  else return EEGF_ERR_ARG;
+  return (int)hipGetLastError();
+}

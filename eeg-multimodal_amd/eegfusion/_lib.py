@@ -30,10 +30,14 @@ SIGNATURES: dict[str, list] = {
     "eegf_seq_lengths": [i32, i32, vp, vp, vp, vp],
     "eegf_varlen_embed": [i32, i32, i32, i32, vp, i64, i64, vp, vp, vp, vp, vp, vp],
     "eegf_varlen_rows": [i32, i32, i32, i32, vp, i64, i64, vp, i64, vp, i64, i32, vp],
-    "eegf_attn_varlen_fwd": [i32, i32, i32, i32, vp, i64, i64, vp, i64, f32, f32, u64, u64, vp, i64, vp, vp],
+    "eegf_attn_varlen_fwd": [i32, i32, i32, i32, vp, i64, i64, vp, i64, vp, f32, f32, u64, u64, vp, i64, vp, vp],
     "eegf_attn_varlen_bwd_workspace": [i64, i32],
-    "eegf_attn_varlen_bwd": [i32, i32, i32, i32, vp, i64, i64, vp, i64, f32, f32, u64, u64, vp, vp, i64, vp, vp, vp,
-                             vp],
+    "eegf_attn_varlen_bwd": [i32, i32, i32, i32, vp, i64, i64, vp, i64, vp, f32, f32, u64, u64, vp, vp, i64, vp, vp,
+                             vp, vp],
+    "eegf_attn_small_fwd": [i32, i32, i32, vp, i64, f32, f32, u64, u64, vp, i64, vp, vp],
+    "eegf_attn_small_bwd": [i32, i32, i32, vp, i64, vp, vp, i64, f32, f32, u64, u64, vp, i64, vp],
+    "eegf_seq_mean": [i32, i32, i32, i32, vp, i64, vp, i64, vp],
+    "eegf_seq_mean_bwd": [i32, i32, i32, i32, vp, i64, vp, i64, f32, vp],
     "eegf_gemm_wgrad_bias": [i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, f32, vp, vp, i64, vp],
     "eegf_gemm_acs": [i32, i32, i32, i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, vp, vp, i64, f32, f32, f32,
                       vp, vp],

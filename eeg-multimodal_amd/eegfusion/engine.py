@@ -35,6 +35,7 @@ from .arena import ParamArena
 HID, NH, DH, FFN, NL = 768, 12, 64, 3072, 12
 DEC_FF, DEC_L = 2048, 3
 FUSED = 3 * HID
+MODALS = ("ti", "it", "ii", "tt", "tisc")   # TICA / ITCA / IICA / TTCA / TISC (custom_models/models.py:28-272)
 EPS_MODES = ("newfrac", "new")    # past_acc.py:132 1/ln((e^eps-w)/(1-w)) | model.py:57 ln(...)
 SPLITK_WS = 24 << 20          # fp32 elements of split-K slab workspace (96 MB)
 VARIANTS = {"concat": _lib.FUSE_CONCAT, "priconcat": _lib.FUSE_PRICONCAT,
@@ -62,11 +63,13 @@ class EngineConfig:
     seed: int = 980616
     tau: float = 1.0               # PriGumbel-v1 gumbel_softmax temperature (train_val.py:95)
     varlen: bool = True            # contract T: BERT over the packed real tokens (pad skipping, 8(f)#2)
+    modal: str = "ti"              # custom_models/models.py variant: ti | it | ii | tt | tisc (MODALS)
 
 
 @dataclass
 class Saved:
     B: int = 0
+    Bb: int = 0                    # BERT batch (2B for TTCA: both token batches in one pass)
     L: int = 0                     # padded sequence length (decoder memory / pooler rows: B * L)
     R: int = 0                     # BERT rows: B * L, or the packed token count rounded up (varlen)
     vl: dict | None = None         # varlen plan (cu_seqlens, packed / total rows) or None
@@ -105,6 +108,10 @@ class FusionEngine:
         self.code = F32 if cfg.dtype == torch.float32 else BF16
         if cfg.variant not in VARIANTS:
             raise ValueError(f"eegfusion: unknown variant {cfg.variant!r} (one of {sorted(VARIANTS)})")
+        if cfg.modal not in MODALS:
+            raise ValueError(f"eegfusion: modal must be one of {MODALS}, got {cfg.modal!r}")
+        if cfg.modal != "ti" and cfg.contract != "T":
+            raise ValueError("eegfusion: the modality variants take token ids / CLIP vectors (contract T)")
         if cfg.eps_mode not in EPS_MODES:
             raise ValueError(f"eegfusion: eps_mode must be one of {EPS_MODES}, got {cfg.eps_mode!r}")
         self.variant = VARIANTS[cfg.variant]
@@ -308,7 +315,10 @@ class FusionEngine:
     def colsum(self, src, ld, rows, width, dst, period=1):
         """dst += column sums of src (rows x width, row stride ld); deferred to the end of the backward
         pass (eegf_colsum_batch) when small, else a two-stage eegf_colsum now."""
-        if self.defer is not None and period == 1 and rows <= 8192 and self._stable(src):
+        # one deferred entry per destination: the batched kernel's blocks add into dst[c] without
+        # ordering between entries (a second sum into the same bias runs now, in stream order)
+        if (self.defer is not None and period == 1 and rows <= 8192 and self._stable(src)
+                and all(P(e[5]) != P(dst) for e in self.defer)):
             self.defer.append((src, int(ld), int(rows), int(width), _code(src), dst))
             return
         ws = self.ws.get("colsum", 1 << 24, torch.float32)
@@ -369,6 +379,195 @@ class FusionEngine:
         self.bgrad(part[: nb * HID], pre + ".weight", nb, HID)
         self.bgrad(part[nb * HID:], pre + ".bias", nb, HID)
 
+    def _uniform_plan(self, B, L, kbias):
+        """every row a full-length sequence (cu[b] = b*L) with the key mask: the varlen attention
+        kernels on the padded layout, for lengths the dense kernels do not take (L % 256)."""
+        key = ("uniform", B, L)
+        cu = self._plans.get(key) if hasattr(self, "_plans") else None
+        if cu is None:
+            self._plans = getattr(self, "_plans", {})
+            cu = torch.arange(0, (B + 1) * L, L, dtype=torch.int32).to(self.a.device)
+            self._plans[key] = cu
+        return dict(cu=cu, T=B * L, rows=B * L, max_len=L, kbias=kbias, uniform=True)
+
+    def _attn_any_fwd(self, qkv, ctx, lse, B, L, kbias, p, rng):
+        """BertSelfAttention-form attention over the padded layout at any L (dense kernels for
+        L % 256 == 0, else the varlen ones with uniform lengths)."""
+        if L % 256 == 0:
+            call("eegf_attn_fwd", self.code, B, NH, L, P(qkv), 3 * HID, P(kbias), DH ** -0.5, float(p), self.cfg.seed,
+                 rng, P(ctx), HID, P(lse), None, _stream())
+        else:
+            vl = self._uniform_plan(B, L, kbias)
+            call("eegf_attn_varlen_fwd", self.code, B, NH, L, P(vl["cu"]), B * L, B * L, P(qkv), 3 * HID, P(kbias),
+                 DH ** -0.5, float(p), self.cfg.seed, rng, P(ctx), HID, P(lse), _stream())
+
+    def _attn_any_bwd(self, qkv, ctx, dctx, lse, dqkv, B, L, kbias, p, rng):
+        if L % 256 == 0:
+            n = _lib.lib().eegf_attn_bwd_workspace(B, L)
+            ws = self.ws.get("b_dqws", n, torch.float32) if n > 0 else None
+            call("eegf_attn_bwd", self.code, B, NH, L, P(qkv), 3 * HID, P(kbias), DH ** -0.5, float(p), self.cfg.seed,
+                 rng, P(ctx), P(dctx), HID, P(lse), None, P(dqkv), P(ws), _stream())
+        else:
+            vl = self._uniform_plan(B, L, kbias)
+            n = _lib.lib().eegf_attn_varlen_bwd_workspace(B * L, L)
+            ws = self.ws.get("b_dqws", n, torch.float32) if n > 0 else None
+            call("eegf_attn_varlen_bwd", self.code, B, NH, L, P(vl["cu"]), B * L, B * L, P(qkv), 3 * HID, P(kbias),
+                 DH ** -0.5, float(p), self.cfg.seed, rng, P(ctx), P(dctx), HID, P(lse), P(dqkv), P(ws), _stream())
+
+    # ------------------------------------------------------- TTCA sequence decoder (models.py:84-129)
+    def _seqdec_fwd(self, t, tgt, mem, B, L, ddrop, rng):
+        """multi_head_decoder(tgt=act sequence, memory=eeg sequence) with no masks, then
+        .permute(1,0,2).mean(dim=1) (models.py:107-109): post-norm TransformerDecoderLayer x3 over
+        [B*L, 768] rows in the encoder dtype; -> cross [B, 768] fp32."""
+        R = B * L
+        x = tgt
+        st = []
+        for d in range(DEC_L):
+            pre = f"multi_head_decoder.layers.{d}."
+            r0 = rng + 400 + 16 * d
+            qkv = self.empty(R, 3 * HID)
+            self.linear(x, self.W(pre + "self_attn.in_proj_weight"), self.F(pre + "self_attn.in_proj_bias"), qkv, R)
+            ctx, lse = self.empty(R, HID), self._f32(B, NH, L)
+            self._attn_any_fwd(qkv, ctx, lse, B, L, None, ddrop, r0)
+            sa = self.empty(R, HID)
+            self.linear(ctx, self.W(pre + "self_attn.out_proj.weight"), self.F(pre + "self_attn.out_proj.bias"), sa, R)
+            x1, ln1 = self.empty(R, HID), (self.empty(R, HID), self._f32(R), self._f32(R))
+            self.ln_fwd(sa, x, pre + "norm1", R, x1, *ln1, 1e-5, ddrop, 1, r0 + 1)
+            cw, cb = self.W(pre + "multihead_attn.in_proj_weight"), self.F(pre + "multihead_attn.in_proj_bias")
+            qkv2 = self.empty(R, 3 * HID)          # [q(x1) | k(mem) v(mem)] in the fused QKV layout
+            self.gemm(x1, cw[:HID], qkv2, R, HID, HID, 1, 1, HID, HID, 3 * HID, epi=_lib.EPI_BIAS, bias=cb[:HID])
+            self.gemm(mem, cw[HID:], qkv2[:, HID:], R, 2 * HID, HID, 1, 1, HID, HID, 3 * HID, epi=_lib.EPI_BIAS,
+                      bias=cb[HID:])
+            ctx2, lse2 = self.empty(R, HID), self._f32(B, NH, L)
+            self._attn_any_fwd(qkv2, ctx2, lse2, B, L, None, ddrop, r0 + 2)
+            ca = self.empty(R, HID)
+            self.linear(ctx2, self.W(pre + "multihead_attn.out_proj.weight"),
+                        self.F(pre + "multihead_attn.out_proj.bias"), ca, R)
+            x2, ln2 = self.empty(R, HID), (self.empty(R, HID), self._f32(R), self._f32(R))
+            self.ln_fwd(ca, x1, pre + "norm2", R, x2, *ln2, 1e-5, ddrop, 1, r0 + 3)
+            f1 = self.empty(R, DEC_FF)
+            self.linear(x2, self.W(pre + "linear1.weight"), self.F(pre + "linear1.bias"), f1, R, epi=_lib.EPI_BIAS_RELU)
+            self.dropout(f1, 1, ddrop, r0 + 4)
+            f2 = self.empty(R, HID)
+            self.linear(f1, self.W(pre + "linear2.weight"), self.F(pre + "linear2.bias"), f2, R)
+            x3, ln3 = self.empty(R, HID), (self.empty(R, HID), self._f32(R), self._f32(R))
+            self.ln_fwd(f2, x2, pre + "norm3", R, x3, *ln3, 1e-5, ddrop, 1, r0 + 5)
+            st.append(dict(x=x, qkv=qkv, ctx=ctx, lse=lse, ln1=ln1, x1=x1, qkv2=qkv2, ctx2=ctx2, lse2=lse2, ln2=ln2,
+                           x2=x2, f1=f1, ln3=ln3))
+            x = x3
+        t["sdec"] = dict(layers=st, mem=mem)
+        cross = self._f32(B, HID)
+        call("eegf_seq_mean", self.code, B, L, HID, P(x), HID, P(cross), HID, _stream())
+        return cross
+
+    def _seqdec_bwd(self, t, dcross, dtgt, dmem, B, L, ddrop, rng):
+        """backward of _seqdec_fwd: dtgt / dmem [B*L, 768] (encoder dtype) overwritten."""
+        R = B * L
+        sd = t["sdec"]
+        mem = sd["mem"]
+        dx3 = self.empty(R, HID)
+        call("eegf_seq_mean_bwd", self.code, B, L, HID, P(dcross), HID, P(dx3), HID, 0.0, _stream())
+        pscale = 1.0 / (1.0 - ddrop) if ddrop > 0 else 1.0
+        for d in reversed(range(DEC_L)):
+            pre = f"multi_head_decoder.layers.{d}."
+            s = sd["layers"][d]
+            r0 = rng + 400 + 16 * d
+            df2, dx2 = self.empty(R, HID), self.empty(R, HID)
+            self.ln_bwd(dx3, *s["ln3"], pre + "norm3", R, df2, dx2, ddrop, 1, r0 + 5)
+            self.wgrad(df2, s["f1"], pre + "linear2.weight", R, bias=pre + "linear2.bias")
+            df1 = self.empty(R, DEC_FF)
+            self.dgrad(df2, self.W(pre + "linear2.weight"), df1, R, epi=_lib.EPI_DRELU, aux=s["f1"], scale=pscale)
+            self.wgrad(df1, s["x2"], pre + "linear1.weight", R, bias=pre + "linear1.bias")
+            self.dgrad(df1, self.W(pre + "linear1.weight"), dx2, R, beta=1.0)
+            dca, dx1 = self.empty(R, HID), self.empty(R, HID)
+            self.ln_bwd(dx2, *s["ln2"], pre + "norm2", R, dca, dx1, ddrop, 1, r0 + 3)
+            self.wgrad(dca, s["ctx2"], pre + "multihead_attn.out_proj.weight", R,
+                       bias=pre + "multihead_attn.out_proj.bias")
+            dctx2 = self.empty(R, HID)
+            self.dgrad(dca, self.W(pre + "multihead_attn.out_proj.weight"), dctx2, R)
+            dqkv2 = self.empty(R, 3 * HID)
+            self._attn_any_bwd(s["qkv2"], s["ctx2"], dctx2, s["lse2"], dqkv2, B, L, None, ddrop, r0 + 2)
+            wn, bn = pre + "multihead_attn.in_proj_weight", pre + "multihead_attn.in_proj_bias"
+            cw = self.W(wn)
+            gw = self.G(wn) if self.need(wn) else None
+            gb = self.G(bn) if self.need(bn) else None
+            self.wgrad(dqkv2, s["x1"], wn, R, ldd=3 * HID, gw=None if gw is None else gw[:HID],
+                       gb=None if gb is None else gb[:HID])
+            self.wgrad(dqkv2[:, HID:], mem, wn, R, ldd=3 * HID, gw=None if gw is None else gw[HID:],
+                       gb=None if gb is None else gb[HID:])
+            self.dgrad(dqkv2, cw[:HID], dx1, R, ldd=3 * HID, beta=1.0)
+            self.dgrad(dqkv2[:, HID:], cw[HID:], dmem, R, ldd=3 * HID, beta=0.0 if d == DEC_L - 1 else 1.0)
+            dsa, dx = self.empty(R, HID), (dtgt if d == 0 else self.empty(R, HID))
+            self.ln_bwd(dx1, *s["ln1"], pre + "norm1", R, dsa, dx, ddrop, 1, r0 + 1)
+            self.wgrad(dsa, s["ctx"], pre + "self_attn.out_proj.weight", R, bias=pre + "self_attn.out_proj.bias")
+            dctx = self.empty(R, HID)
+            self.dgrad(dsa, self.W(pre + "self_attn.out_proj.weight"), dctx, R)
+            dqkv = self.empty(R, 3 * HID)
+            self._attn_any_bwd(s["qkv"], s["ctx"], dctx, s["lse"], dqkv, B, L, None, ddrop, r0)
+            self.wgrad(dqkv, s["x"], pre + "self_attn.in_proj_weight", R, bias=pre + "self_attn.in_proj_bias")
+            self.dgrad(dqkv, self.W(pre + "self_attn.in_proj_weight"), dx, R, beta=1.0)
+            dx3 = dx
+
+    # --------------------------------------------------------- TISC 2-token encoder (models.py:215-272)
+    def _enc2_fwd(self, t, X, B, ddrop, rng):
+        """multi_head_encoder over the two tokens [mean(EEG seq), action] of each sample, then
+        .mean(dim=0) (models.py:251-253): post-norm TransformerEncoderLayer x3 (ReLU, 2048, LN 1e-5),
+        fp32 like the single-query decoder; X [2B, 768] fp32 (row 2b, 2b+1 = sample b's tokens)."""
+        R = 2 * B
+        st = []
+        for e in range(DEC_L):
+            pre = f"multi_head_encoder.layers.{e}."
+            r0 = rng + 500 + 16 * e
+            qkv = self.eh(R, 3 * HID)
+            self.linear(X, self.F(pre + "self_attn.in_proj_weight"), self.F(pre + "self_attn.in_proj_bias"), qkv, R)
+            ctx, probs = self.eh(R, HID), self._f32(B, NH, 2, 2)
+            call("eegf_attn_small_fwd", F32, B, 2, P(qkv), 3 * HID, DH ** -0.5, float(ddrop), self.cfg.seed, r0,
+                 P(ctx), HID, P(probs), _stream())
+            sa = self.eh(R, HID)
+            self.linear(ctx, self.F(pre + "self_attn.out_proj.weight"), self.F(pre + "self_attn.out_proj.bias"), sa, R)
+            x1, ln1 = self.eh(R, HID), (self.eh(R, HID), self._f32(R), self._f32(R))
+            self.ln_fwd(sa, X, pre + "norm1", R, x1, *ln1, 1e-5, ddrop, 1, r0 + 1)
+            f1 = self.eh(R, DEC_FF)
+            self.linear(x1, self.F(pre + "linear1.weight"), self.F(pre + "linear1.bias"), f1, R, epi=_lib.EPI_BIAS_RELU)
+            self.dropout(f1, 1, ddrop, r0 + 2)
+            f2 = self.eh(R, HID)
+            self.linear(f1, self.F(pre + "linear2.weight"), self.F(pre + "linear2.bias"), f2, R)
+            x2, ln2 = self.eh(R, HID), (self.eh(R, HID), self._f32(R), self._f32(R))
+            self.ln_fwd(f2, x1, pre + "norm2", R, x2, *ln2, 1e-5, ddrop, 1, r0 + 3)
+            st.append(dict(x=X, qkv=qkv, ctx=ctx, probs=probs, ln1=ln1, x1=x1, f1=f1, ln2=ln2))
+            X = x2
+        t["enc"] = st
+        enc = self._f32(B, HID)
+        call("eegf_seq_mean", F32, B, 2, HID, P(X), HID, P(enc), HID, _stream())
+        return enc
+
+    def _enc2_bwd(self, t, dX, B, ddrop, rng):
+        """backward of _enc2_fwd: dX [2B, 768] fp32, the gradient at the encoder output on entry and
+        at its input on return (updated in place)."""
+        R = 2 * B
+        pscale = 1.0 / (1.0 - ddrop) if ddrop > 0 else 1.0
+        for e in reversed(range(DEC_L)):
+            pre = f"multi_head_encoder.layers.{e}."
+            s = t["enc"][e]
+            r0 = rng + 500 + 16 * e
+            df2, dx1 = self.eh(R, HID), self.eh(R, HID)
+            self.ln_bwd(dX, *s["ln2"], pre + "norm2", R, df2, dx1, ddrop, 1, r0 + 3)
+            self.wgrad(df2, s["f1"], pre + "linear2.weight", R, bias=pre + "linear2.bias")
+            df1 = self.eh(R, DEC_FF)
+            self.dgrad(df2, self.F(pre + "linear2.weight"), df1, R, epi=_lib.EPI_DRELU, aux=s["f1"], scale=pscale)
+            self.wgrad(df1, s["x1"], pre + "linear1.weight", R, bias=pre + "linear1.bias")
+            self.dgrad(df1, self.F(pre + "linear1.weight"), dx1, R, beta=1.0)
+            dsa = self.eh(R, HID)
+            self.ln_bwd(dx1, *s["ln1"], pre + "norm1", R, dsa, dX, ddrop, 1, r0 + 1)
+            self.wgrad(dsa, s["ctx"], pre + "self_attn.out_proj.weight", R, bias=pre + "self_attn.out_proj.bias")
+            dctx = self.eh(R, HID)
+            self.dgrad(dsa, self.F(pre + "self_attn.out_proj.weight"), dctx, R)
+            dqkv = self.eh(R, 3 * HID)
+            call("eegf_attn_small_bwd", F32, B, 2, P(s["qkv"]), 3 * HID, P(s["probs"]), P(dctx), HID, DH ** -0.5,
+                 float(ddrop), self.cfg.seed, r0, P(dqkv), 3 * HID, _stream())
+            self.wgrad(dqkv, s["x"], pre + "self_attn.in_proj_weight", R, bias=pre + "self_attn.in_proj_bias")
+            self.dgrad(dqkv, self.F(pre + "self_attn.in_proj_weight"), dX, R, beta=1.0)
+
     def _varlen_plan(self, mask, B, L):
         """Contract T pad skipping: per-row token counts of the attention mask (one device pass, one
         small D2H copy), cu_seqlens, and the packed row count rounded up to the 256-row GEMM tile.
@@ -389,17 +588,74 @@ class FusionEngine:
     # =================================================================== forward
     def forward(self, batch: dict, hard: bool, training: bool, save: bool = True):
         """batch (device tensors): contract W: eeg [B,C,T] f32, act [B,A] f32;
-        contract T: title_input [B,L] i64, text_mask [B,L] i64, frame_input [B,1,512] f32."""
+        contract T: title_input [B,L] i64, text_mask [B,L] i64, frame_input [B,1,512] f32 (the modality
+        variants add title_input2 / text_mask2 (TTCA) or frame_input2 (IICA), MODALS)."""
         cfg = self.cfg
         self._refresh_shadow()
         sv = Saved(hard=hard, training=training)
         t = sv.t
         sv.rng = self.rng_counter
         self.rng_counter += 1 << 12
+        ddrop = cfg.dec_dropout if training else 0.0
+        modal = cfg.modal
+        if modal == "ii":
+            # IICA (models.py:176-214): no BERT; the decoder's memory is the action image token
+            ve, va = self._visual_fwd(batch["frame_input"], t, "act"), self._visual_fwd(batch["frame_input2"], t, "act2")
+            B = ve.shape[0]
+            sv.B = sv.Bb = B
+            sv.L = 1
+            cross = self._dec1_fwd(t, ve, va, 1, None, ddrop, sv.rng)
+            feats = (ve, va, cross)
+        else:
+            bb = batch
+            if modal == "tt":
+                # TTCA (models.py:84-129): one BERT pass over both token batches (shared weights)
+                bb = {"title_input": torch.cat((batch["title_input"], batch["title_input2"])).contiguous(),
+                      "text_mask": torch.cat((batch["text_mask"], batch["text_mask2"])).contiguous()}
+            h, pooled = self._bert_fwd(bb, sv, save, training)
+            B, L = sv.B, sv.L
+            if modal == "tt":
+                B = B // 2
+                sv.B = B
+                cross = self._seqdec_fwd(t, h[B * L:], h[:B * L], B, L, ddrop, sv.rng)
+                feats = (pooled[:B], pooled[B:], cross)
+            elif modal == "tisc":
+                # TISC (models.py:215-272): tokens [mean(EEG seq), action image] -> 3-layer encoder -> mean
+                X = self.eh(2 * B, HID)
+                call("eegf_seq_mean", self.code, B, L, HID, P(h), HID, P(X), 2 * HID, _stream())
+                vis = self._visual_fwd(batch["frame_input"], t, "act", out=X[1::2])
+                enc = self._enc2_fwd(t, X, B, ddrop, sv.rng)
+                feats = (pooled, vis, enc)
+            else:
+                act = batch["act"] if cfg.contract == "W" else batch["frame_input"]
+                vis = self._visual_fwd(act, t, "act")
+                cross = self._dec1_fwd(t, vis, h, L, t["kbias"], ddrop, sv.rng)
+                feats = (vis, pooled, cross) if modal == "it" else (pooled, vis, cross)
+        t["vis"] = feats
+
+        # ---------------- fusion + privacy stage + head (fp32)
+        logits, fh = self.fuse_head_fwd(*feats, hard, sv.rng)
+        t.update(fh)
+        return logits, sv
+
+    def _visual_fwd(self, x, t, key, out=None):
+        """visual_encoder on [B,1,in] / [B,in] fp32 (model.py:18,36): out [B,768] fp32 (or a strided
+        row view)"""
+        B = x.shape[0]
+        act = x.reshape(B, -1).contiguous().float()
+        vis = out if out is not None else self.eh(B, HID)
+        self.gemm(act, self.F("visual_encoder.weight"), vis, B, HID, act.shape[1], 1, 1, act.shape[1], act.shape[1],
+                  vis.stride(0), epi=_lib.EPI_BIAS, bias=self.F("visual_encoder.bias"))
+        t[key] = act
+        return vis
+
+    def _bert_fwd(self, batch, sv, save, training):
+        """EEG front-end + BertModel (model.py:37-39): -> (sequence output [B*L, 768] in the compute
+        dtype, padded layout; pooled [B, 768] fp32)."""
+        cfg = self.cfg
+        t = sv.t
         pdrop = cfg.hidden_dropout if training else 0.0
         adrop = cfg.attn_dropout if training else 0.0
-        ddrop = cfg.dec_dropout if training else 0.0
-
         # ---------------- EEG front-end + BERT embeddings
         if cfg.contract == "W":
             eeg = batch["eeg"]
@@ -416,9 +672,15 @@ class FusionEngine:
             mask = batch["text_mask"]
             kbias = torch.empty(B, L, dtype=torch.float32, device=self.a.device)
             call("eegf_key_bias", B * L, P(mask), P(kbias), _stream())
-            # DP-SGD's per-sample norms index sites by B x L rows: it keeps the padded layout
-            vl = self._varlen_plan(mask, B, L) if cfg.varlen and self.psn is None else None
-            if vl is None:
+            # DP-SGD's per-sample norms index sites by B x L rows: it keeps the padded layout; TTCA /
+            # TISC consume the padded positions' outputs (unmasked decoder memory, plain sequence mean)
+            packable = cfg.varlen and self.psn is None and cfg.modal in ("ti", "it")
+            vl = self._varlen_plan(mask, B, L) if packable else None
+            if vl is None and (L % 256 or L % 128):
+                # dense lengths the dense attention kernels do not take: the varlen kernels with one
+                # full-length sequence per row and the key mask
+                vl = self._uniform_plan(B, L, kbias)
+            if vl is None or vl.get("uniform"):
                 x = self.empty(B * L, HID)
                 call("eegf_embed_gather", self.code, B * L, HID, P(ids),
                      P(self.F("bert.embeddings.word_embeddings.weight")), P(x), _stream())
@@ -431,7 +693,7 @@ class FusionEngine:
                      P(self.F("bert.embeddings.position_embeddings.weight")), P(x), P(ids_p), _stream())
                 t["ids"] = ids_p
             sv.vl = vl
-        sv.B, sv.L = B, L
+        sv.B, sv.Bb, sv.L = B, B, L
         vl = sv.vl
         if vl is None:
             if save and L % 256:
@@ -448,9 +710,10 @@ class FusionEngine:
         # the FFN pre-activations are not stored
         s0, m0, r0 = (self.empty(R, HID), self._f32(R), self._f32(R)) if save else (None, None, None)
         # position rows: the LN table add (dense) or already in the packed gather (varlen)
+        packed = vl is not None and not vl.get("uniform")
         self.ln_fwd(x, None, e + "LayerNorm", R, h, s0, m0, r0, 1e-12, pdrop, 2, sv.rng + 1,
-                    table=self.F(e + "position_embeddings.weight") if vl is None else None,
-                    period=L if vl is None else 1, table2=self.F(e + "token_type_embeddings.weight"))
+                    table=None if packed else self.F(e + "position_embeddings.weight"),
+                    period=1 if packed else L, table2=self.F(e + "token_type_embeddings.weight"))
         t["emb"] = (s0, m0, r0)
         scale = DH ** -0.5
 
@@ -471,8 +734,9 @@ class FusionEngine:
                 call("eegf_attn_fwd", self.code, B, NH, L, P(qkv), 3 * HID, P(kbias), scale, float(adrop),
                      self.cfg.seed, sv.rng + 12 + 3 * i, P(ctx), HID, P(lse), P(bits), _stream())
             else:
-                call("eegf_attn_varlen_fwd", self.code, B, NH, L, P(vl["cu"]), vl["T"], R, P(qkv), 3 * HID, scale,
-                     float(adrop), self.cfg.seed, sv.rng + 12 + 3 * i, P(ctx), HID, P(lse), _stream())
+                call("eegf_attn_varlen_fwd", self.code, B, NH, L, P(vl["cu"]), vl["T"], R, P(qkv), 3 * HID,
+                     P(vl.get("kbias")), scale, float(adrop), self.cfg.seed, sv.rng + 12 + 3 * i, P(ctx), HID, P(lse),
+                     _stream())
             self._ev_end("attn_fwd", ev, 4.0 * B * NH * L * L * DH)
             ao = self.ws.get("ao", R * HID, self.dt).view(R, HID)
             self.linear(ctx, self.W(pre + "attention.output.dense.weight"), self.F(pre + "attention.output.dense.bias"),
@@ -497,7 +761,7 @@ class FusionEngine:
                                    ln2=(s2, m2, r2)))
             h = h2
         t["layers"] = layers
-        if vl is not None:        # decoder memory / pooler input: the padded [B, L] layout, zero pad rows
+        if packed:                # decoder memory / pooler input: the padded [B, L] layout, zero pad rows
             hp = self.empty(B * L, HID)
             call("eegf_varlen_rows", self.code, B, L, HID, P(vl["cu"]), vl["T"], R, P(h), HID, P(hp), HID, 1,
                  _stream())
@@ -507,15 +771,15 @@ class FusionEngine:
         self.linear(h, self.W("bert.pooler.dense.weight"), self.F("bert.pooler.dense.bias"), pooled, B, lda=L * HID,
                     epi=_lib.EPI_BIAS_TANH)
         t["pooled"] = pooled
+        return h, pooled
 
-        # ---------------- action encoder (fp32)
-        act = batch["act"] if cfg.contract == "W" else batch["frame_input"].reshape(B, -1)
-        act = act.contiguous().float()
-        vis = self.eh(B, HID)
-        self.linear(act, self.F("visual_encoder.weight"), self.F("visual_encoder.bias"), vis, B)
-        t["act"], t["vis"] = act, vis
-
-        # ---------------- decoder (single query token; fp32 over the encoder-dtype memory)
+    def _dec1_fwd(self, t, vis, h, L, kbias, ddrop, rng):
+        """multi_head_decoder with one query token per sample (model.py:40-44) over the memory h
+        [B*L, 768] (encoder dtype, or fp32 for IICA's single-token memory), memory key bias [B, L]
+        (nullable); fp32, single-query rewrite.  -> cross [B, 768] fp32."""
+        B = vis.shape[0]
+        scale = DH ** -0.5
+        t["dmem_src"] = (h, L, kbias)
         x = vis
         dl = []
         for d in range(DEC_L):
@@ -524,11 +788,11 @@ class FusionEngine:
             v = self.eh(B, HID)
             self.linear(x, in_w[2 * HID:], in_b[2 * HID:], v, B)
             # one query, one key: the attention weight is 1, so dropout of it is a per-(row, head) mask on v
-            self.dropout(v, 64, ddrop, sv.rng + 103 + 8 * d)
+            self.dropout(v, 64, ddrop, rng + 103 + 8 * d)
             sa = self.eh(B, HID)
             self.linear(v, self.F(pre + "self_attn.out_proj.weight"), self.F(pre + "self_attn.out_proj.bias"), sa, B)
             x1, ln1 = self.eh(B, HID), (self.eh(B, HID), self._f32(B), self._f32(B))
-            self.ln_fwd(sa, x, pre + "norm1", B, x1, *ln1, 1e-5, ddrop, 1, sv.rng + 100 + 8 * d)
+            self.ln_fwd(sa, x, pre + "norm1", B, x1, *ln1, 1e-5, ddrop, 1, rng + 100 + 8 * d)
             cw, cb = self.F(pre + "multihead_attn.in_proj_weight"), self.F(pre + "multihead_attn.in_proj_bias")
             q = self.eh(B, HID)
             self.linear(x1, cw[:HID], cb[:HID], q, B)
@@ -541,7 +805,7 @@ class FusionEngine:
             cc = self.eh(B, NH, HID)
             xws = self.ws.get("xattn", B * NH * L, torch.float32)
             call("eegf_xattn_fwd", _code(h), F32, B, L, P(h), P(qp), P(kbias), float(ddrop), self.cfg.seed,
-                 sv.rng + 104 + 8 * d, P(xws), P(probs), P(psum), P(cc), _stream())
+                 rng + 104 + 8 * d, P(xws), P(probs), P(psum), P(cc), _stream())
             ctxd = self.eh(B, HID)
             # ctx[b, h*64+n] = sum_c cc[b,h,c] Wv[h*64+n, c] + s[b,h] bv[h*64+n]   (s = sum_j p~_j; 1 w/o dropout)
             self.gemm(cc, cw[2 * HID:], ctxd, B, DH, HID, 1, 1, NH * HID, HID, HID,
@@ -553,24 +817,19 @@ class FusionEngine:
             self.linear(ctxd, self.F(pre + "multihead_attn.out_proj.weight"),
                         self.F(pre + "multihead_attn.out_proj.bias"), ca, B)
             x2, ln2 = self.eh(B, HID), (self.eh(B, HID), self._f32(B), self._f32(B))
-            self.ln_fwd(ca, x1, pre + "norm2", B, x2, *ln2, 1e-5, ddrop, 1, sv.rng + 101 + 8 * d)
+            self.ln_fwd(ca, x1, pre + "norm2", B, x2, *ln2, 1e-5, ddrop, 1, rng + 101 + 8 * d)
             f1 = self.eh(B, DEC_FF)
             self.linear(x2, self.F(pre + "linear1.weight"), self.F(pre + "linear1.bias"), f1, B, epi=_lib.EPI_BIAS_RELU)
-            self.dropout(f1, 1, ddrop, sv.rng + 105 + 8 * d)      # _ff_block's inner dropout
+            self.dropout(f1, 1, ddrop, rng + 105 + 8 * d)      # _ff_block's inner dropout
             f2 = self.eh(B, HID)
             self.linear(f1, self.F(pre + "linear2.weight"), self.F(pre + "linear2.bias"), f2, B)
             x3, ln3 = self.eh(B, HID), (self.eh(B, HID), self._f32(B), self._f32(B))
-            self.ln_fwd(f2, x2, pre + "norm3", B, x3, *ln3, 1e-5, ddrop, 1, sv.rng + 102 + 8 * d)
+            self.ln_fwd(f2, x2, pre + "norm3", B, x3, *ln3, 1e-5, ddrop, 1, rng + 102 + 8 * d)
             dl.append(dict(x=x, v=v, x1=x1, ln1=ln1, q=q, qp=qp, probs=probs, psum=psum, cc=cc, ctx=ctxd, x2=x2,
                            ln2=ln2, f1=f1, ln3=ln3))
             x = x3
         t["dec"] = dl
-        cross = x
-
-        # ---------------- fusion + privacy stage + head (fp32)
-        logits, fh = self.fuse_head_fwd(pooled, vis, cross, hard, sv.rng)
-        t.update(fh)
-        return logits, sv
+        return x
 
     def fuse_head_fwd(self, pooled, vis, cross, hard: bool, rng: int):
         """concat + min-max + privacy stage (one kernel) and the fc head over the three encoder
@@ -587,7 +846,8 @@ class FusionEngine:
         rng_ = self._f32(B)
         inj = self.injected or {}
         eps_a = math.exp(cfg.eps)
-        call("eegf_fusion_fwd", F32, B, self.variant, P(pooled), HID, P(vis), HID, P(cross), HID,
+        call("eegf_fusion_fwd", F32, B, self.variant, P(pooled), pooled.stride(0), P(vis), vis.stride(0), P(cross),
+             cross.stride(0),
              P(self.F("DP")) if "DP" in self.a.offsets else None, P(inj.get("noise")), P(inj.get("gumbels")),
              P(inj.get("row_noise")), int(hard), EPS_MODES.index(cfg.eps_mode), eps_a, 1.0 / cfg.eps,
              self.cfg.seed, rng + 200, P(g), P(xn), P(amin), P(amax), P(rng_), _stream())
@@ -617,25 +877,64 @@ class FusionEngine:
         (DP gradient only — the PriGumbel DP pass)."""
         cfg = self.cfg
         t = sv.t
-        B, L = sv.B, sv.L
-        R, vl = sv.R or B * L, sv.vl
-        pdrop = cfg.hidden_dropout if sv.training else 0.0
-        adrop = cfg.attn_dropout if sv.training else 0.0
         ddrop = cfg.dec_dropout if sv.training else 0.0
-        dpooled, dvis, dcross = self.fuse_head_bwd(t, dlogits, sv.hard, sv.rng)
+        d1, d2, d3 = self.fuse_head_bwd(t, dlogits, sv.hard, sv.rng)
         if head_only:
             return
-
-        # ---------------- decoder backward (fp32; memory gradient in the encoder dtype)
-        mem = t["mem"]
+        modal, B = cfg.modal, sv.B
+        if modal == "ii":
+            dva = self.eh(B, HID)                                   # decoder memory (action token) grad
+            dx = self._dec1_bwd(t, d3, dva, ddrop, sv.rng)
+            call("eegf_axpby", F32, B * HID, 1.0, P(dx), 1.0, P(d1), _stream())
+            call("eegf_axpby", F32, B * HID, 1.0, P(d2), 1.0, P(dva), _stream())
+            self._visual_bwd(d1, t["act"])
+            self._visual_bwd(dva, t["act2"])
+            self._ready(lambda n: True)
+            return
+        L = sv.L
+        if modal == "tt":
+            dmem = self.empty(2 * B * L, HID)                       # [eeg rows | act rows]
+            self._seqdec_bwd(t, d3, dmem[B * L:], dmem[:B * L], B, L, ddrop, sv.rng)
+            dpool = self.eh(2 * B, HID)
+            call("eegf_axpby", F32, B * HID, 1.0, P(d1), 0.0, P(dpool[:B]), _stream())
+            call("eegf_axpby", F32, B * HID, 1.0, P(d2), 0.0, P(dpool[B:]), _stream())
+            self._bert_bwd(sv, dmem, dpool)
+            return
+        if modal == "tisc":
+            dX = self.eh(2 * B, HID)
+            call("eegf_seq_mean_bwd", F32, B, 2, HID, P(d3), HID, P(dX), HID, 0.0, _stream())
+            self._enc2_bwd(t, dX, B, ddrop, sv.rng)                 # dX <- d(encoder input)
+            dmem = self.empty(B * L, HID)
+            call("eegf_seq_mean_bwd", self.code, B, L, HID, P(dX), 2 * HID, P(dmem), HID, 0.0, _stream())
+            self._visual_bwd(d2, t["act"])
+            self._visual_bwd(dX[1::2], t["act"], ldd=2 * HID)
+            self._bert_bwd(sv, dmem, d1)
+            return
+        dpooled, dvis = (d2, d1) if modal == "it" else (d1, d2)
         dmem = self.empty(B * L, HID)
+        dx = self._dec1_bwd(t, d3, dmem, ddrop, sv.rng)
+        # vis receives the fusion path + the decoder path
+        call("eegf_axpby", F32, B * HID, 1.0, P(dx), 1.0, P(dvis), _stream())
+        self._visual_bwd(dvis, t["act"])
+        self._bert_bwd(sv, dmem, dpooled)
+
+    def _visual_bwd(self, dvis, act, ldd=None):
+        B = act.shape[0]
+        self.wgrad(dvis, act, "visual_encoder.weight", B, ldd=ldd)
+        self.bgrad(dvis, "visual_encoder.bias", B, ld=ldd)
+
+    def _dec1_bwd(self, t, dcross, dmem, ddrop, rng):
+        """backward of _dec1_fwd: writes the memory gradient into dmem (overwritten) and returns the
+        query-token (tgt) gradient [B, 768] fp32."""
+        mem, L, _ = t["dmem_src"]
+        B = dcross.shape[0]
         dx3 = dcross
         scale = DH ** -0.5
         for d in reversed(range(DEC_L)):
             pre = f"multi_head_decoder.layers.{d}."
             s = t["dec"][d]
             df2, dx2 = self.eh(B, HID), self.eh(B, HID)
-            self.ln_bwd(dx3, *s["ln3"], pre + "norm3", B, df2, dx2, ddrop, 1, sv.rng + 102 + 8 * d)
+            self.ln_bwd(dx3, *s["ln3"], pre + "norm3", B, df2, dx2, ddrop, 1, rng + 102 + 8 * d)
             self.wgrad(df2, s["f1"], pre + "linear2.weight", B)
             self.bgrad(df2, pre + "linear2.bias", B)
             df1 = self.eh(B, DEC_FF)
@@ -646,7 +945,7 @@ class FusionEngine:
             self.bgrad(df1, pre + "linear1.bias", B)
             self.dgrad(df1, self.F(pre + "linear1.weight"), dx2, B, beta=1.0)
             dca, dx1 = self.eh(B, HID), self.eh(B, HID)
-            self.ln_bwd(dx2, *s["ln2"], pre + "norm2", B, dca, dx1, ddrop, 1, sv.rng + 101 + 8 * d)
+            self.ln_bwd(dx2, *s["ln2"], pre + "norm2", B, dca, dx1, ddrop, 1, rng + 101 + 8 * d)
             self.wgrad(dca, s["ctx"], pre + "multihead_attn.out_proj.weight", B)
             self.bgrad(dca, pre + "multihead_attn.out_proj.bias", B)
             dctx = self.eh(B, HID)
@@ -673,7 +972,7 @@ class FusionEngine:
             dqp = self.eh(B, NH, HID)
             xws = self.ws.get("xattn", B * NH * L, torch.float32)
             call("eegf_xattn_bwd", _code(mem), F32, B, L, P(mem), P(s["qp"]), P(s["probs"]), P(dpsum), P(dcc),
-                 float(ddrop), self.cfg.seed, sv.rng + 104 + 8 * d, P(xws), P(dmem), 0.0 if d == DEC_L - 1 else 1.0,
+                 float(ddrop), self.cfg.seed, rng + 104 + 8 * d, P(xws), P(dmem), 0.0 if d == DEC_L - 1 else 1.0,
                  P(dqp), _stream())
             dq = self.eh(B, HID)
             # dq[b, h*64+i] = sum_c dqp[b,h,c] Wk[h*64+i, c] / 8
@@ -688,12 +987,12 @@ class FusionEngine:
                 self.bgrad(dq, bname, B, out=self.G(bname)[:HID])
             self.dgrad(dq, cw[:HID], dx1, B, beta=1.0)
             dsa, dx = self.eh(B, HID), self.eh(B, HID)
-            self.ln_bwd(dx1, *s["ln1"], pre + "norm1", B, dsa, dx, ddrop, 1, sv.rng + 100 + 8 * d)
+            self.ln_bwd(dx1, *s["ln1"], pre + "norm1", B, dsa, dx, ddrop, 1, rng + 100 + 8 * d)
             self.wgrad(dsa, s["v"], pre + "self_attn.out_proj.weight", B)
             self.bgrad(dsa, pre + "self_attn.out_proj.bias", B)
             dv = self.eh(B, HID)
             self.dgrad(dsa, self.F(pre + "self_attn.out_proj.weight"), dv, B)
-            self.dropout(dv, 64, ddrop, sv.rng + 103 + 8 * d)
+            self.dropout(dv, 64, ddrop, rng + 103 + 8 * d)
             sw = self.F(pre + "self_attn.in_proj_weight")
             if self.need(pre + "self_attn.in_proj_weight"):
                 self.gemm(dv, s["x"], self.G(pre + "self_attn.in_proj_weight")[2 * HID:], HID, HID, B, 0, 0, HID, HID,
@@ -702,11 +1001,20 @@ class FusionEngine:
                 self.bgrad(dv, pre + "self_attn.in_proj_bias", B, out=self.G(pre + "self_attn.in_proj_bias")[2 * HID:])
             self.dgrad(dv, sw[2 * HID:], dx, B, beta=1.0)
             dx3 = dx
-        # vis receives the fusion path + the decoder path
-        call("eegf_axpby", F32, B * HID, 1.0, P(dx3), 1.0, P(dvis), _stream())
-        self.wgrad(dvis, t["act"], "visual_encoder.weight", B)
-        self.bgrad(dvis, "visual_encoder.bias", B)
+        return dx3
 
+    def _bert_bwd(self, sv, dmem, dpooled):
+        """pooler + BertModel + EEG front-end backward from the sequence-output gradient dmem
+        [B*L, 768] (padded layout, encoder dtype; the pooler's part is added here) and dpooled fp32."""
+        cfg = self.cfg
+        t = sv.t
+        B, L = sv.Bb, sv.L
+        R, vl = sv.R or B * L, sv.vl
+        packed = vl is not None and not vl.get("uniform")
+        pdrop = cfg.hidden_dropout if sv.training else 0.0
+        adrop = cfg.attn_dropout if sv.training else 0.0
+        mem = t["mem"]
+        scale = DH ** -0.5
         # ---------------- pooler (fp32 tanh derivative, encoder-dtype GEMMs)
         pooled = t["pooled"]
         dpp32 = self.eh(B, HID)
@@ -725,7 +1033,7 @@ class FusionEngine:
 
         # ---------------- BERT encoder backward
         dh = dmem
-        if vl is not None:        # padded memory gradient -> the packed rows (zeros past the tokens)
+        if packed:                # padded memory gradient -> the packed rows (zeros past the tokens)
             dh = self.empty(R, HID)
             call("eegf_varlen_rows", self.code, B, L, HID, P(vl["cu"]), vl["T"], R, P(dmem), HID, P(dh), HID, 0,
                  _stream())
@@ -763,8 +1071,8 @@ class FusionEngine:
                      P(dqkv), P(dq_ws), _stream())
             else:
                 call("eegf_attn_varlen_bwd", self.code, B, NH, L, P(vl["cu"]), vl["T"], R, P(s["qkv"]), 3 * HID,
-                     scale, float(adrop), self.cfg.seed, sv.rng + 12 + 3 * i, P(s["ctx"]), P(dctx), HID, P(s["lse"]),
-                     P(dqkv), P(dq_ws), _stream())
+                     P(vl.get("kbias")), scale, float(adrop), self.cfg.seed, sv.rng + 12 + 3 * i, P(s["ctx"]), P(dctx),
+                     HID, P(s["lse"]), P(dqkv), P(dq_ws), _stream())
             self._ev_end("attn_bwd", ev, 2.5 * 4.0 * B * NH * L * L * DH)
             qn = pre + "attention.self.query.weight"
             bn = pre + "attention.self.query.bias"
@@ -786,7 +1094,7 @@ class FusionEngine:
         self.ln_bwd(dh, *t["emb"], e + "LayerNorm", R, demb, None, pdrop, 2, sv.rng + 1)
         if self.need(e + "position_embeddings.weight"):
             dpos = demb
-            if vl is not None:    # position j of every sequence: the padded layout's period-L column sums
+            if packed:            # position j of every sequence: the padded layout's period-L column sums
                 dpos = self.empty(B * L, HID)
                 call("eegf_varlen_rows", self.code, B, L, HID, P(vl["cu"]), vl["T"], R, P(demb), HID, P(dpos), HID,
                      1, _stream())
@@ -845,7 +1153,8 @@ class FusionEngine:
         B = pooled.shape[0]
         inj = self.injected or {}
         g = self.eh(B, FUSED)
-        call("eegf_fusion_fwd", F32, B, _lib.FUSE_PRICONCAT, P(pooled), HID, P(vis), HID, P(cross), HID, None, None,
+        call("eegf_fusion_fwd", F32, B, _lib.FUSE_PRICONCAT, P(pooled), pooled.stride(0), P(vis), vis.stride(0),
+             P(cross), cross.stride(0), None, None,
              None, None, 0, 0, math.exp(cfg.eps), 1.0 / cfg.eps, self.cfg.seed, rng + 200, P(g), None, None, None,
              None, _stream())
         z1 = self.eh(B, FUSED)
@@ -927,8 +1236,8 @@ class FusionEngine:
         """Parameters that take part in the forward graph (others keep grad None, as in torch)."""
         out = set()
         for n in self.a.offsets:
-            if n.startswith("multi_head_decoderlayer."):
-                continue                                  # unused template layer (model.py:20)
+            if n.startswith(("multi_head_decoderlayer.", "multi_head_encoderlayer.")):
+                continue                                  # unused template layer (model.py:20, models.py:227)
             if n == "bert.embeddings.word_embeddings.weight" and self.cfg.contract == "W":
                 continue
             if n == "DP" and self.variant != _lib.FUSE_PRIGUMBEL:

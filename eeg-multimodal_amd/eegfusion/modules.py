@@ -156,18 +156,26 @@ class FusionModel(nn.Module):
     def __init__(self, variant: str, contract: str = "T", eps: float = 1.0, eps_mode: str = "newfrac",
                  dtype: torch.dtype = torch.float32, eeg_channels: int = 64, act_dim: int = 32, frame_dim: int = 512,
                  with_dp: bool = True, dp_init: torch.Tensor | None = None, dropout: float = 0.1, seed: int = 980616,
-                 tau: float = 1.0):
+                 tau: float = 1.0, modal: str = "ti"):
         super().__init__()
-        self._variant, self._contract = variant, contract
-        self.bert = _bert()
-        _init_bert_(self.bert)
+        self._variant, self._contract, self._modal = variant, contract, modal
+        # module sets of the custom_models variants (models.py:28-272): no BERT in IICA, no visual
+        # encoder in TTCA, a TransformerEncoder instead of the decoder in TISC
+        if modal != "ii":
+            self.bert = _bert()
+            _init_bert_(self.bert)
         if contract == "W":
             self.eeg_encoder = nn.Linear(eeg_channels, HID)
             self.visual_encoder = nn.Linear(act_dim, HID)
-        else:
+        elif modal != "tt":
             self.visual_encoder = nn.Linear(frame_dim, HID)
-        self.multi_head_decoderlayer = nn.TransformerDecoderLayer(d_model=HID, nhead=12)
-        self.multi_head_decoder = nn.TransformerDecoder(self.multi_head_decoderlayer, num_layers=DEC_L)
+        if modal == "tisc":
+            self.multi_head_encoderlayer = nn.TransformerEncoderLayer(d_model=HID, nhead=12)
+            self.multi_head_encoder = nn.TransformerEncoder(self.multi_head_encoderlayer, num_layers=DEC_L,
+                                                            enable_nested_tensor=False)
+        else:
+            self.multi_head_decoderlayer = nn.TransformerDecoderLayer(d_model=HID, nhead=12)
+            self.multi_head_decoder = nn.TransformerDecoder(self.multi_head_decoderlayer, num_layers=DEC_L)
         if variant == "prigumbel_v1":
             # train_val.py:125-142 registration order: classifier (first assigned at :134), w, dropout,
             # fc1, fc2; no fc_layers, no DP
@@ -187,7 +195,7 @@ class FusionModel(nn.Module):
         self.eps = torch.tensor(eps)
         self._cfg = EngineConfig(contract=contract, variant=variant, dtype=dtype, eps=float(eps), eps_mode=eps_mode,
                                  hidden_dropout=dropout, attn_dropout=dropout, dec_dropout=dropout,
-                                 eeg_channels=eeg_channels, act_dim=act_dim, seed=seed, tau=float(tau))
+                                 eeg_channels=eeg_channels, act_dim=act_dim, seed=seed, tau=float(tau), modal=modal)
         self._build_arena(torch.device("cpu"))
         self._dp = None                      # DP-SGD state (eegfusion.dpsgd.GradSampleModule)
 
@@ -362,6 +370,75 @@ class TICA_LapDropout(FusionModel):
     def forward(self, eeg_txt_input, eeg_txt_mask, act_img_input, act_img_mask, epsilon, hard):
         self.eps = torch.tensor(float(epsilon))
         return self._run(self._token_batch(act_img_input, act_img_mask, eeg_txt_input, eeg_txt_mask), hard)
+
+
+def _tokens(x):
+    """token ids / masks as [B, L] int64 (a pickle may hold [1, L] per sample: [B, 1, L] batches)"""
+    return x.reshape(x.shape[0], x.shape[-1]).contiguous().long()
+
+
+class _LapDropoutVariant(FusionModel):
+    """Common body of the custom_models *_LapDropout variants: the PriGumbel newfrac gate over the
+    variant's three fused features, forward(..., epsilon, hard)."""
+
+    def __init__(self, modal: str, bert_coef=None, contract: str = "T", **kw):
+        super().__init__("prigumbel", contract=contract, modal=modal, **kw)
+        if bert_coef and os.path.exists(str(bert_coef)) and modal != "ii":
+            load_bert_weights(self, bert_coef)
+
+    def _go(self, batch, epsilon, hard):
+        self.eps = torch.tensor(float(epsilon))
+        return self._run(batch, hard)
+
+
+class TTCA_LapDropout(_LapDropoutVariant):
+    """models.py:84-129 — EEG and action both as text: one BERT (shared) over both token batches, the
+    decoder with the action sequence as target and the EEG sequence as memory (no masks), mean over the
+    target tokens; features BERT(eeg) pooled | BERT(act) pooled | cross."""
+
+    def __init__(self, bert_coef: str = "bert-base-uncased", **kw):
+        super().__init__("tt", bert_coef, **kw)
+
+    def forward(self, eeg_txt_input, eeg_txt_mask, act_txt_input, act_txt_mask, epsilon, hard):
+        return self._go({"title_input": _tokens(eeg_txt_input), "text_mask": _tokens(eeg_txt_mask),
+                         "title_input2": _tokens(act_txt_input), "text_mask2": _tokens(act_txt_mask)}, epsilon, hard)
+
+
+class ITCA_LapDropout(_LapDropoutVariant):
+    """models.py:130-175 — EEG as image (CLIP vector through visual_encoder), action as text (BERT);
+    the single-query decoder over the action sequence; features visual(eeg) | BERT(act) pooled | cross."""
+
+    def __init__(self, bert_coef: str = "bert-base-uncased", **kw):
+        super().__init__("it", bert_coef, **kw)
+
+    def forward(self, eeg_img_input, eeg_img_mask, act_txt_input, act_txt_mask, epsilon, hard):
+        return self._go({"title_input": _tokens(act_txt_input), "text_mask": _tokens(act_txt_mask),
+                         "frame_input": eeg_img_input.contiguous().float()}, epsilon, hard)
+
+
+class IICA_LapDropout(_LapDropoutVariant):
+    """models.py:176-214 — both modalities as images: no BERT; visual_encoder (shared) on both CLIP
+    vectors; the decoder with the EEG token as target and the action token as memory (length 1)."""
+
+    def __init__(self, **kw):
+        super().__init__("ii", None, **kw)
+
+    def forward(self, eeg_img_input, eeg_img_mask, act_img_input, act_img_mask, epsilon, hard):
+        return self._go({"frame_input": eeg_img_input.contiguous().float(),
+                         "frame_input2": act_img_input.contiguous().float()}, epsilon, hard)
+
+
+class TISC_LapDropout(_LapDropoutVariant):
+    """models.py:215-272 — EEG as text, action as image, 'single attention': a 3-layer
+    TransformerEncoder over the two tokens [mean of the BERT sequence output, action image embedding],
+    mean over them; features BERT(eeg) pooled | visual(act) | encoder mean."""
+
+    def __init__(self, bert_coef: str = "bert-base-uncased", **kw):
+        super().__init__("tisc", bert_coef, **kw)
+
+    def forward(self, eeg_txt_input, eeg_txt_mask, act_img_input, act_img_mask, epsilon, hard):
+        return self._go({"title_input": _tokens(eeg_txt_input), "text_mask": _tokens(eeg_txt_mask),
+                         "frame_input": act_img_input.contiguous().float()}, epsilon, hard)
 
 
 class GumbelSoftmaxDropout(nn.Module):

@@ -114,16 +114,38 @@ int eegf_varlen_rows(int dtype, int B, int S, int width, const int* cu_seqlens, 
 /* Packed self-attention (BertSelfAttention over each sequence's real tokens, no key bias): as
  * eegf_attn_fwd with the rows of sequence b at cu[b] ..; max_len = the padded length L of the batch
  * (>= every sequence length): LSE is [B, 12, max_len] and the dropout element numbering is the padded
- * ((b*12 + h)*L + q)*L + key, so a packed batch draws exactly its padded form's masks. */
+ * ((b*12 + h)*L + q)*L + key, so a packed batch draws exactly its padded form's masks.  key_bias
+ * [B, max_len] (nullable) is added to the scores as in eegf_attn_fwd: with uniform cu_seqlens
+ * (cu[b] = b*L) these kernels also run the padded layout at any L (the dense ones need L % 256). */
 int eegf_attn_varlen_fwd(int dtype, int B, int H, int max_len, const int* cu_seqlens, long packed_rows,
-                         long total_rows, const void* qkv, long ld_qkv, float scale, float drop_p,
+                         long total_rows, const void* qkv, long ld_qkv, const float* key_bias, float scale,
+                         float drop_p,
                          unsigned long long seed, unsigned long long offset, void* out, long ld_out, float* lse,
                          hipStream_t stream);
 long eegf_attn_varlen_bwd_workspace(long total_rows, int max_len);
 int eegf_attn_varlen_bwd(int dtype, int B, int H, int max_len, const int* cu_seqlens, long packed_rows,
-                         long total_rows, const void* qkv, long ld_qkv, float scale, float drop_p,
+                         long total_rows, const void* qkv, long ld_qkv, const float* key_bias, float scale,
+                         float drop_p,
                          unsigned long long seed, unsigned long long offset, const void* out, const void* dout,
                          long ld_out, const float* lse, void* dqkv, float* dq_workspace, hipStream_t stream);
+
+/* ---- modality variants (custom_models/models.py:84-272) */
+/* Self-attention over S <= 8 tokens per sample (TISC's TransformerEncoder over [mean(EEG seq), action],
+ * models.py:227-228, F.multi_head_attention_forward): rows n*S .. n*S+S-1 of qkv [N*S, >= 2304]; one wave
+ * per (sample, head); probs [N, 12, S, S] fp32 = the undropped softmax (saved for the backward);
+ * attention-weight dropout by Philox element ((n*12 + h)*S + i)*S + j. */
+int eegf_attn_small_fwd(int dtype, int N, int S, const void* qkv, long ld_qkv, float scale, float drop_p,
+                        unsigned long long seed, unsigned long long offset, void* out, long ld_out, float* probs,
+                        hipStream_t stream);
+int eegf_attn_small_bwd(int dtype, int N, int S, const void* qkv, long ld_qkv, const float* probs, const void* dout,
+                        long ld_out, float scale, float drop_p, unsigned long long seed, unsigned long long offset,
+                        void* dqkv, long ld_dqkv, hipStream_t stream);
+/* out[b] (fp32) = mean of rows b*L .. b*L+L-1 of x (TTCA decoder output / TISC sequence and token
+ * means, models.py:109, :253, :260); backward dx rows = beta dx + dmean[b] / L. */
+int eegf_seq_mean(int dtype, int B, int L, int width, const void* x, long ld_x, float* out, long ld_out,
+                  hipStream_t stream);
+int eegf_seq_mean_bwd(int dtype, int B, int L, int width, const float* dmean, long ld_dmean, void* dx, long ld_dx,
+                      float beta, hipStream_t stream);
 
 /* fusion variants (eegf_fusion_fwd/bwd) */
 #define FUSE_CONCAT 0        /* model.py ConcatModel.feature: minmax(cat)            model.py:46-50      */

@@ -157,11 +157,74 @@ def decoder_layer(p, i, x, mem, mem_pad, tgt_pad):
 
 def decoder(p, tgt, mem, mem_mask, tgt_mask):
     """multi_head_decoder(tgt, memory, tgt_key_padding_mask, memory_key_padding_mask)
-    followed by .permute(1,0,2).mean(dim=1) (model.py:40-44)."""
+    followed by .permute(1,0,2).mean(dim=1) (model.py:40-44).  mem_mask / tgt_mask None: no mask
+    (TTCA / IICA call the decoder without masks, models.py:107-108, :196-197)."""
     x = tgt
     for i in range(DEC_LAYERS):
-        x = decoder_layer(p, i, x, mem, mem_mask == 0, tgt_mask == 0)
+        x = decoder_layer(p, i, x, mem, None if mem_mask is None else mem_mask == 0,
+                          None if tgt_mask is None else tgt_mask == 0)
     return x.mean(dim=1)
+
+
+def encoder_layer(p, i, x):
+    """TransformerEncoderLayer.forward, norm_first=False, ReLU, d_ff 2048, LN 1e-5 (torch 2.10
+    transformer.py TransformerEncoderLayer; TISC_LapDropout, models.py:227-228): x [B,S,E]."""
+    pre = f"multi_head_encoder.layers.{i}."
+    sa = mha_literal(x, x, p[pre + "self_attn.in_proj_weight"], p[pre + "self_attn.in_proj_bias"],
+                     p[pre + "self_attn.out_proj.weight"], p[pre + "self_attn.out_proj.bias"], None,
+                     site=("enc_sa_w", i))
+    x = _ln(x + _drop(("enc_sa", i), sa), p[pre + "norm1.weight"], p[pre + "norm1.bias"], LN_DEC)
+    ff = _lin(_drop(("enc_ff_inner", i), F.relu(_lin(x, p, pre + "linear1"))), p, pre + "linear2")
+    return _ln(x + _drop(("enc_ff", i), ff), p[pre + "norm2.weight"], p[pre + "norm2.bias"], LN_DEC)
+
+
+# ------------------------------------------ modality variants (custom_models/models.py:84-272)
+# Batch keys (the engine's): title_input / text_mask = the first BERT input, title_input2 /
+# text_mask2 the second (TTCA), frame_input / frame_input2 the CLIP-vector inputs [B,1,512].
+MODALS = ("ti", "it", "ii", "tt", "tisc")
+
+
+def encoders_modal(p, batch, modal):
+    """-> the three fused features in the variant's concat order.
+    ti   TICA_LapDropout  (models.py:28-82):   BERT(eeg txt) | visual(act img) | decoder(act img; eeg seq)
+    it   ITCA_LapDropout  (models.py:130-175): visual(eeg img) | BERT(act txt) | decoder(eeg img; act seq)
+    ii   IICA_LapDropout  (models.py:176-214): visual(eeg img) | visual(act img) | decoder(eeg img; act img)
+    tt   TTCA_LapDropout  (models.py:84-129):  BERT(eeg txt) | BERT(act txt) | decoder(act seq; eeg seq), no masks
+    tisc TISC_LapDropout  (models.py:215-272): BERT(eeg txt) | visual(act img) | encoder([mean(eeg seq), act img])"""
+    if modal == "ti":
+        emb = bert_embeddings(p, input_ids=batch["title_input"])
+        seq, pooled = bert(p, emb, batch["text_mask"])
+        vis = _lin(batch["frame_input"], p, "visual_encoder")
+        return pooled, vis.squeeze(1), decoder(p, vis, seq, batch["text_mask"], batch.get("vedio_mask"))
+    if modal == "it":
+        emb = bert_embeddings(p, input_ids=batch["title_input"])
+        seq, pooled = bert(p, emb, batch["text_mask"])
+        vis = _lin(batch["frame_input"], p, "visual_encoder")
+        return vis.squeeze(1), pooled, decoder(p, vis, seq, batch["text_mask"], batch.get("vedio_mask"))
+    if modal == "ii":
+        ve = _lin(batch["frame_input"], p, "visual_encoder")
+        va = _lin(batch["frame_input2"], p, "visual_encoder")
+        return ve.squeeze(1), va.squeeze(1), decoder(p, ve, va, None, None)
+    if modal == "tt":
+        se, pe = bert(p, bert_embeddings(p, input_ids=batch["title_input"]), batch["text_mask"])
+        sa, pa = bert(p, bert_embeddings(p, input_ids=batch["title_input2"]), batch["text_mask2"])
+        return pe, pa, decoder(p, sa, se, None, None)
+    if modal == "tisc":
+        se, pe = bert(p, bert_embeddings(p, input_ids=batch["title_input"]), batch["text_mask"])
+        va = _lin(batch["frame_input"], p, "visual_encoder")
+        x = torch.cat((se.mean(dim=1).unsqueeze(1), va), dim=1)     # [B, 2, 768] (batch-major)
+        for i in range(DEC_LAYERS):
+            x = encoder_layer(p, i, x)
+        return pe, va.squeeze(1), x.mean(dim=1)
+    raise ValueError(modal)
+
+
+def forward_modal(p, batch, modal, noise, gumbels, eps=1.0, hard=False):
+    """the *_LapDropout forward after the encoders (models.py:69-82): min-max, PriGumbel newfrac gate,
+    fc head."""
+    f = torch.cat(encoders_modal(p, batch, modal), dim=1)
+    g = prigumbel_gate(minmax(f), p["DP"], noise, gumbels, eps, "newfrac", hard)
+    return head(p, g)
 
 
 # --------------------------------------------------------------------- fusion + privacy
@@ -301,9 +364,42 @@ def cal_loss(logits, labels):
 
 
 # -------------------------------------------------------------- parameter inventory
-def param_shapes(contract: str = "W", variant: str = "prigumbel", eeg_channels=64, act_dim=32) -> dict:
-    """state_dict names/shapes of the path (reference names, SURVEY Appendix A.6 / probe7)."""
+def param_shapes(contract: str = "W", variant: str = "prigumbel", eeg_channels=64, act_dim=32,
+                 modal: str = "ti") -> dict:
+    """state_dict names/shapes of the path (reference names, SURVEY Appendix A.6 / probe7); `modal`
+    selects a custom_models variant's module set (no BERT for ii, no visual encoder for tt, the
+    TransformerEncoder instead of the decoder for tisc)."""
     s = {}
+    if modal != "ii":
+        _bert_shapes(s)
+    if contract == "W":
+        s["eeg_encoder.weight"] = (HID, eeg_channels)
+        s["eeg_encoder.bias"] = (HID,)
+        s["visual_encoder.weight"] = (HID, act_dim)
+        s["visual_encoder.bias"] = (HID,)
+    elif modal != "tt":
+        s["visual_encoder.weight"] = (HID, 512)
+        s["visual_encoder.bias"] = (HID,)
+    if modal == "tisc":
+        for pre in ["multi_head_encoderlayer."] + [f"multi_head_encoder.layers.{i}." for i in range(DEC_LAYERS)]:
+            s[pre + "self_attn.in_proj_weight"] = (3 * HID, HID)
+            s[pre + "self_attn.in_proj_bias"] = (3 * HID,)
+            s[pre + "self_attn.out_proj.weight"] = (HID, HID)
+            s[pre + "self_attn.out_proj.bias"] = (HID,)
+            s[pre + "linear1.weight"] = (DEC_FF, HID)
+            s[pre + "linear1.bias"] = (DEC_FF,)
+            s[pre + "linear2.weight"] = (HID, DEC_FF)
+            s[pre + "linear2.bias"] = (HID,)
+            for n in ("norm1", "norm2"):
+                s[pre + n + ".weight"] = (HID,)
+                s[pre + n + ".bias"] = (HID,)
+    else:
+        _decoder_shapes(s)
+    _head_shapes(s, variant)
+    return s
+
+
+def _bert_shapes(s):
     e = "bert.embeddings."
     s[e + "word_embeddings.weight"] = (30522, HID)
     s[e + "position_embeddings.weight"] = (512, HID)
@@ -324,13 +420,9 @@ def param_shapes(contract: str = "W", variant: str = "prigumbel", eeg_channels=6
         s[pre + "output.dense.bias"] = (HID,)
     s["bert.pooler.dense.weight"] = (HID, HID)
     s["bert.pooler.dense.bias"] = (HID,)
-    if contract == "W":
-        s["eeg_encoder.weight"] = (HID, eeg_channels)
-        s["eeg_encoder.bias"] = (HID,)
-        s["visual_encoder.weight"] = (HID, act_dim)
-    else:
-        s["visual_encoder.weight"] = (HID, 512)
-    s["visual_encoder.bias"] = (HID,)
+
+
+def _decoder_shapes(s):
     for pre in ["multi_head_decoderlayer."] + [f"multi_head_decoder.layers.{i}." for i in range(DEC_LAYERS)]:
         for a in ("self_attn", "multihead_attn"):
             s[pre + a + ".in_proj_weight"] = (3 * HID, HID)
@@ -344,6 +436,9 @@ def param_shapes(contract: str = "W", variant: str = "prigumbel", eeg_channels=6
         for n in ("norm1", "norm2", "norm3"):
             s[pre + n + ".weight"] = (HID,)
             s[pre + n + ".bias"] = (HID,)
+
+
+def _head_shapes(s, variant):
     if variant == "prigumbel_v1":
         s["classifier.weight"] = (2, HID)
         s["classifier.bias"] = (2,)
@@ -352,7 +447,7 @@ def param_shapes(contract: str = "W", variant: str = "prigumbel", eeg_channels=6
         s["fc1.bias"] = (FUSED,)
         s["fc2.weight"] = (HID, FUSED)
         s["fc2.bias"] = (HID,)
-        return s
+        return
     s["fc_layers.0.weight"] = (FUSED, FUSED)
     s["fc_layers.0.bias"] = (FUSED,)
     s["fc_layers.2.weight"] = (HID, FUSED)
@@ -361,4 +456,3 @@ def param_shapes(contract: str = "W", variant: str = "prigumbel", eeg_channels=6
     s["classifier.bias"] = (2,)
     if variant in ("prigumbel", "concat"):
         s["DP"] = (1, FUSED)
-    return s

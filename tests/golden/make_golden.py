@@ -484,6 +484,73 @@ def gen_prigumbel_v1():
                               seed=SEED, B=B_W, C=C_W, T=T_W, A=A_W), out)
 
 
+def import_custom_models():
+    """python/src/custom_models/models.py (opacus stubbed, BertModel.from_pretrained local — the
+    shims of import_reference, which must run first)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("ref_custom_models", REF / "python/src/custom_models/models.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def gen_modal_variants():
+    """custom_models/models.py:84-272 — TTCA / ITCA / IICA / TISC_LapDropout (and TICA for the same
+    inputs) on contract-T style inputs: token ids [B, 128] with real lengths, CLIP-like vectors
+    [B, 1, 512]; eps 1.0, soft gate (hard for TISC), injected Laplace noise, recorded Gumbel draws,
+    CE mean.  Batch keys follow the engine (title_input / text_mask / frame_input, *2 for the
+    second input of the pair)."""
+    cm = import_custom_models()
+    B, L = 2, 128
+    out = {}
+    for ci, (modal, cls, hard) in enumerate((("ti", "TICA_LapDropout", False), ("it", "ITCA_LapDropout", False),
+                                             ("ii", "IICA_LapDropout", False), ("tt", "TTCA_LapDropout", False),
+                                             ("tisc", "TISC_LapDropout", True))):
+        torch.manual_seed(30 + ci)
+        gen = torch.Generator().manual_seed(40 + ci)
+        m = getattr(cm, cls)() if modal == "ii" else getattr(cm, cls)("bert-base-uncased")
+        m = prepare(m, "T")
+        ids, masks = [], []
+        for lens in ([51, 37], [40, 66]):
+            i_ = torch.zeros(B, L, dtype=torch.long)
+            m_ = torch.zeros(B, L, dtype=torch.long)
+            for b, n in enumerate(lens):
+                i_[b, :n] = torch.cat([torch.tensor([101]), torch.randint(1000, 1030, (n - 2,), generator=gen),
+                                       torch.tensor([102])])
+                m_[b, :n] = 1
+            ids.append(i_)
+            masks.append(m_)
+        img = [torch.randn(B, 1, 512, generator=gen) * 0.5 for _ in range(2)]
+        one = torch.ones(B, 1, dtype=torch.long)
+        labels = torch.tensor([1, 0])
+        noise = laplace_noise(gen, (B, 2304))
+        m.noiser = InjectedNoise(noise)
+        if modal == "ti":
+            args, batch = (ids[0], masks[0], img[1], one), dict(title_input=ids[0], text_mask=masks[0], frame_input=img[1])
+        elif modal == "it":
+            args, batch = (img[0], one, ids[1], masks[1]), dict(title_input=ids[1], text_mask=masks[1], frame_input=img[0])
+        elif modal == "ii":
+            args, batch = (img[0], one, img[1], one), dict(frame_input=img[0], frame_input2=img[1])
+        elif modal == "tt":
+            args, batch = (ids[0], masks[0], ids[1], masks[1]), dict(title_input=ids[0], text_mask=masks[0],
+                                                                   title_input2=ids[1], text_mask2=masks[1])
+        else:
+            args, batch = (ids[0], masks[0], img[1], one), dict(title_input=ids[0], text_mask=masks[0], frame_input=img[1])
+        with RecordExp() as rec:
+            logits = m(*args, 1.0, hard)
+        loss = nn.functional.cross_entropy(logits, labels)
+        loss.backward()
+        pre = f"{modal}:"
+        out.update({pre + k: v for k, v in batch.items()})
+        out.update({pre + "labels": labels, pre + "noise": noise, pre + "gumbels": -torch.log(rec.draws[0]),
+                    pre + "logits": logits.detach(), pre + "loss": loss.detach()})
+        out.update({pre + k: v for k, v in grad_record(m).items()})
+        print("modal", modal, float(loss))
+    save("modal_variants", dict(modals=["ti", "it", "ii", "tt", "tisc"], hard=dict(ti=False, it=False, ii=False, tt=False,
+                                                                                  tisc=True),
+                                eps=1.0, contract="T", B=B, L=L, seed=SEED), out)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
     past_acc, main_0430, ref_model = import_reference()
@@ -499,3 +566,4 @@ if __name__ == "__main__":
     gen_priconcat_lap_full(main_0430)
     gen_feawei_features()
     gen_prigumbel_v1()
+    gen_modal_variants()

@@ -21,15 +21,15 @@ def load(name: str):
     return cfg, {k: z[k] for k in z.files if k != "config"}
 
 
-@functools.lru_cache(maxsize=4)
-def _det_params_np(contract: str, variant: str, seed: int = SEED):
-    shapes = O.param_shapes(contract, variant)
+@functools.lru_cache(maxsize=8)
+def _det_params_np(contract: str, variant: str, seed: int = SEED, modal: str = "ti"):
+    shapes = O.param_shapes(contract, variant, modal=modal)
     return {k: det_tensor(seed, k, s) for k, s in shapes.items() if k != "DP"}
 
 
-def det_params(contract: str, variant: str, dp=None, requires_grad=True) -> dict[str, torch.Tensor]:
-    p = {k: torch.from_numpy(v.copy()) for k, v in _det_params_np(contract, variant).items()}
-    if "DP" in O.param_shapes(contract, variant):
+def det_params(contract: str, variant: str, dp=None, requires_grad=True, modal: str = "ti") -> dict[str, torch.Tensor]:
+    p = {k: torch.from_numpy(v.copy()) for k, v in _det_params_np(contract, variant, modal=modal).items()}
+    if "DP" in O.param_shapes(contract, variant, modal=modal):
         p["DP"] = torch.as_tensor(dp if dp is not None else np.zeros((1, O.FUSED), np.float32)).float().clone()
     for t in p.values():
         t.requires_grad_(requires_grad)
@@ -81,3 +81,9 @@ def check_grads(grads: dict, fx: dict, tol: float, skip=()):
         if e > tol:
             bad.append((n, "values", e))
     assert not bad, bad[:10]
+
+
+def modal_case(fx: dict, modal: str) -> dict:
+    """the arrays of one variant of tests/golden/modal_variants.npz (keys '<modal>:<name>')"""
+    pre = modal + ":"
+    return {k[len(pre):]: v for k, v in fx.items() if k.startswith(pre)}

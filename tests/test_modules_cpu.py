@@ -79,3 +79,19 @@ def test_half_conversion_refused():
     m = PriGumbelModel(1.0, contract="W")
     with pytest.raises(RuntimeError):
         m.half()
+
+
+@pytest.mark.parametrize("modal,cls", [("ti", "TICA_LapDropout"), ("it", "ITCA_LapDropout"), ("ii", "IICA_LapDropout"),
+                                       ("tt", "TTCA_LapDropout"), ("tisc", "TISC_LapDropout")])
+def test_modal_variant_state_dict_keys(modal, cls):
+    """custom_models/models.py variants: the parameter names / shapes are the reference modules' (read
+    from the reference-generated fixture's gradient records, tests/golden/modal_variants.npz)."""
+    import custom_models.models as M
+    from goldens import load, modal_case
+    _, fx = load("modal_variants")
+    ref = {k.split(":", 1)[1] for k in modal_case(fx, modal) if k.startswith(("gsum:", "gnone:"))}
+    m = getattr(M, cls)() if modal == "ii" else getattr(M, cls)("no-such-dir")
+    assert set(m.state_dict()) == ref, set(m.state_dict()) ^ ref
+    from oracle import fusion_oracle as O
+    shapes = O.param_shapes("T", "prigumbel", modal=modal)
+    assert {k: tuple(v.shape) for k, v in m.state_dict().items()} == shapes

@@ -186,3 +186,21 @@ def test_prigumbel_v1(ci):
     assert rel_err(logits.detach(), f["logits"]) < 2e-5
     assert abs(loss.item() - float(f["loss"])) < 1e-5
     check_grads(_grads(p), f, 1e-4)
+
+
+@pytest.mark.parametrize("modal", ["ti", "it", "ii", "tt", "tisc"])
+def test_modal_variants(modal):
+    """custom_models/models.py TICA/ITCA/IICA/TTCA/TISC_LapDropout (reference-generated fixture):
+    the oracle's encoders_modal + PriGumbel gate + head, injected Laplace / Gumbel draws."""
+    from goldens import modal_case
+    cfg, fx_all = load("modal_variants")
+    fx = modal_case(fx_all, modal)
+    p = det_params("T", "prigumbel", modal=modal)
+    batch = {k: torch.from_numpy(fx[k]) for k in ("title_input", "text_mask", "title_input2", "text_mask2",
+                                                  "frame_input", "frame_input2") if k in fx}
+    logits = O.forward_modal(p, batch, modal, torch.from_numpy(fx["noise"]), torch.from_numpy(fx["gumbels"]),
+                             cfg["eps"], cfg["hard"][modal])
+    loss = torch.nn.functional.cross_entropy(logits, torch.from_numpy(fx["labels"]))
+    loss.backward()
+    assert rel_err(logits.detach(), fx["logits"]) < 2e-5
+    check_grads(_grads(p), fx, 1e-4)

@@ -64,7 +64,7 @@ def test_attn_varlen_matches_padded(dt, p):
              out_d.data_ptr(), H * DH, lse_d.data_ptr(), None, _s())
     out_v = torch.full((R, H * DH), float("nan"), device="cuda").to(dt)
     lse_v = torch.empty(B, H, L, device="cuda")
-    lib.call("eegf_attn_varlen_fwd", code, B, H, L, cu.data_ptr(), T, R, qkv_pk.data_ptr(), 3 * H * DH, 0.125, p, 11, 5,
+    lib.call("eegf_attn_varlen_fwd", code, B, H, L, cu.data_ptr(), T, R, qkv_pk.data_ptr(), 3 * H * DH, None, 0.125, p, 11, 5,
              out_v.data_ptr(), H * DH, lse_v.data_ptr(), _s())
     dout_pad = torch.randn(B, L, H * DH, device="cuda").to(dt)
     dout_pk = torch.zeros(R, H * DH, device="cuda", dtype=dt)
@@ -77,7 +77,7 @@ def test_attn_varlen_matches_padded(dt, p):
              out_d.data_ptr(), dout_pad.data_ptr(), H * DH, lse_d.data_ptr(), None, dq_d.data_ptr(), ws_d.data_ptr(), _s())
     dq_v = torch.full((R, 3 * H * DH), float("nan"), device="cuda").to(dt)
     ws_v = torch.empty(max(lib.lib().eegf_attn_varlen_bwd_workspace(R, L), 1), device="cuda")
-    lib.call("eegf_attn_varlen_bwd", code, B, H, L, cu.data_ptr(), T, R, qkv_pk.data_ptr(), 3 * H * DH, 0.125, p, 11, 5,
+    lib.call("eegf_attn_varlen_bwd", code, B, H, L, cu.data_ptr(), T, R, qkv_pk.data_ptr(), 3 * H * DH, None, 0.125, p, 11, 5,
              out_v.data_ptr(), dout_pk.data_ptr(), H * DH, lse_v.data_ptr(), dq_v.data_ptr(), ws_v.data_ptr(), _s())
     torch.cuda.synchronize()
     tol = 2e-5 if dt == torch.float32 else 1e-2
