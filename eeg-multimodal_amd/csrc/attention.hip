@@ -433,11 +433,11 @@ int l256_grid(int items) {
 }  // namespace
 
 // Which directions take the L = 256 kernels: bit 0 forward, bit 1 backward (eegf_tune key 2,
-// initial value from EEGF_ATTN256 = 0 / fwd / bwd / all).  Default forward only: the persistent
-// backward (attn_bwd256_kernel) measures slower than attn_bwd_kernel with dropout on.
+// initial value from EEGF_ATTN256 = 0 / fwd / bwd / all).  Default both: B=256, p=0.1 the persistent
+// backward takes 399 us against 473 for attn_bwd_kernel (profiles/r2g_attn_ab.log).
 int g_attn256_mode = [] {
   const char* e = getenv("EEGF_ATTN256");
-  if (!e) return 1;
+  if (!e) return 3;
   if (e[0] == '0') return 0;
   if (e[0] == 'b') return 2;
   if (e[0] == 'a') return 3;

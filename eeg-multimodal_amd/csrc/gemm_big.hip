@@ -109,16 +109,17 @@ DEV bf16x8 rd_col_rm(const bf16* t, int r0, int c0, int lane) {
   return r;
 }
 
-template <bool LOAD, int NTH = NT>
+template <bool LOAD, int NTH = NT, int TNT = TN>
 DEV void tile_io(bf16* lds, bf16* gp, long ld, int m0, int n0, int M, int N, int tid) {
+  constexpr int LDCT = TNT + 8, CPR = TNT / 8;      // epilogue tile row stride, 16-B chunks per row
 #pragma unroll 4
-  for (int k = 0; k < (TM * TN / 8) / NTH; ++k) {
+  for (int k = 0; k < (TM * TNT / 8) / NTH; ++k) {
     const int c = tid + NTH * k;
-    const int r = c >> 5, cc = (c & 31) * 8;
+    const int r = c / CPR, cc = (c % CPR) * 8;
     const int m = m0 + r, n = n0 + cc;
     if (m >= M || n >= N) continue;
     bf16* g = gp + (long)m * ld + n;
-    bf16* l = lds + r * LDC + cc;
+    bf16* l = lds + r * LDCT + cc;
     if (n + 8 <= N) {
       if (LOAD) st16(l, ld16(g)); else st16(g, ld16(l));
     } else {
@@ -133,10 +134,11 @@ DEV void st4(bf16* p, const float (&v)[4]) { bf16x4 x; x[0] = (bf16)v[0]; x[1] =
 // Shared epilogue of the 256x256 kernels: acc[i][j] holds rows wm*128 + 16i + (lane&15), columns
 // wn*16NJ + 16j + 4*(lane>>4) + 0..3 of the block tile (m0, n0) (NJ = 4: 8 waves of 128x64, NJ = 8:
 // 4 waves of 128x128); NTH threads.
-template <int EPI, typename TO, int NJ = 4, int NTH = NT>
+template <int EPI, typename TO, int NJ = 4, int NTH = NT, int TNT = TN>
 DEV void big_epilogue(const BigArgs& g, f32x4 (&acc)[8][NJ], bf16* lds, int m0, int n0, int tid, int lane, int wm,
                       int wn) {
   constexpr int WN = 16 * NJ;
+  constexpr int LDC = TNT + 8;
   constexpr bool HAS_BIAS = EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_TANH ||
                             EPI == EPI_BIAS_GELU_D;
   constexpr bool AUX_IN = EPI == EPI_DGELU || EPI == EPI_DRELU || EPI == EPI_DTANH || EPI == EPI_MUL_AUX;
@@ -169,7 +171,7 @@ DEV void big_epilogue(const BigArgs& g, f32x4 (&acc)[8][NJ], bf16* lds, int m0, 
   bf16* ct = lds;
   bf16* Cb = (bf16*)g.C;
   if (AUX_IN || g.beta != 0.f) {
-    tile_io<true, NTH>(ct, AUX_IN ? g.aux : Cb, AUX_IN ? g.ldaux : g.ldc, m0, n0, g.M, g.N, tid);
+    tile_io<true, NTH, TNT>(ct, AUX_IN ? g.aux : Cb, AUX_IN ? g.ldaux : g.ldc, m0, n0, g.M, g.N, tid);
     __syncthreads();
   }
 #pragma unroll
@@ -221,7 +223,7 @@ DEV void big_epilogue(const BigArgs& g, f32x4 (&acc)[8][NJ], bf16* lds, int m0, 
     // store the pre-activation tile, then compute GELU while those stores drain (raw barriers: a
     // __syncthreads() here would wait for the stores); LDS reads of the tile are complete per
     // thread once its stores have issued
-    tile_io<false, NTH>(ct, g.aux, g.ldaux, m0, n0, g.M, g.N, tid);
+    tile_io<false, NTH, TNT>(ct, g.aux, g.ldaux, m0, n0, g.M, g.N, tid);
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
 #pragma unroll
@@ -245,7 +247,7 @@ DEV void big_epilogue(const BigArgs& g, f32x4 (&acc)[8][NJ], bf16* lds, int m0, 
       }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
-  tile_io<false, NTH>(ct, Cb, g.ldc, m0, n0, g.M, g.N, tid);
+  tile_io<false, NTH, TNT>(ct, Cb, g.ldc, m0, n0, g.M, g.N, tid);
   }
 }
 
@@ -1204,6 +1206,169 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
   big_epilogue<EPI, TO, 8, NT4>(g, acc, lds, m0, n0, tid, lane, wm, wn);
 }
 
+// ---------------------------------------------------------------------------------------------
+// 4-wave 256x128 kernel for the K = 768 bf16-output GEMMs with heavy epilogues (QKV and FFN1
+// forward with bias / GELU / GELU', the out-projection, the input gradients with an activation
+// product): the same K-loop as gemm4w (asm LDS-DMA in the saddr form, next K-tile's fragments read
+// inside the current one's MFMA shadows, accumulators pinned to AGPRs, one counted vmcnt + one
+// barrier per K-tile) on a half-width tile: 2 x 2 waves of 128x64 (128 accumulator AGPRs, <= 256
+// registers per lane) and a 3-deep ring of BK = 32 K-tiles (3 x 24 KB), so TWO workgroups share a
+// CU and one's epilogue (bias / GELU VALU, LDS-staged stores) runs under the other's MFMAs — the
+// one-workgroup-per-CU kernels leave the MFMA idle for the whole epilogue.
+// A K-contiguous; B K-contiguous (forward) or k-major (input gradient).
+constexpr int TNH = 128, SLOTH = (TM + TNH) * BK4, NSLOTH = 3;
+constexpr int LDSH = NSLOTH * SLOTH > TM * (TNH + 8) ? NSLOTH * SLOTH : TM * (TNH + 8);
+static_assert(LDSH * 2 <= 80 * 1024, "two workgroups per CU");
+DEV void vm_wait_h(int n) {      // n younger K-tiles (6 LDS-DMAs each) may stay in flight
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+  }
+}
+
+template <bool BKC, int EPI>
+__global__ void __launch_bounds__(NT4, 2) gemm4h_kernel(BigArgs g) {
+  __shared__ __attribute__((aligned(16))) bf16 lds[LDSH];   // ring NSLOTH x 24 KB | epilogue tile
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int tiles_n = (g.N + TNH - 1) / TNH, tiles_m = (g.M + TM - 1) / TM;
+  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int tm = t / tiles_n, tn = t % tiles_n;
+  const int m0 = tm * TM, n0 = tn * TNH;
+  const int nk = g.K / BK4;
+
+  // staging per K-tile: 4 A parts (16 rows x 64 B each) + 2 B parts per wave; B k-major: [32 k][128 cols]
+  // images, 4 k-rows x 256 B per wave-instruction, 16-B column chunk (lane & 15) ^ swz_k(k)
+  auto voffA = [&](int j) -> uint32_t {
+    const int r = (wave * 4 + j) * 16 + (lane >> 2);
+    const int c = (lane & 3) ^ sw4(r);
+    return (uint32_t)(((long)(min(m0 + r, g.M - 1) - m0) * g.lda + c * 8) * 2);
+  };
+  auto voffB = [&](int j) -> uint32_t {
+    if (BKC) {
+      const int r = (wave * 2 + j) * 16 + (lane >> 2);
+      const int c = (lane & 3) ^ sw4(r);
+      return (uint32_t)(((long)(min(n0 + r, g.N - 1) - n0) * g.ldb + c * 8) * 2);
+    }
+    const int k = (wave * 2 + j) * 4 + (lane >> 4);
+    const int c = (lane & 15) ^ swz_k(k);
+    return (uint32_t)(((long)k * g.ldb + min(n0 + c * 8, g.N - 8) - n0) * 2);
+  };
+  uint32_t vA[4], vB[2];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) vA[j] = voffA(j);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) vB[j] = voffB(j);
+  const bf16* baseA = g.A + (long)m0 * g.lda;
+  const bf16* baseB = BKC ? g.B + (long)n0 * g.ldb : g.B + n0;
+  const long stepB = BKC ? BK4 : (long)BK4 * g.ldb;
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr_of(lds));
+  auto stage_part = [&](int kt, int slot, int j) {      // part j (0-3 A, 4-5 B) of K-tile kt -> slot
+    if (j < 4) {
+      glds16_asm_sa(baseA + kt * BK4, vA[j], lds0 + 2u * (slot * SLOTH + (wave * 4 + j) * 16 * BK4));
+    } else {
+      const int jb = j - 4;
+      glds16_asm_sa(baseB + kt * stepB, vB[jb],
+                    lds0 + 2u * (slot * SLOTH + TM * BK4 + (BKC ? (wave * 2 + jb) * 16 * BK4 : (wave * 2 + jb) * 4 * TNH)));
+    }
+  };
+  const int fr = lane & 15, fq = lane >> 4;
+  const int offA = (wm * 128 + fr) * BK4 + ((fq ^ sw4(fr)) << 3);
+  const int offB = TM * BK4 + (wn * 64 + fr) * BK4 + ((fq ^ sw4(fr)) << 3);
+  int tB0[4], tB1[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (!BKC) {
+      const int q = fr >> 2, p4 = fr & 3;
+      const int col = wn * 64 + 16 * i + 4 * p4, ch = col >> 3, off = col & 7;
+      const int ka = 8 * fq + q, kb = ka + 4;
+      tB0[i] = TM * BK4 + ka * TNH + (((ch ^ swz_k(ka)) << 3) | off);
+      tB1[i] = TM * BK4 + kb * TNH + (((ch ^ swz_k(kb)) << 3) | off);
+    }
+  }
+  auto rdA = [&](const bf16* img, int i) { return *(const bf16x8*)(img + offA + i * 16 * BK4); };
+  auto rdB = [&](const bf16* img, int i) {
+    return BKC ? *(const bf16x8*)(img + offB + i * 16 * BK4) : rd_col_off(img, tB0[i], tB1[i]);
+  };
+
+  f32x4 acc[8][4];
+  for (int kt = 0; kt < NSLOTH; ++kt)
+    if (kt < nk)
+      for (int j = 0; j < 6; ++j) stage_part(kt, kt, j);
+  vm_wait_h(max(0, min(nk, NSLOTH) - 2));
+  raw_barrier();
+  bf16x8 fa[2][8], fb[2][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) fa[0][i] = rdA(lds, i);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) fb[0][i] = rdB(lds, i);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  raw_barrier();
+
+  auto ktile = [&](auto Hc, int k, int slot, int nslot, auto Ic, auto Tc) __attribute__((always_inline)) {
+    constexpr int H = decltype(Hc)::value;
+    constexpr bool INIT = decltype(Ic)::value, TAIL = decltype(Tc)::value;
+    const bool more = !TAIL || k + 1 < nk, st = !TAIL || k + NSLOTH < nk;
+    const bf16* nimg = lds + nslot * SLOTH;
+    auto mma = [&](int s, int jj) {
+      if (INIT) mma16_acc0(acc[s][jj], fb[H][jj], fa[H][s]);
+      else mma16_acc(acc[s][jj], fb[H][jj], fa[H][s]);
+    };
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      mma(s, 0);
+      if (more) fa[H ^ 1][s] = rdA(nimg, s);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(s, 1);
+      if (more && s < 4) fb[H ^ 1][s] = rdB(nimg, s);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(s, 2);
+      if (st && s < 6) stage_part(k + NSLOTH, slot, s);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(s, 3);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // K-tile k + 2 retired (its fragments are read in the next K-tile); younger: k + 3
+    if (!TAIL) vm_wait_h(NSLOTH - 2);
+    else vm_wait_h(max(0, min(nk - 1, k + NSLOTH) - (k + 2)));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads of k + 1 done: its slot may be restaged
+    raw_barrier();
+  };
+  using C0 = std::integral_constant<int, 0>;
+  using C1 = std::integral_constant<int, 1>;
+  using F = std::false_type;
+  using T = std::true_type;
+  auto nxt = [](int sl) { return sl == NSLOTH - 1 ? 0 : sl + 1; };
+  int slot = 0;
+  if (nk > NSLOTH) ktile(C0{}, 0, slot, nxt(slot), T{}, F{});
+  else ktile(C0{}, 0, slot, nxt(slot), T{}, T{});
+  slot = nxt(slot);
+  int kt = 1;
+  for (; kt + 1 + NSLOTH < nk; kt += 2) {
+    ktile(C1{}, kt, slot, nxt(slot), F{}, F{});
+    slot = nxt(slot);
+    ktile(C0{}, kt + 1, slot, nxt(slot), F{}, F{});
+    slot = nxt(slot);
+  }
+  for (; kt < nk; kt += 2) {
+    ktile(C1{}, kt, slot, nxt(slot), F{}, T{});
+    slot = nxt(slot);
+    if (kt + 1 < nk) {
+      ktile(C0{}, kt + 1, slot, nxt(slot), F{}, T{});
+      slot = nxt(slot);
+    }
+  }
+  // the asm MFMAs are opaque to the hazard recognizer: cover the result latency before the first
+  // accumulator read
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  big_epilogue<EPI, bf16, 4, NT4, TNH>(g, acc, lds, m0, n0, tid, lane, wm, wn);
+}
+
+int g_gemm4h = [] { const char* e = getenv("EEGF_GEMM4H"); return e ? atoi(e) : 2; }();   // eegf_tune key 8
+
 template <bool AKC, bool BKC, int EPI, typename TO>
 int launch_big(const BigArgs& a, int splits, hipStream_t s) {
   const int tiles = ((a.M + TM - 1) / TM) * ((a.N + TN - 1) / TN);
@@ -1229,6 +1394,15 @@ int launch_big(const BigArgs& a, int splits, hipStream_t s) {
       }
     }
     if constexpr (AKC && sizeof(TO) == 2) {
+      // 256x128 two-workgroups-per-CU kernel (eegf_tune key 8: 0 off, 1 every short-K GEMM, 2 (default)
+      // N <= 768 only: the attention out-projection forward / input gradient, 940 -> 969 and
+      // 808 -> 947 TFLOP/s; wider N stays on the 8-phase kernel, profiles/r2h_gemm_ab.log)
+      const bool h_ok = g_gemm4h == 1 || (g_gemm4h == 2 && a.N <= 768);
+      if (h_ok && splits == 1 && !a.colsum_part && a.K < 2048 && a.K % BK4 == 0 && a.N >= 128) {
+        const int tiles_h = ((a.M + TM - 1) / TM) * ((a.N + TNH - 1) / TNH);
+        hipLaunchKernelGGL((gemm4h_kernel<BKC, EPI>), dim3(tiles_h), dim3(NT4), 0, s, a);
+        return (int)hipGetLastError();
+      }
       const bool usep = g_gemm8p > 0;
       if (usep && splits == 1 && a.K >= 2 * BK) {
         const dim3 grid(tiles < big_cus() ? tiles : big_cus());
@@ -1417,6 +1591,7 @@ extern "C" int eegf_tune(int key, int value) {
   if (key == 3) { const int o = g_big_prio; g_big_prio = value; return o; }
   if (key == 4) { const int o = g_gemm8p; g_gemm8p = value; return o; }
   if (key == 5) { const int o = g_gemm4w_cs; g_gemm4w_cs = value; return o; }
+  if (key == 8) { const int o = g_gemm4h; g_gemm4h = value; return o; }
   if (key == 7) { const int o = g_ln_bwd_rpb; if (value < 4 || value > 1024 || value % 4) return EEGF_ERR_ARG; g_ln_bwd_rpb = value; return o; }
   if (key == 6) { const int o = g_ln_rpw; if (value < 1 || value > 64) return EEGF_ERR_ARG; g_ln_rpw = value; return o; }
   return EEGF_ERR_ARG;

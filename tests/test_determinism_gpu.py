@@ -1,0 +1,55 @@
+"""Bitwise run-to-run reproducibility of the production bf16 training step (every reduction
+has a fixed order, no float atomics on the contract-W path).
+
+B = 16 PriGumbel hard (every large-shape route: persistent L = 256 attention, 256x256 / 256x128 GEMMs,
+split-K weight gradients, deferred column sums), the same inputs five times with the caching
+allocator's layout shifted between runs: logits and all parameter gradients must be identical bit for
+bit.  This is the check that caught the persistent backward's missing LDS-DMA wait before its barrier
+(a wave read the next chunk's rows before another wave's staging landed: ~1e-6 gradient noise in most
+runs, garbage LayerNorm-weight gradients in a few).
+"""
+import pytest
+import torch
+
+from goldens import det_params, w_values_dp
+
+pytestmark = pytest.mark.gpu
+
+
+def _inputs(B=16):
+    from oracle import fusion_oracle as O
+    g = torch.Generator().manual_seed(1601)
+    eeg = torch.randn(B, 64, 256, generator=g)
+    act = torch.randn(B, 32, generator=g) * 0.5
+    labels = (torch.rand(B, generator=g) < 0.66).long()
+    noise = O.laplace_from_uniform(torch.rand(B, 2304, generator=g) * 2 - 1)
+    gumbels = -torch.log(-torch.log(torch.rand(2, B, 2304, generator=g).clamp(1e-6, 1 - 1e-6)))
+    return [t.cuda() for t in (eeg, act, labels, noise, gumbels)]
+
+
+def _step(eeg, act, labels, noise, gumbels, dropout):
+    from eegfusion.modules import PriGumbelModel
+    torch.manual_seed(0)
+    m = PriGumbelModel(1.0, contract="W", dropout=dropout)
+    m.load_state_dict(det_params("W", "prigumbel", w_values_dp(), requires_grad=False), strict=False)
+    m = m.cuda().train().set_compute_dtype(torch.bfloat16)
+    m.engine.injected = dict(noise=noise, gumbels=gumbels.contiguous())
+    logits = m.forward_window(eeg, act, True)
+    torch.nn.functional.cross_entropy(logits, labels).backward()
+    torch.cuda.synchronize()
+    out = {n: t.grad.detach().clone() for n, t in m.named_parameters() if t.grad is not None}
+    out["logits"] = logits.detach().clone()
+    return out
+
+
+@pytest.mark.parametrize("dropout", [0.0, 0.1])
+def test_training_step_bitwise_reproducible(dropout):
+    args = _inputs()
+    base = _step(*args, dropout)
+    assert len(base) > 150
+    pad = []
+    for it in range(4):
+        pad.append(torch.empty(1 + 777777 * (it + 1), device="cuda"))     # shift the allocator layout
+        cur = _step(*args, dropout)
+        bad = [n for n in base if not torch.equal(cur[n], base[n])]
+        assert not bad, (it, len(bad), bad[:8])

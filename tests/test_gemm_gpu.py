@@ -491,3 +491,57 @@ def test_gemm_wgrad_bias_ineligible():
                                          dw.data_ptr(), 768, 1.0, db.data_ptr(), ws.data_ptr(), ws.numel() * 4,
                                          torch.cuda.current_stream().cuda_stream)
     assert st == _lib.ERR_ARG
+
+
+@pytest.mark.parametrize("epi", ["none", "bias", "bias_gelu", "bias_gelu_d", "gelu_noaux", "bias_relu", "bias_tanh",
+                                 "none_beta"])
+@pytest.mark.parametrize("M,N,K", [(4352, 808, 768), (2048, 2304, 96), (8192, 3072, 32), (65536, 3072, 768)])
+def test_gemm_4h_fwd(epi, M, N, K):
+    """The 256x128 two-workgroups-per-CU kernel (eegf_tune key 8) on the forward layout: N / M edge
+    tiles, K = one K-tile, the bench's FFN1 shape with every epilogue."""
+    k = _k()
+    old = _tune(8, 1)
+    try:
+        torch.manual_seed(31)
+        x = (torch.randn(M, K, device="cuda") * 0.3).to(torch.bfloat16)
+        w = (torch.randn(N, K, device="cuda") * 0.3).to(torch.bfloat16)
+        b = torch.randn(N, device="cuda")
+        if epi in ("none", "none_beta"):
+            c = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+            beta = 1.0 if epi == "none_beta" else 0.0
+            ref = beta * c.double() + 0.5 * (x.double() @ w.double().t())
+            k.gemm(x, w, c, M=M, N=N, K=K, a_kc=1, b_kc=1, lda=K, ldb=K, ldc=N, alpha=0.5, beta=beta)
+            torch.cuda.synchronize()
+            _check(c, ref, torch.bfloat16)
+            return
+        e = "bias_gelu" if epi == "gelu_noaux" else epi
+        aux = torch.empty(M, N, device="cuda", dtype=torch.bfloat16) if epi in ("bias_gelu", "bias_gelu_d") else None
+        out = k.linear(x, w, b, epi=e, aux=aux)
+        torch.cuda.synchronize()
+        ref, pre = _ref_epi(x.double() @ w.double().t(), e, b, None, 1.0)
+        _check(out, ref, torch.bfloat16)
+        if aux is not None:
+            _check(aux, pre, torch.bfloat16)
+    finally:
+        _tune(8, old)
+
+
+@pytest.mark.parametrize("epi", ["none", "mul_aux", "dgelu", "drelu", "dtanh"])
+@pytest.mark.parametrize("M,N,K", [(4352, 808, 768), (2048, 3072, 96), (65536, 3072, 768), (65536, 768, 768)])
+def test_gemm_4h_dgrad(epi, M, N, K):
+    """256x128 kernel with a k-major B (input gradient, transpose-read fragments of a 128-column image)."""
+    k = _k()
+    old = _tune(8, 1)
+    try:
+        torch.manual_seed(32)
+        dy = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+        w = (torch.randn(K, N, device="cuda") * 0.1).to(torch.bfloat16)
+        aux = torch.randn(M, N, device="cuda").to(torch.bfloat16) if epi != "none" else None
+        if epi == "dtanh":
+            aux = torch.tanh(aux.float()).to(torch.bfloat16)
+        out = k.linear_dgrad(dy, w, epi=epi, aux=aux, epi_scale=1.25)
+        torch.cuda.synchronize()
+        ref, _ = _ref_epi(dy.double() @ w.double(), epi, None, aux, 1.25)
+        _check(out, ref, torch.bfloat16)
+    finally:
+        _tune(8, old)

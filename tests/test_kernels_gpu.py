@@ -423,7 +423,7 @@ def test_window_tokens(dt):
 def test_attention_l256_persistent(pdrop, mode):
     """L = 256 bf16 path with more (b, h) items than workgroups: every persistent workgroup runs
     several items (next-item K/V/Q prefetch, chunk stream across items).  mode (eegf_tune key 2):
-    1 = persistent forward (default), 3 = persistent forward and backward."""
+    1 = persistent forward, 3 = persistent forward and backward (default)."""
     lib = _lib()
     lib.lib().eegf_tune.argtypes = [lib.i32, lib.i32]
     old = lib.lib().eegf_tune(2, mode)

@@ -17,6 +17,8 @@ SHAPES = [
     ("ao_fwd", R, 768, 768, "fwd", "bias"),
     ("ffn1_fwd", R, 3072, 768, "fwd", "bias_gelu"),
     ("ffn1_fwd_nogelu", R, 3072, 768, "fwd", "bias"),
+    ("ffn1_fwd_gelu_d", R, 3072, 768, "fwd", "bias_gelu_d"),
+    ("ffn2_dgrad_mulaux", R, 3072, 768, "dgrad", "mul_aux"),
     ("ffn2_fwd", R, 768, 3072, "fwd", "bias"),
     ("ffn2_dgrad_dgelu", R, 3072, 768, "dgrad", "dgelu"),
     ("ffn2_dgrad_plain", R, 3072, 768, "dgrad", "none"),
@@ -41,7 +43,7 @@ def run(name, M, N, Kd, layout, epi, iters=20):
         B = torch.randn(N, Kd, device=dev, dtype=dt) * 0.05
         C = torch.empty(M, N, device=dev, dtype=dt)
         bias = torch.randn(N, device=dev)
-        aux = torch.empty(M, N, device=dev, dtype=dt) if epi == "bias_gelu" else None
+        aux = torch.empty(M, N, device=dev, dtype=dt) if epi in ("bias_gelu", "bias_gelu_d") else None
         f = lambda: K.gemm(A, B, C, M=M, N=N, K=Kd, a_kc=1, b_kc=1, lda=Kd, ldb=Kd, ldc=N, epi=epi, bias=bias,
                            aux=aux, ldaux=N)
         bb = bias.to(dt)
@@ -83,16 +85,19 @@ def run(name, M, N, Kd, layout, epi, iters=20):
         for _ in range(5):
             for v in VARIANTS:
                 # 5: 2-phase with static priority; 6: persistent 8-phase; -1: default routing
-                # 0-4: key 1 = v; 5: 2-phase + static prio; 6: persistent; 7: 8-phase MODE 5; 8: 4-wave
-                lib.eegf_tune(1, {5: 0, 6: -1, 7: 5, 8: 6}.get(v, v))
+                # 0-4: key 1 = v; 5: 2-phase + static prio; 6: persistent; 7: 8-phase MODE 5; 8: 4-wave;
+                # 9: default routing with the 256x128 two-workgroup kernel (key 8)
+                lib.eegf_tune(1, {5: 0, 6: -1, 7: 5, 8: 6, 9: -1}.get(v, v))
                 lib.eegf_tune(3, 1 if v == 5 else 0)
                 lib.eegf_tune(4, 1 if v == 6 else 0)
+                lib.eegf_tune(8, 1 if v == 9 else 0)
                 f()
                 torch.cuda.synchronize()
                 r[v].append(timed(f, iters))
         lib.eegf_tune(1, -1)
         lib.eegf_tune(3, 0)
         lib.eegf_tune(4, 0)
+        lib.eegf_tune(8, 0)
         med = {v: sorted(x)[len(x) // 2] for v, x in r.items()}
         tt = timed(tf, iters)
         print(f"{name:16s} {M}x{N}x{Kd} " + " | ".join(f"v{v} {tf_(med[v]):6.1f}" for v in med)
