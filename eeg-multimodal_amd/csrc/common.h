@@ -56,7 +56,12 @@ DEV void glds16_asm_s(const void* base, uint32_t voff, const void* lds_base) {
 // saddr form with a 32-bit LDS byte address (no generic->LDS pointer cast per call) and a base the
 // caller knows to be wave-uniform
 DEV void glds16_asm_sa(const void* base, uint32_t voff, uint32_t lds_addr) {
-  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(base), "s"(lds_addr)
+  // readfirstlane: a no-op on a base the compiler already keeps in SGPRs, and it keeps the "s"
+  // constraint satisfiable when control flow elsewhere in the kernel makes it place the base in VGPRs
+  const uint64_t b = (uint64_t)(uintptr_t)base;
+  const uint64_t bu = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+                      (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(bu), "s"(lds_addr)
                : "memory", "m0");
 }
 DEV uint32_t lds_addr_of(const void* p) {

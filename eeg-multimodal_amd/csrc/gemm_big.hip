@@ -36,10 +36,24 @@ struct BigArgs {
   float alpha, beta, epi_scale;
   int ksplit;            // >0: split-K slice length; C = fp32 slabs [blockIdx.y][M][N]
   float* colsum_part;    // AKC only: [tiles_m][K] partial column sums of A (nullable)
-  int prio;              // 1: waves 4-7 run at s_setprio 1 for the whole kernel (eegf_tune key 3)
   float* rowsum_part;    // gemm4w RS only: [splits][M] sums over this split's K of each row of a k-major A
+  long long* ts;         // diagnostics (eegf_gemm_big_timestamps): per-workgroup phase times, null = off
 };
-int g_big_prio = [] { const char* e = getenv("EEGF_GEMM_PRIO"); return e ? atoi(e) : 0; }();
+// Phase timestamps (100 MHz s_memrealtime) of one workgroup: 0 start, 1 prologue done, 2 K-loop done,
+// 3 epilogue issued; slot 4 = the CU it ran on (8 int64 per workgroup) -- tools/gemm_phases.py turns them into per-phase times and dispatch gaps
+DEV void ts_mark(const BigArgs& g, int k) {
+  if (g.ts && threadIdx.x == 0) {
+    long long* p = g.ts + ((long)blockIdx.y * gridDim.x + blockIdx.x) * 8;
+    p[k] = (long long)__builtin_amdgcn_s_memrealtime();
+    if (k == 0) {                    // which CU: XCC id << 16 | HW_ID bits 8-15 (CU, SH, SE)
+      uint32_t hw, xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      p[4] = (long long)(((xcc & 15u) << 16) | ((hw >> 8) & 255u));
+    }
+  }
+}
+long long* g_ts_buf = nullptr;
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) const void glb_void;
@@ -263,7 +277,6 @@ __global__ void __launch_bounds__(NT, 1) gemm_big_kernel(BigArgs g) {
   const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
   const int tm = t / tiles_n, tn = t % tiles_n;
   const int m0 = tm * TM, n0 = tn * TN;
-  if (g.prio && wave >= 4) __builtin_amdgcn_s_setprio(1);   // static priority for the younger half
 
   f32x4 acc[8][4];
 #pragma unroll
@@ -431,18 +444,16 @@ DEV void raw_barrier() {
 
 // Layouts: AKC/BKC as gemm_big_kernel (row-major half images read with ds_read_b128, k-major ones
 // with ds_read_b64_tr_b16); fp32 output = split-K slabs over blockIdx.y as gemm_big_kernel.
-// MODE 1: staggered groups, per-phase vmcnt; 2: lockstep, per-phase vmcnt; 3: as 1 without setprio;
-// 4: lockstep with one vmcnt per K-tile (phase 3: every half staged up to phase 1 of this tile retired,
-//    the two younger ones stay in flight across the barrier); 5: as 4 plus a barrier after each
-//    phase's MFMAs (the guide template's two barriers per phase).
+// Schedule: the 8 waves run the 4 phases of a K-tile in lockstep (one barrier per phase, MFMAs at
+// s_setprio 1) with one counted vmcnt per K-tile (phase 3: every half staged up to phase 1 of this
+// tile retired, the two younger ones stay in flight across the barrier).  The staggered-group and
+// per-phase-vmcnt variants measured 2-25 % slower (profiles/r1s2_gemm_ab.log) and were removed.
 // CS: fused column sums of A (as gemm_big_kernel's): in workgroups of tile column 0, waves 0-3 contract
 // 32 local rows of A_h0 at phase 0 and waves 4-7 32 rows of A_h1 at phase 2 against a ones operand
 // (4 extra MFMAs per K-tile); the 8 partials go through red[2][8][64] in LDS and wave 0 folds the
 // previous K-tile's into ks[K] at phase 1.
-template <bool AKC, bool BKC, int EPI, typename TO, int MODE, bool CS = false>
+template <bool AKC, bool BKC, int EPI, typename TO, bool CS = false>
 __global__ void __launch_bounds__(NT, 1) gemm8_kernel(BigArgs g) {
-  constexpr bool STAG = MODE == 1 || MODE == 3, PRIO = MODE != 3, TILEWAIT = MODE == 4 || MODE == 5;
-  constexpr bool POSTBAR = STAG || MODE == 5;       // second barrier per phase, after the MFMAs
   // CS: operand ring 128 KB | red[2][8][64] 4 KB | ks[K] fp32 12 KB  (the epilogue reuses the front)
   __shared__ __attribute__((aligned(16))) bf16 lds[CS ? (8 * HALF + 1024 * 2 + CS_KMAX * 2) : LDS_ELEMS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -490,22 +501,15 @@ __global__ void __launch_bounds__(NT, 1) gemm8_kernel(BigArgs g) {
     else if (p == 2) stageA(tt, 0);
     else stageB(tt, 0);
   };
-  auto younger = [&](int phi) {       // real stages among phases phi-3 .. phi
-    int n = 0;
-#pragma unroll
-    for (int x = 0; x < 4; ++x) n += stage_tile_of(phi - x) < nk ? 1 : 0;
-    return n;
-  };
-
   // prologue = the stages of phases -6 .. -1
   auto younger2 = [&](int phi) {      // real stages among phases phi-1, phi
     return (stage_tile_of(phi - 1) < nk ? 1 : 0) + (stage_tile_of(phi) < nk ? 1 : 0);
   };
+  ts_mark(g, 0);
   for (int phi = -6; phi < 0; ++phi) stage_phase(phi);
-  if (TILEWAIT) vm_wait(younger2(-1));  // retires phases -6 .. -3 (every half of tile 0)
-  else vm_wait(younger(-1));          // retires phases -6, -5 (A_h0(0), B_h0(0))
+  vm_wait(younger2(-1));              // retires phases -6 .. -3 (every half of tile 0)
   raw_barrier();
-  if (STAG && wm == 1) raw_barrier();  // stagger group 1 by one barrier
+  ts_mark(g, 1);
 
   const bool do_cs = CS && AKC && tn == 0;
   float* red = (float*)(lds + 8 * HALF);
@@ -564,12 +568,11 @@ __global__ void __launch_bounds__(NT, 1) gemm8_kernel(BigArgs g) {
       }
       // (b) stage one half-tile, (c) retire the one staged 4 phases ago
       stage_phase(phi);
-      if (!TILEWAIT) vm_wait(younger(phi));
-      else if (p == 3) vm_wait(younger2(phi));
+      if (p == 3) vm_wait(younger2(phi));
       raw_barrier();
       // (e) the quadrant's 16 MFMAs
       const int mh = (p == 0 || p == 1) ? 0 : 1, nh = (p == 1 || p == 2) ? 1 : 0;
-      if (PRIO) __builtin_amdgcn_s_setprio(1);
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
@@ -579,13 +582,12 @@ __global__ void __launch_bounds__(NT, 1) gemm8_kernel(BigArgs g) {
             const bf16x8 bv = nh == 0 ? br0[jj][kc] : br1[jj][kc];
             acc[mh * 4 + ii][nh * 2 + jj] = mma16(bv, ar[ii][kc], acc[mh * 4 + ii][nh * 2 + jj]);
           }
-      if (PRIO) __builtin_amdgcn_s_setprio(0);
-      if (POSTBAR) raw_barrier();
+      __builtin_amdgcn_s_setprio(0);
     }
   }
-  if (STAG && wm == 0) raw_barrier();  // re-align the groups
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  ts_mark(g, 2);
   if (CS) {
     if (do_cs && tid < 64) {
       const float* rp = red + ((nk - 1) & 1) * 512;
@@ -601,277 +603,7 @@ __global__ void __launch_bounds__(NT, 1) gemm8_kernel(BigArgs g) {
   }
   // acc[i][j]: i = 4*mh + ii -> rows wm*128 + 64*mh + 16*ii = wm*128 + 16*i (same map as gemm_big)
   big_epilogue<EPI, TO>(g, acc, lds, m0, n0, tid, lane, wm, wn);
-}
-
-// ---------------------------------------------------------------------------------------------
-// Persistent form of the lockstep 8-phase schedule (MODE 4), bf16 output, K-contiguous A.
-// grid = min(tiles, CUs); workgroup b runs the tiles v = b, b + grid, ... (each mapped through
-// xcd_remap exactly as the one-shot grid would place block v), and the K-tile STREAM runs on across
-// tiles: stream index G = it * nk + kt, buffer G & 1, and the stages of a tile's last phases already
-// fetch the next tile's K-tiles 0 / 1.  The epilogue stores straight from the accumulators (8-byte
-// row segments, no LDS: the ring holds the next tile's operands), so it overlaps those loads instead
-// of following a prologue bubble.  CS: the fused A column sums of gemm8_kernel, per tile.
-// Measured (tools/gemm_bench.py --ab, profiles/r1s2_gemm_persist_ab.log): 5-10 % SLOWER than the one-
-// shot gemm8 MODE 4 on every bench shape except the aux-input epilogues (+10 %), so opt-in only.
-// 4-wave kernel with fused column sums (eegf_tune key 5): work in progress, the sums of K-tile 1 miss
-// half the rows (tools/dbg_acs.py) -- off by default, dgrad+colsum stays on gemm8_kernel CS
-int g_gemm4w_cs = 0;
-int g_gemm8p = [] { const char* e = getenv("EEGF_GEMM8P"); return e ? atoi(e) : 0; }();
-
-int big_cus() {
-  static const int cus = [] {
-    int dev = 0, n = 256;
-    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-    return n > 0 ? n : 256;
-  }();
-  return cus;
-}
-
-DEV bf16x4 pack4(const float (&v)[4]) {
-  bf16x4 x;
-  x[0] = (bf16)v[0]; x[1] = (bf16)v[1]; x[2] = (bf16)v[2]; x[3] = (bf16)v[3];
-  return x;
-}
-
-// acc[i][j][r] -> row wm*128 + 16i + (lane&15), column wn*64 + 16j + 4(lane>>4) + r of the tile.
-// The compiler's waitcnt pass treats vmcnt as out of order once stores and loads are both pending
-// (gfx9 counts stores in vmcnt), so any wait it computes after an epilogue is vmcnt(0), which would
-// drain the next tile's operand stages.  Hence: the tile's bias row arrives in LDS by LDS-DMA at the
-// START of the tile (retired by the tile's own counted waits, published by its phase barriers), the
-// aux / C inputs are all loaded before the first store, and interior tiles (EDGE = false) have no
-// data-dependent branches around their loads and stores.
-template <int EPI>
-constexpr bool epi_has_bias() {
-  return EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_TANH || EPI == EPI_BIAS_GELU_D;
-}
-
-template <int EPI, bool EDGE>
-DEV void direct_epilogue_body(const BigArgs& g, f32x4 (&acc)[8][4], const float* bias_lds, int m0, int n0, int lane,
-                              int wm, int wn) {
-  constexpr bool HAS_BIAS = epi_has_bias<EPI>();
-  constexpr bool AUX_IN = EPI == EPI_DGELU || EPI == EPI_DRELU || EPI == EPI_DTANH || EPI == EPI_MUL_AUX;
-  bf16* Cb = (bf16*)g.C;
-  const int rl = m0 + wm * 128 + (lane & 15);
-  const int cl = n0 + wn * 64 + 4 * (lane >> 4);
-  const bool load_in = AUX_IN || (EPI == EPI_NONE && g.beta != 0.f);
-  const bf16* src = AUX_IN ? g.aux : Cb;
-  const long lds_ = AUX_IN ? g.ldaux : g.ldc;
-  bf16x4 av[8][4];
-  if (load_in) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        int m = rl + 16 * i, n = cl + 16 * j;
-        if (EDGE) { m = min(m, g.M - 1); n = min(n, g.N - 4); }
-        av[i][j] = *(const bf16x4*)(src + (long)m * lds_ + n);
-      }
-  }
-  f32x4 bias[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-    bias[j] = HAS_BIAS ? *(const f32x4*)(bias_lds + wn * 64 + 16 * j + 4 * (lane >> 4)) : f32x4{0.f, 0.f, 0.f, 0.f};
-  {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int m = rl + 16 * i;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = cl + 16 * j;
-        float o[4], o2[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float v = g.alpha * acc[i][j][r];
-          const float a = load_in ? (float)av[i][j][r] : 0.f;
-          if (HAS_BIAS) v += bias[j][r];
-          if (EPI == EPI_BIAS_RELU) v = relu_nan(v);
-          else if (EPI == EPI_BIAS_TANH) v = tanhf(v);
-          else if (EPI == EPI_DGELU) v *= gelu_grad(a);
-          else if (EPI == EPI_DRELU) v = a > 0.f ? v * g.epi_scale : 0.f;
-          else if (EPI == EPI_DTANH) v *= (1.f - a * a);
-          else if (EPI == EPI_MUL_AUX) v *= a;
-          else if (EPI == EPI_NONE && g.beta != 0.f) v += g.beta * a;
-          o[r] = v;
-        }
-        if (EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_D) {
-#pragma unroll
-          for (int h2 = 0; h2 < 2; ++h2) {
-            f32x2 gl, gd;
-            gelu2(f32x2{o[2 * h2], o[2 * h2 + 1]}, gl, EPI == EPI_BIAS_GELU_D ? &gd : nullptr);
-            o2[2 * h2] = EPI == EPI_BIAS_GELU_D ? gd.x : o[2 * h2];      // aux: gelu' or the pre-activation
-            o2[2 * h2 + 1] = EPI == EPI_BIAS_GELU_D ? gd.y : o[2 * h2 + 1];
-            o[2 * h2] = gl.x;
-            o[2 * h2 + 1] = gl.y;
-          }
-        }
-        if (!EDGE || (m < g.M && n < g.N)) {
-          *(bf16x4*)(Cb + (long)m * g.ldc + n) = pack4(o);
-          if (EPI == EPI_BIAS_GELU_D || (EPI == EPI_BIAS_GELU && g.aux))
-            *(bf16x4*)(g.aux + (long)m * g.ldaux + n) = pack4(o2);
-        }
-      }
-    }
-  }
-  // edge tiles: the math may sink into the exec-masked store blocks, leaving the aux loads of
-  // skipped blocks pending in the waitcnt pass's model (it then drains at the next K-loop head);
-  // retire them here, once per edge tile (the builtin, unlike an asm wait, is seen by the pass)
-  if (EDGE && load_in) __builtin_amdgcn_s_waitcnt(0x0F70);     // vmcnt(0)
-}
-
-template <int EPI>
-DEV void direct_epilogue(const BigArgs& g, f32x4 (&acc)[8][4], const float* bias_lds, int m0, int n0, int lane, int wm,
-                         int wn) {
-  if (m0 + TM <= g.M && n0 + TN <= g.N) direct_epilogue_body<EPI, false>(g, acc, bias_lds, m0, n0, lane, wm, wn);
-  else direct_epilogue_body<EPI, true>(g, acc, bias_lds, m0, n0, lane, wm, wn);
-}
-
-template <bool BKC, int EPI, bool CS = false>
-__global__ void __launch_bounds__(NT, 1) gemm8p_kernel(BigArgs g) {
-  // operand ring 128 KB | bias rows [2][256] fp32 2 KB (+ CS: red[2][8][64] 4 KB | ks[K] fp32 12 KB)
-  __shared__ __attribute__((aligned(16))) bf16 lds[8 * HALF + 1024 + (CS ? 1024 * 2 + CS_KMAX * 2 : 0)];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 2, wn = wave & 3;
-  const int tiles_n = (g.N + TN - 1) / TN, tiles = ((g.M + TM - 1) / TM) * tiles_n;
-  const int my = (tiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
-  const int nk = g.K / BK;                 // >= 2
-  const int total = my * nk;               // K-tile stream of this workgroup
-
-  auto tile_of = [&](int it, int& tm, int& tn) {
-    const int t = xcd_remap((int)blockIdx.x + it * (int)gridDim.x, tiles);
-    tm = t / tiles_n;
-    tn = t - tm * tiles_n;
-  };
-  int tmc, tnc, tmn, tnn;
-  tile_of(0, tmc, tnc);
-  if (my > 1) tile_of(1, tmn, tnn); else { tmn = tmc; tnn = tnc; }
-  int kend = nk;                           // stream end of the current tile
-
-  // stage half `which` (0 A_h0, 1 A_h1, 2 B_h0, 3 B_h1) of stream K-tile s (current or next tile)
-  auto stage_s = [&](int s, int which) {
-    const bool nx = s >= kend;
-    const int k0 = (s - (nx ? kend : kend - nk)) * BK;
-    bf16* d = lds + (s & 1) * 4 * HALF + which * HALF;
-    if (which < 2) stage_half(d, g.A, g.lda, (nx ? tmn : tmc) * TM, 6, 128, 64 * which, g.M, k0, wave, lane);
-    else if (BKC) stage_half(d, g.B, g.ldb, (nx ? tnn : tnc) * TN, 5, 64, 32 * (which - 2), g.N, k0, wave, lane);
-    else stage_half_km(d, g.B, g.ldb, (nx ? tnn : tnc) * TN, 5, 64, 32 * (which - 2), g.N, k0, wave, lane);
-  };
-  auto stage_tile_of = [&](int phi) { const int tt = phi >> 2, p = phi & 3; return tt + (p <= 1 ? 1 : 2); };
-  auto stage_phase = [&](int phi) {
-    const int tt = stage_tile_of(phi), p = phi & 3;
-    if (tt >= total) return;
-    stage_s(tt, p == 0 ? 3 : p == 1 ? 1 : p == 2 ? 0 : 2);
-  };
-  auto younger2 = [&](int phi) {
-    return (stage_tile_of(phi - 1) < total ? 1 : 0) + (stage_tile_of(phi) < total ? 1 : 0);
-  };
-  for (int phi = -6; phi < 0; ++phi) stage_phase(phi);
-  vm_wait(younger2(-1));
-  raw_barrier();
-
-  float* bias_rows = (float*)(lds + 8 * HALF);
-  float* red = bias_rows + 512;
-  float* ks = red + 2 * 8 * 64;
-  const int cs_h = wave >> 2, cs_lr0 = 32 * (wave & 3);
-  auto rdB = [&](const bf16* Bh, int jj, int kc) {
-    return BKC ? rd_row(Bh, wn * 32 + jj * 16 + (lane & 15), 4 * kc + (lane >> 4))
-               : rd_colh(Bh, 32 * kc + 8 * (lane >> 4), wn * 32 + jj * 16, lane);
-  };
-  bf16x8 ar[4][2], br0[2][2], br1[2][2];
-  f32x4 acc[8][4];
-  for (int it = 0; it < my; ++it) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // the tile's bias row -> bias_rows[it & 1] by one LDS-DMA of wave 0: older than every stage of
-    // this tile, so the first phase-3 vm_wait retires it and that phase's barrier publishes it
-    if (epi_has_bias<EPI>() && wave == 0)
-      glds16((const bf16*)(g.bias + min(tnc * TN + 4 * lane, g.N - 4)), (bf16*)(bias_rows + (it & 1) * 256));
-    const bool do_cs = CS && tnc == 0;
-    bf16x8 ones;
-    if (CS) {
-      const int cs_rows = g.M - tmc * TM - ((cs_lr0 >> 6) * 128 + 64 * cs_h + (cs_lr0 & 63) + 8 * (lane >> 4));
-#pragma unroll
-      for (int e = 0; e < 8; ++e) ones[e] = (bf16)(e < cs_rows ? 1.0f : 0.0f);
-    }
-    for (int kt = 0; kt < nk; ++kt) {
-      const int G = it * nk + kt;
-      const bf16* Ab = lds + (G & 1) * 4 * HALF;
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        const int phi = 4 * G + p;
-        if (CS && do_cs) {
-          if (p == 2 * cs_h) {
-            const bf16* Ah = Ab + cs_h * HALF;
-#pragma unroll
-            for (int f = 0; f < 4; ++f) {
-              const f32x4 c = mma16(ones, rd_col_rm(Ah, cs_lr0 + 8 * (lane >> 4), 16 * f, lane), f32x4{0.f, 0.f, 0.f, 0.f});
-              if (lane < 16) red[(kt & 1) * 512 + wave * 64 + 16 * f + lane] = c[0];
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          }
-          if (p == 1 && kt > 0 && tid < 64) {
-            const float* rp = red + ((kt - 1) & 1) * 512;
-            float v = 0.f;
-#pragma unroll
-            for (int w = 0; w < 8; ++w) v += rp[w * 64 + tid];
-            ks[(kt - 1) * BK + tid] = v;
-          }
-        }
-        if (p == 0) {
-#pragma unroll
-          for (int jj = 0; jj < 2; ++jj)
-#pragma unroll
-            for (int kc = 0; kc < 2; ++kc) br0[jj][kc] = rdB(Ab + 2 * HALF, jj, kc);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        if (p == 1) {
-#pragma unroll
-          for (int jj = 0; jj < 2; ++jj)
-#pragma unroll
-            for (int kc = 0; kc < 2; ++kc) br1[jj][kc] = rdB(Ab + 3 * HALF, jj, kc);
-        }
-        if (p == 0 || p == 2) {
-          const bf16* Ah = Ab + (p == 0 ? 0 : HALF);
-#pragma unroll
-          for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-            for (int kc = 0; kc < 2; ++kc) ar[ii][kc] = rd_row(Ah, wm * 64 + ii * 16 + (lane & 15), 4 * kc + (lane >> 4));
-        }
-        stage_phase(phi);
-        if (p == 3) vm_wait(younger2(phi));
-        raw_barrier();
-        const int mh = (p == 0 || p == 1) ? 0 : 1, nh = (p == 1 || p == 2) ? 1 : 0;
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-          for (int jj = 0; jj < 2; ++jj)
-#pragma unroll
-            for (int kc = 0; kc < 2; ++kc) {
-              const bf16x8 bv = nh == 0 ? br0[jj][kc] : br1[jj][kc];
-              acc[mh * 4 + ii][nh * 2 + jj] = mma16(bv, ar[ii][kc], acc[mh * 4 + ii][nh * 2 + jj]);
-            }
-        __builtin_amdgcn_s_setprio(0);
-      }
-    }
-    if (CS && do_cs) {
-      if (tid < 64) {
-        const float* rp = red + ((nk - 1) & 1) * 512;
-        float v = 0.f;
-#pragma unroll
-        for (int w = 0; w < 8; ++w) v += rp[w * 64 + tid];
-        ks[(nk - 1) * BK + tid] = v;
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      for (int k = tid; k < g.K; k += NT) g.colsum_part[(long)tmc * g.K + k] = ks[k];
-    }
-    direct_epilogue<EPI>(g, acc, bias_rows + (it & 1) * 256, tmc * TM, tnc * TN, lane, wm, wn);
-    tmc = tmn;
-    tnc = tnn;
-    kend += nk;
-    if (it + 2 < my) tile_of(it + 2, tmn, tnn);
-  }
+  ts_mark(g, 3);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -918,21 +650,15 @@ DEV bf16x8 rd_col_off(const bf16* t, int o0, int o1) {
 // AKC / BKC: operand K-contiguous (row-major [rows][K] image, ds_read_b128 fragments) or k-major
 // ([K][cols] in memory: [32 k][256 cols] image with the swz_k chunk swizzle of stage_kmajor,
 // ds_read_b64_tr_b16 fragments: input-gradient B, weight-gradient A and B)
-// CS (AKC only): fused column sums of A over the tile's rows for tile column 0 (the bias gradient of
-// an input-gradient GEMM): wave w sums rows 64w .. 64w + 63 of the staged K-tile with 4 MFMAs
-// against a ones operand (A^T fragments by transpose reads), parks its 32 partials in
-// red[k & 1][w]; wave 0 folds the previous K-tile's 4 partials (fixed order) into ks[K] after the
-// K-tile barrier.  The ring is 4 deep then (128 KB + red 1 KB + ks 12 KB).
 // RS (weight gradients, A = dY k-major): the same kernel also sums every A row over K (the bias
 // gradient dY.sum(0) of the nn.Linear whose weight gradient this is): in workgroups of tile column 0,
 // wave (wm, wn) sums its row blocks s = 4 wn .. 4 wn + 3 from the A fragments it already holds,
 // partials -> rowsum_part[split][M].
-template <bool AKC, bool BKC, int EPI, typename TO, bool CS = false, bool RS = false>
+template <bool AKC, bool BKC, int EPI, typename TO, bool RS = false>
 __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
-  constexpr int NSLOT4 = CS ? 4 : ::NSLOT4;
-  constexpr int LDS4 = CS ? (NSLOT4 * SLOT4 + 512 + CS_KMAX * 2) : NSLOT4 * SLOT4;
+  constexpr int LDS4 = NSLOT4 * SLOT4;
   static_assert(LDS4 * 2 <= 160 * 1024 && LDS4 >= TM * LDC, "LDS budget / epilogue tile");
-  __shared__ __attribute__((aligned(16))) bf16 lds[LDS4];   // ring NSLOT4 x 32 KB | epilogue tile (| red | ks)
+  __shared__ __attribute__((aligned(16))) bf16 lds[LDS4];   // ring NSLOT4 x 32 KB | epilogue tile
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
@@ -1007,61 +733,6 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
   auto rdB = [&](const bf16* img, int i) {
     return BKC ? *(const bf16x8*)(img + offB + i * 16 * BK4) : rd_col_off(img, tB0[i], tB1[i]);
   };
-  float* red = (float*)(lds + NSLOT4 * SLOT4);            // [2][4 waves][32]
-  float* ks = red + 256;                                   // [K]
-  const bool do_cs = CS && tn == 0;
-  // column sums on the MFMA: D = ones[16 x 32 rows] x A^T-chunk[32 rows x 16 k] (every D row = the
-  // 16 column sums), A^T read from the row-major image with ds_read_b64_tr_b16.  Wave w: rows
-  // 64w + 32rc + .. (rc = 0, 1), k-blocks cb = 0, 1 -> 4 MFMAs + 4 fragment reads per K-tile.
-  bf16x8 cs_ones[2];
-  int cs_o0[2][2], cs_o1[2][2];
-#pragma unroll
-  for (int rc = 0; rc < 2; ++rc) {
-    const int rb = 64 * wave + 32 * rc + 8 * fq;           // first row of the lane's 8-row group
-#pragma unroll
-    for (int e = 0; e < 8; ++e) cs_ones[rc][e] = (bf16)(m0 + rb + e < g.M ? 1.0f : 0.0f);
-#pragma unroll
-    for (int cb = 0; cb < 2; ++cb) {
-      const int q = fr >> 2, p4 = fr & 3, col = 16 * cb + 4 * p4, ch = col >> 3, off = col & 7;
-      const int ra = rb + q, rbb = rb + 4 + q;
-      cs_o0[rc][cb] = ra * BK4 + (((ch ^ sw4(ra)) << 3) | off);
-      cs_o1[rc][cb] = rbb * BK4 + (((ch ^ sw4(rbb)) << 3) | off);
-    }
-  }
-  f32x4 csd[2];
-  bf16x8 cst[2];
-  // chunk c = 0..3 of a K-tile image: (rc, cb) = (c & 1, c >> 1).  In the loop the read of chunk c
-  // sits in group c and its MFMA in group c + 1, after N younger LDS ops of that wave (group c + 1's
-  // fragment reads: 1 ds_read_b128 + 2 transpose reads, and chunk c + 1's 2 reads when c < 3; wave 0's
-  // fold only adds younger ops): lgkmcnt(N) retires exactly the chunk's read.
-  auto cs_read = [&](const bf16* img, int c) {
-    cst[c & 1] = rd_col_off(img, cs_o0[c & 1][c >> 1], cs_o1[c & 1][c >> 1]);
-  };
-  // csd is zeroed (VALU) at the start of the K-tile, a group (>= 8 MFMAs) before the chunk MFMAs
-  // read it: the asm MFMAs are invisible to the hazard recognizer, and an "=v" output tied to a
-  // "+v" input of the next chunk let the compiler place a copy right behind the MFMA (read before
-  // the result was written: the rc = 1 rows went missing)
-  auto cs_zero = [&]() {
-    csd[0] = f32x4{0.f, 0.f, 0.f, 0.f};
-    csd[1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  };
-  auto cs_mfma = [&](int c, int) {       // compiler-visible MFMA: the hazard recognizer covers it
-    csd[c >> 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cs_ones[c & 1], cst[c & 1], csd[c >> 1], 0, 0, 0);
-  };
-  auto cs_store = [&](int k) {      // lanes 0..15 hold the 16 sums of each k-block (D row 0)
-    if (lane < 16) {
-      float* r = red + (k & 1) * 128 + wave * 32;
-      r[lane] = csd[0][0];
-      r[16 + lane] = csd[1][0];
-    }
-  };
-  auto cs_fold = [&](int k) {                              // wave 0: ks[k*32 + l] = sum of the 4 partials
-    if (wave == 0 && lane < 32) {
-      const float* r = red + (k & 1) * 128 + lane;
-      ks[k * BK4 + lane] = ((r[0] + r[32]) + r[64]) + r[96];
-    }
-  };
-
   f32x4 acc[8][8];           // defined by the first K-tile's MFMAs (mma16_acc0)
   // RS: per-lane fp32 partial row sums (row 16 s + (lane & 15), k-block lane >> 4) of the wave's 4 row
   // blocks, summed on the VALU from the A fragments already in registers (16 VALU per fragment, in the
@@ -1072,6 +743,7 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
   float rsv[4] = {0.f, 0.f, 0.f, 0.f};
 
   // prologue: K-tiles 0 .. NSLOT4-1 staged; 0 and 1 retired
+  ts_mark(g, 0);
   for (int kt = 0; kt < NSLOT4; ++kt)
     if (kt < nk)
       for (int j = 0; j < 8; ++j) stage_part(baseA + kt * stepA, baseB + kt * stepB, kt, j);
@@ -1083,22 +755,10 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
     fa[0][i] = rdA(lds, i);
     fb[0][i] = rdB(lds, i);
   }
-  if (CS && do_cs) {      // K-tiles 0 and 1's column sums (retired above); the loop does k + 1's, k >= 1
-#pragma unroll
-    for (int t2 = 0; t2 < 2; ++t2) {
-      if (t2 == 1 && nk < 2) break;
-      cs_zero();
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        cs_read(lds + t2 * SLOT4, c);
-        cs_mfma(c, 0);
-      }
-      cs_store(t2);
-    }
-  }
   // K-tile 0's slot is restaged in the first K-tile: every wave's reads of it must be done
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   raw_barrier();
+  ts_mark(g, 1);
 
   // one K-tile k (ring slot `slot`): fragments fa/fb[H] (read in the previous K-tile), the next
   // K-tile's (slot nslot) into [H ^ 1]; TAIL: near the end of K (fewer tiles left to read / stage)
@@ -1125,18 +785,11 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
       mma(s, 2);
       if (st) stage_part(sA, sB, slot, s);
       __builtin_amdgcn_sched_barrier(0);
-      // CS: sums of the NEXT K-tile from its image (tile k's own slot is being restaged now); fold
-      // of tile k's partials (stored in the previous K-tile / the prologue, published by its barrier)
       mma(s, 3);
-      if (CS && !INIT && do_cs && more && s == 0) cs_zero();
-      if (CS && !INIT && do_cs && more && s < 4) cs_read(nimg, s);
       __builtin_amdgcn_sched_barrier(0);
       mma(s, 4);
-      if (CS && !INIT && do_cs && more && s >= 1 && s <= 4) cs_mfma(s - 1, s == 4 ? 3 : 5);
       __builtin_amdgcn_sched_barrier(0);
       mma(s, 5);
-      if (CS && s == 1 && do_cs) cs_fold(k);
-      if (CS && !INIT && s == 7 && do_cs && more) cs_store(k + 1);
       __builtin_amdgcn_sched_barrier(0);
       mma(s, 6);
       mma(s, 7);
@@ -1188,10 +841,6 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
   // the asm MFMAs are opaque to the hazard recognizer: cover the result latency before the first
   // accumulator read
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_waitcnt vmcnt(0)" ::: "memory");
-  if (CS && do_cs) {                     // every K-tile folded in the loop (fold(k) in K-tile k)
-    __syncthreads();
-    for (int k = tid; k < g.K; k += NT4) g.colsum_part[(long)tm * g.K + k] = ks[k];
-  }
   if (RS && do_rs) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {      // fold the 4 k-blocks (lane groups 16 apart), fixed order
@@ -1203,7 +852,9 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
     }
   }
   __syncthreads();
+  ts_mark(g, 2);
   big_epilogue<EPI, TO, 8, NT4>(g, acc, lds, m0, n0, tid, lane, wm, wn);
+  ts_mark(g, 3);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1232,6 +883,7 @@ __global__ void __launch_bounds__(NT4, 2) gemm4h_kernel(BigArgs g) {
   __shared__ __attribute__((aligned(16))) bf16 lds[LDSH];   // ring NSLOTH x 24 KB | epilogue tile
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  ts_mark(g, 0);
   const int wm = wave >> 1, wn = wave & 1;
   const int tiles_n = (g.N + TNH - 1) / TNH, tiles_m = (g.M + TM - 1) / TM;
   const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
@@ -1306,6 +958,7 @@ __global__ void __launch_bounds__(NT4, 2) gemm4h_kernel(BigArgs g) {
   for (int i = 0; i < 4; ++i) fb[0][i] = rdB(lds, i);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   raw_barrier();
+  ts_mark(g, 1);
 
   auto ktile = [&](auto Hc, int k, int slot, int nslot, auto Ic, auto Tc) __attribute__((always_inline)) {
     constexpr int H = decltype(Hc)::value;
@@ -1364,7 +1017,9 @@ __global__ void __launch_bounds__(NT4, 2) gemm4h_kernel(BigArgs g) {
   // accumulator read
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  ts_mark(g, 2);
   big_epilogue<EPI, bf16, 4, NT4, TNH>(g, acc, lds, m0, n0, tid, lane, wm, wn);
+  ts_mark(g, 3);
 }
 
 int g_gemm4h = [] { const char* e = getenv("EEGF_GEMM4H"); return e ? atoi(e) : 2; }();   // eegf_tune key 8
@@ -1380,14 +1035,6 @@ int launch_big(const BigArgs& a, int splits, hipStream_t s) {
     // the 4-wave kernel (profiles/r1s2_gemm4w_ab.log, r1s2_gemm4w_kmajor_ab.log): +7-8 % on the
     // weight gradients and on K >= 2048 (K-loop-bound; at K = 768 its unoverlapped epilogue loses)
     if (sizeof(TO) == 4 ? (!AKC && !BKC) : a.K >= 2048) {
-      if (g_gemm4w_cs > 0) {            // fused column sums on the 4-wave kernel: opt-in, NOT parity-green
-        if constexpr (AKC && !BKC && sizeof(TO) == 2) {
-          if (a.colsum_part) {
-            hipLaunchKernelGGL((gemm4w_kernel<AKC, BKC, EPI, TO, true>), dim3(tiles, splits), dim3(NT4), 0, s, a);
-            return (int)hipGetLastError();
-          }
-        }
-      }
       if (!a.colsum_part) {
         hipLaunchKernelGGL((gemm4w_kernel<AKC, BKC, EPI, TO>), dim3(tiles, splits), dim3(NT4), 0, s, a);
         return (int)hipGetLastError();
@@ -1403,41 +1050,23 @@ int launch_big(const BigArgs& a, int splits, hipStream_t s) {
         hipLaunchKernelGGL((gemm4h_kernel<BKC, EPI>), dim3(tiles_h), dim3(NT4), 0, s, a);
         return (int)hipGetLastError();
       }
-      const bool usep = g_gemm8p > 0;
-      if (usep && splits == 1 && a.K >= 2 * BK) {
-        const dim3 grid(tiles < big_cus() ? tiles : big_cus());
-        if constexpr (!BKC) {
-          if (a.colsum_part) {
-            hipLaunchKernelGGL((gemm8p_kernel<BKC, EPI, true>), grid, dim3(NT), 0, s, a);
-            return (int)hipGetLastError();
-          }
-        }
-        if (!a.colsum_part) {
-          hipLaunchKernelGGL((gemm8p_kernel<BKC, EPI>), grid, dim3(NT), 0, s, a);
-          return (int)hipGetLastError();
-        }
-      }
     }
     if (use8) {
       if constexpr (AKC && !BKC && sizeof(TO) == 2) {
         if (a.colsum_part) {
-          hipLaunchKernelGGL((gemm8_kernel<AKC, BKC, EPI, TO, 4, true>), dim3(tiles, splits), dim3(NT), 0, s, a);
+          hipLaunchKernelGGL((gemm8_kernel<AKC, BKC, EPI, TO, true>), dim3(tiles, splits), dim3(NT), 0, s, a);
           return (int)hipGetLastError();
         }
       }
       if (!a.colsum_part) {
-        hipLaunchKernelGGL((gemm8_kernel<AKC, BKC, EPI, TO, 4>), dim3(tiles, splits), dim3(NT), 0, s, a);
+        hipLaunchKernelGGL((gemm8_kernel<AKC, BKC, EPI, TO>), dim3(tiles, splits), dim3(NT), 0, s, a);
         return (int)hipGetLastError();
       }
     }
-  } else if (g_gemm8 && !a.colsum_part) {
+  } else if ((g_gemm8 == 4 || g_gemm8 == 6) && !a.colsum_part) {
     const dim3 grid(tiles, splits);
-    if (g_gemm8 == 2) hipLaunchKernelGGL((gemm8_kernel<AKC, BKC, EPI, TO, 2>), grid, dim3(NT), 0, s, a);
-    else if (g_gemm8 == 4) hipLaunchKernelGGL((gemm8_kernel<AKC, BKC, EPI, TO, 4>), grid, dim3(NT), 0, s, a);
-    else if (g_gemm8 == 5) hipLaunchKernelGGL((gemm8_kernel<AKC, BKC, EPI, TO, 5>), grid, dim3(NT), 0, s, a);
-    else if (g_gemm8 == 6) hipLaunchKernelGGL((gemm4w_kernel<AKC, BKC, EPI, TO>), grid, dim3(NT4), 0, s, a);
-    else if (g_gemm8 == 3) hipLaunchKernelGGL((gemm8_kernel<AKC, BKC, EPI, TO, 3>), grid, dim3(NT), 0, s, a);
-    else hipLaunchKernelGGL((gemm8_kernel<AKC, BKC, EPI, TO, 1>), grid, dim3(NT), 0, s, a);
+    if (g_gemm8 == 4) hipLaunchKernelGGL((gemm8_kernel<AKC, BKC, EPI, TO>), grid, dim3(NT), 0, s, a);
+    else hipLaunchKernelGGL((gemm4w_kernel<AKC, BKC, EPI, TO>), grid, dim3(NT4), 0, s, a);
     return (int)hipGetLastError();
   }
   if constexpr (AKC && !BKC && sizeof(TO) == 2) {
@@ -1506,9 +1135,9 @@ int eegf_gemm_big_wgrad_bias(int M, int N, int K, const void* A, long lda, const
   float* slabs = (float*)workspace;
   float* part = slabs + (splits > 1 ? (long)splits * M * N : 0);
   BigArgs a{(const bf16*)A, (const bf16*)B, splits > 1 ? (void*)slabs : (void*)C, nullptr, nullptr, lda, ldb, ldc, 0,
-            M, N, K, 1.0f, beta, 1.0f, splits > 1 ? ks : 0, nullptr, 0, part};
+            M, N, K, 1.0f, beta, 1.0f, splits > 1 ? ks : 0, nullptr, part, g_ts_buf};
   const int tiles = ((M + TM - 1) / TM) * ((N + TN - 1) / TN);
-  hipLaunchKernelGGL((gemm4w_kernel<false, false, EPI_NONE, float, false, true>), dim3(tiles, splits), dim3(NT4), 0,
+  hipLaunchKernelGGL((gemm4w_kernel<false, false, EPI_NONE, float, true>), dim3(tiles, splits), dim3(NT4), 0,
                      stream, a);
   if (splits > 1) {
     const long MN = (long)M * N;
@@ -1531,7 +1160,7 @@ int eegf_gemm_big(int a_kc, int b_kc, int epi, int out_f32, int M, int N, int K,
   if (lda % 8 || ldb % 8 || ldc % 8 || (aux && ldaux % 8)) return 1;
   if ((((uintptr_t)A | (uintptr_t)B | (uintptr_t)C | (uintptr_t)aux) & 15) != 0) return 1;
   BigArgs a{(const bf16*)A, (const bf16*)B, C, bias, (bf16*)aux, lda, ldb, ldc, ldaux, M, N, K, alpha, beta,
-            epi_scale, 0, a_colsum, g_big_prio};
+            epi_scale, 0, a_colsum, nullptr, g_ts_buf};
   if (a_colsum && (!a_kc || out_f32)) return 1;
   if (out_f32) {
     if (a_kc || b_kc || epi != EPI_NONE || M < 256 || N < 256 || K < 4096 || ldc % 4) return 1;
@@ -1580,17 +1209,25 @@ int eegf_gemm_big_colsum_tiles(int M, int N, int K) {
 
 extern int g_attn256_mode;     // attention.hip
 
-// Tuning / A-B hook (returns the old value): key 1 = 8-phase GEMM schedule (-1 auto (default), 0 off,
-// 1 staggered, 2 lockstep, 3 staggered without setprio, 4 lockstep with one vmcnt per K-tile); key 2 = L = 256
-// attention kernels (bit 0 forward, bit 1 backward); key 3 = static s_setprio 1 for waves 4-7 of the
-// 2-phase 256x256 kernel; key 4 = persistent 8-phase kernel (0 off (default), 1 every eligible
-// bf16-output GEMM).
+// Tuning / A-B hook (returns the old value; test and benchmark state, include/eegfusion.h lists the
+// keys): 1 = 256x256 GEMM kernel (-1 automatic routing (default), 0 2-phase, 4 8-phase, 6 4-wave);
+// 2 = L = 256 attention kernels (bit 0 forward, bit 1 backward); 6 / 7 = LayerNorm rows; 8 = the
+// 256x128 two-workgroups-per-CU GEMM.
+// Diagnostics: every following big-GEMM launch writes 4 phase timestamps + the CU id per workgroup
+// into buf (int64 [grid.y][grid.x][8], s_memrealtime 100 MHz ticks) until called again with nullptr.
+extern "C" int eegf_gemm_big_timestamps(long long* buf) {
+  g_ts_buf = buf;
+  return 0;
+}
+
 extern "C" int eegf_tune(int key, int value) {
-  if (key == 1) { const int o = g_gemm8; g_gemm8 = value; return o; }
+  if (key == 1) {
+    if (value != -1 && value != 0 && value != 4 && value != 6) return EEGF_ERR_ARG;
+    const int o = g_gemm8;
+    g_gemm8 = value;
+    return o;
+  }
   if (key == 2) { const int o = g_attn256_mode; g_attn256_mode = value; return o; }
-  if (key == 3) { const int o = g_big_prio; g_big_prio = value; return o; }
-  if (key == 4) { const int o = g_gemm8p; g_gemm8p = value; return o; }
-  if (key == 5) { const int o = g_gemm4w_cs; g_gemm4w_cs = value; return o; }
   if (key == 8) { const int o = g_gemm4h; g_gemm4h = value; return o; }
   if (key == 7) { const int o = g_ln_bwd_rpb; if (value < 4 || value > 1024 || value % 4) return EEGF_ERR_ARG; g_ln_bwd_rpb = value; return o; }
   if (key == 6) { const int o = g_ln_rpw; if (value < 1 || value > 64) return EEGF_ERR_ARG; g_ln_rpw = value; return o; }

@@ -58,19 +58,21 @@ int eegf_gemm(int dtype, int out_dtype, int a_kcontig, int b_kcontig, int epi,
               const float* bias, long strideBias, void* aux, long ldaux, long strideAux,
               float alpha, float beta, float epi_scale, void* workspace, long ws_bytes,
               hipStream_t stream);
-/* Tuning / A-B hook (benchmarks, parity tests).  Returns the previous value, or EEGF_ERR_ARG.
- *   key 1: 256x256 GEMM schedule: -1 = automatic routing (default), 0 = 2-phase 8-wave, 1..5 =
- *          8-wave 8-phase variants (4 = the one the router uses), 6 = the 4-wave 128x128-per-wave kernel;
+/* Tuning / A-B hook (benchmarks, parity tests; not part of the reference interface).  Returns the
+ * previous value, or EEGF_ERR_ARG.
+ *   key 1: 256x256 GEMM kernel: -1 = automatic routing (default), 0 = 2-phase 8-wave, 4 = 8-phase
+ *          8-wave (the schedule the router uses for short K), 6 = the 4-wave 128x128-per-wave kernel;
  *   key 2: L = 256 attention kernels (bit 0 persistent forward, bit 1 persistent backward; default 3);
- *   key 3: static s_setprio for waves 4-7 of the 2-phase kernel;
- *   key 4: persistent 8-phase kernel (0 off, default);
- *   key 5: fused column sums on the 4-wave kernel (0 off, default; experimental, not parity-green).
  *   key 6: maximum rows per wave of eegf_ln_fwd (1..64, default 16; fewer when the grid would drop
  *          below 1024 workgroups);
  *   key 7: rows per workgroup of eegf_ln_bwd when rows >= 65536 (multiple of 4, default 64);
  *   key 8: 256x128 two-workgroups-per-CU GEMM for K < 2048 bf16 outputs: 0 off, 1 every such GEMM,
  *          2 (default) N <= 768 only. */
 int eegf_tune(int key, int value);
+/* Diagnostics (no reference counterpart): every following 256-row GEMM launch of the 8-wave / 4-wave
+ * kernels writes 4 s_memrealtime stamps per workgroup (start, prologue done, K-loop done, epilogue
+ * issued, slot 4 the CU id) into buf = int64 [grid.y][grid.x][8]; nullptr switches it off.  tools/gemm_phases.py. */
+int eegf_gemm_big_timestamps(long long* buf);
 /* Rows of the a_colsum partial buffer eegf_gemm_acs writes for this shape (ceil(M/256)), or 0 when
  * the fused column sums are unavailable (needs bf16 in/out, K-contiguous A, M >= 2048, N >= 256,
  * K % 64 == 0, 8-aligned dims). */

@@ -305,73 +305,62 @@ def _tune(key, value):
     return lib.eegf_tune(key, value)
 
 
-# (M, N, K): 768 tiles (3 per workgroup), 260 ragged tiles with a ragged N (workgroups 0-3 run 2),
-# the shortest stream (K = 128: 2 K-tiles per tile), an odd K-tile count
-PERSIST_SHAPES = [(16384, 3072, 768), (16640, 808, 320), (16384, 1024, 128), (8192, 2304, 192)]
+# (M, N, K): 768 tiles, 260 ragged tiles with a ragged N, a short K (2 K-tiles), an odd K-tile count
+ROUTE_SHAPES = [(16384, 3072, 768), (16640, 808, 320), (16384, 1024, 128), (8192, 2304, 192)]
 
 
-@pytest.mark.parametrize("persist", [0, 1])
 @pytest.mark.parametrize("epi", ["bias", "bias_gelu", "bias_gelu_d", "gelu_noaux", "none_beta"])
-@pytest.mark.parametrize("M,N,K", PERSIST_SHAPES)
-def test_gemm_big_persistent_fwd(persist, epi, M, N, K):
-    """The persistent 8-phase kernel (K-tile stream across a workgroup's tiles, direct-store
-    epilogue) against the one-shot kernels' reference, both routings."""
+@pytest.mark.parametrize("M,N,K", ROUTE_SHAPES)
+def test_gemm_big_routed_fwd(epi, M, N, K):
+    """Forward GEMMs with every bf16 epilogue through the default routing (8-phase 256x256 kernel for
+    wide N, 256x128 two-workgroup kernel for N <= 768) against a float64 reference."""
     k = _k()
-    old = _tune(4, persist)
-    try:
-        torch.manual_seed(21)
-        x = (torch.randn(M, K, device="cuda") * 0.3).to(torch.bfloat16)
-        w = (torch.randn(N, K, device="cuda") * 0.3).to(torch.bfloat16)
-        b = torch.randn(N, device="cuda")
-        if epi == "none_beta":
-            c = torch.randn(M, N, device="cuda").to(torch.bfloat16)
-            ref = c.double() + 0.5 * (x.double() @ w.double().t())
-            k.gemm(x, w, c, M=M, N=N, K=K, a_kc=1, b_kc=1, lda=K, ldb=K, ldc=N, alpha=0.5, beta=1.0)
-            torch.cuda.synchronize()
-            _check(c, ref, torch.bfloat16)
-            return
-        e = "bias_gelu" if epi == "gelu_noaux" else epi
-        aux = torch.empty(M, N, device="cuda", dtype=torch.bfloat16) if epi in ("bias_gelu", "bias_gelu_d") else None
-        out = k.linear(x, w, b, epi=e, aux=aux)
+    torch.manual_seed(21)
+    x = (torch.randn(M, K, device="cuda") * 0.3).to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda") * 0.3).to(torch.bfloat16)
+    b = torch.randn(N, device="cuda")
+    if epi == "none_beta":
+        c = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+        ref = c.double() + 0.5 * (x.double() @ w.double().t())
+        k.gemm(x, w, c, M=M, N=N, K=K, a_kc=1, b_kc=1, lda=K, ldb=K, ldc=N, alpha=0.5, beta=1.0)
         torch.cuda.synchronize()
-        ref, pre = _ref_epi(x.double() @ w.double().t(), e, b, None, 1.0)
-        _check(out, ref, torch.bfloat16)
-        if aux is not None:
-            _check(aux, pre, torch.bfloat16)
-    finally:
-        _tune(4, old)
-
-
-@pytest.mark.parametrize("persist", [0, 1])
-@pytest.mark.parametrize("epi", ["none", "mul_aux", "dgelu"])
-@pytest.mark.parametrize("M,N,K", PERSIST_SHAPES)
-def test_gemm_big_persistent_dgrad_colsum(persist, epi, M, N, K):
-    """Input-gradient GEMM with fused dY column sums on the persistent kernel (per-tile sums of the
-    workgroups' column-0 tiles) and without the sums."""
-    from eegfusion import _lib
-    old = _tune(4, persist)
-    try:
-        torch.manual_seed(22)
-        dy = torch.randn(M, K, device="cuda").to(torch.bfloat16)
-        w = (torch.randn(K, N, device="cuda") * 0.1).to(torch.bfloat16)
-        c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-        aux = torch.randn(M, N, device="cuda").to(torch.bfloat16) if epi != "none" else None
-        code = {"none": _lib.EPI_NONE, "mul_aux": _lib.EPI_MUL_AUX, "dgelu": _lib.EPI_DGELU}[epi]
-        tiles = (M + 255) // 256
-        part = torch.full((tiles, K), float("nan"), device="cuda")
-        _lib.call("eegf_gemm_acs", 1, 1, 1, 0, code, M, N, K, dy.data_ptr(), K, w.data_ptr(), N, c.data_ptr(), N,
-                  None, aux.data_ptr() if aux is not None else None, N if aux is not None else 0, 1.0, 0.0, 1.0,
-                  part.data_ptr(), torch.cuda.current_stream().cuda_stream)
-        torch.cuda.synchronize()
-        ref, _ = _ref_epi(dy.double() @ w.double(), epi, None, aux, 1.0)
         _check(c, ref, torch.bfloat16)
-        pref = torch.nn.functional.pad(dy.double(), (0, 0, 0, tiles * 256 - M)).view(tiles, 256, K).sum(1)
-        assert ((part.double() - pref).abs().max() / pref.abs().max()).item() < 1e-5
-        k_out = _k().linear_dgrad(dy, w, epi=epi, aux=aux)
-        torch.cuda.synchronize()
-        assert torch.equal(k_out, c)
-    finally:
-        _tune(4, old)
+        return
+    e = "bias_gelu" if epi == "gelu_noaux" else epi
+    aux = torch.empty(M, N, device="cuda", dtype=torch.bfloat16) if epi in ("bias_gelu", "bias_gelu_d") else None
+    out = k.linear(x, w, b, epi=e, aux=aux)
+    torch.cuda.synchronize()
+    ref, pre = _ref_epi(x.double() @ w.double().t(), e, b, None, 1.0)
+    _check(out, ref, torch.bfloat16)
+    if aux is not None:
+        _check(aux, pre, torch.bfloat16)
+
+
+@pytest.mark.parametrize("epi", ["none", "mul_aux", "dgelu"])
+@pytest.mark.parametrize("M,N,K", ROUTE_SHAPES)
+def test_gemm_big_routed_dgrad_colsum(epi, M, N, K):
+    """Input-gradient GEMM with fused dY column sums (per-tile sums of the column-0 tiles, 8-phase
+    kernel) and without the sums (default routing), same result bit for bit."""
+    from eegfusion import _lib
+    torch.manual_seed(22)
+    dy = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(K, N, device="cuda") * 0.1).to(torch.bfloat16)
+    c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    aux = torch.randn(M, N, device="cuda").to(torch.bfloat16) if epi != "none" else None
+    code = {"none": _lib.EPI_NONE, "mul_aux": _lib.EPI_MUL_AUX, "dgelu": _lib.EPI_DGELU}[epi]
+    tiles = (M + 255) // 256
+    part = torch.full((tiles, K), float("nan"), device="cuda")
+    _lib.call("eegf_gemm_acs", 1, 1, 1, 0, code, M, N, K, dy.data_ptr(), K, w.data_ptr(), N, c.data_ptr(), N,
+              None, aux.data_ptr() if aux is not None else None, N if aux is not None else 0, 1.0, 0.0, 1.0,
+              part.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    ref, _ = _ref_epi(dy.double() @ w.double(), epi, None, aux, 1.0)
+    _check(c, ref, torch.bfloat16)
+    pref = torch.nn.functional.pad(dy.double(), (0, 0, 0, tiles * 256 - M)).view(tiles, 256, K).sum(1)
+    assert ((part.double() - pref).abs().max() / pref.abs().max()).item() < 1e-5
+    k_out = _k().linear_dgrad(dy, w, epi=epi, aux=aux)
+    torch.cuda.synchronize()
+    assert torch.equal(k_out, c)
 
 
 @pytest.mark.parametrize("epi", ["none", "bias", "bias_gelu", "bias_gelu_d", "gelu_noaux", "none_beta"])

@@ -29,6 +29,7 @@ SHAPES = [
     ("ffn1_wgrad", 3072, 768, R, "wgrad", "none"),
     ("ffn2_wgrad", 768, 3072, R, "wgrad", "none"),
     ("ao_wgrad", 768, 768, R, "wgrad", "none"),
+    ("wide_fwd_k3072", R, 3072, 3072, "fwd", "none"),
     ("sq4k", 4096, 4096, 4096, "fwd", "none"),       # the guide's 8-phase template reference shape
     ("sq8k", 8192, 8192, 8192, "fwd", "none"),
 ]
@@ -84,20 +85,15 @@ def run(name, M, N, Kd, layout, epi, iters=20):
         r = {v: [] for v in VARIANTS}
         for _ in range(5):
             for v in VARIANTS:
-                # 5: 2-phase with static priority; 6: persistent 8-phase; -1: default routing
-                # 0-4: key 1 = v; 5: 2-phase + static prio; 6: persistent; 7: 8-phase MODE 5; 8: 4-wave;
-                # 9: default routing with the 256x128 two-workgroup kernel (key 8)
-                lib.eegf_tune(1, {5: 0, 6: -1, 7: 5, 8: 6, 9: -1}.get(v, v))
-                lib.eegf_tune(3, 1 if v == 5 else 0)
-                lib.eegf_tune(4, 1 if v == 6 else 0)
-                lib.eegf_tune(8, 1 if v == 9 else 0)
+                # -1: default routing; 0: 2-phase 8-wave; 4: 8-phase 8-wave; 8: 4-wave (key 1 = 6);
+                # 9: default routing with the 256x128 two-workgroup kernel for every short-K GEMM (key 8)
+                lib.eegf_tune(1, -1 if v in (-1, 9) else {8: 6}.get(v, v))
+                lib.eegf_tune(8, 1 if v == 9 else 2 if v == -1 else 0)
                 f()
                 torch.cuda.synchronize()
                 r[v].append(timed(f, iters))
         lib.eegf_tune(1, -1)
-        lib.eegf_tune(3, 0)
-        lib.eegf_tune(4, 0)
-        lib.eegf_tune(8, 0)
+        lib.eegf_tune(8, 2)
         med = {v: sorted(x)[len(x) // 2] for v, x in r.items()}
         tt = timed(tf, iters)
         print(f"{name:16s} {M}x{N}x{Kd} " + " | ".join(f"v{v} {tf_(med[v]):6.1f}" for v in med)
@@ -115,7 +111,7 @@ def run(name, M, N, Kd, layout, epi, iters=20):
 
 
 AB = "--ab" in sys.argv
-VARIANTS = [int(x) for x in next((a.split("=")[1] for a in sys.argv if a.startswith("--variants=")), "0,1,2,3,4").split(",")]
+VARIANTS = [int(x) for x in next((a.split("=")[1] for a in sys.argv if a.startswith("--variants=")), "-1,0,4,8").split(",")]
 
 
 if __name__ == "__main__":

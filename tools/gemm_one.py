@@ -26,7 +26,7 @@ if var == "torch":
     f = lambda: torch.nn.functional.linear(A, B)
 else:
     v = int(var)
-    lib.eegf_tune(1, {7: 5, 8: 6}.get(v, v))
+    lib.eegf_tune(1, {8: 6}.get(v, v))        # -1 auto, 0 2-phase, 4 8-phase, 8 4-wave
     f = lambda: K.gemm(A, B, C, M=M, N=N, K=Kd, a_kc=1, b_kc=1, lda=Kd, ldb=Kd, ldc=N)
 for _ in range(iters):
     f()

@@ -15,7 +15,7 @@ for s in "${@:2}"; do
     newtests) tstep newtests timeout -k 10 600 python -u -m pytest tests/test_fixtures_gpu.py tests/test_production_gpu.py -v --timeout 240 --timeout-method thread > $O/${TAG}_new_tests.log 2>&1 || exit 1 ;;
     prof16) (cd /tmp && export TMPDIR=/tmp && step prof16 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$O/${TAG}_prof16 -o run -- python3 -m pytest $GRAFT_REPO_ROOT/tests/test_production_gpu.py -x -q -k "b16 and not priconcat and not True" --timeout 240 > $GRAFT_REPO_ROOT/$O/${TAG}_prof16.log 2>&1) || exit 1 ;;
     tests) tstep tests timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 240 --timeout-method thread > $O/${TAG}_gpu_tests.log 2>&1 || exit 1 ;;
-    gemm8tests) EEGF_GEMM8=1 step gemm8tests timeout -k 10 300 python -u -m pytest tests/test_gemm_gpu.py -x -q --timeout 120 --timeout-method thread > $O/${TAG}_gemm8_tests.log 2>&1 || exit 1 ;;
+    gemm8tests) EEGF_GEMM8=4 step gemm8tests timeout -k 10 300 python -u -m pytest tests/test_gemm_gpu.py -x -q --timeout 120 --timeout-method thread > $O/${TAG}_gemm8_tests.log 2>&1 || exit 1 ;;
     gemmab) step gemmab timeout -k 10 300 python -u tools/gemm_bench.py --ab > $O/${TAG}_gemm_ab.log 2>&1 || exit 1 ;;
     attn) step attn timeout -k 10 120 python -u tools/attn_bench.py > $O/${TAG}_attn.log 2>&1 && EEGF_ATTN256=0 step attn0 timeout -k 10 120 python -u tools/attn_bench.py >> $O/${TAG}_attn.log 2>&1 || exit 1 ;;
     attntests) step attntests timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread -k "attention" > $O/${TAG}_attn_tests.log 2>&1 || exit 1 ;;
