@@ -38,7 +38,27 @@ struct BigArgs {
   float* colsum_part;    // AKC only: [tiles_m][K] partial column sums of A (nullable)
   float* rowsum_part;    // gemm4w RS only: [splits][M] sums over this split's K of each row of a k-major A
   long long* ts;         // diagnostics (eegf_gemm_big_timestamps): per-workgroup phase times, null = off
+  int group_m;           // tile raster: 0 row-major, G > 0 groups of G row panels walked column by column
 };
+// key 9: -1 (default) = groups of 4 row panels when the grid is at least 8 tile columns wide (the
+// K = 768 forward / input-gradient GEMMs with N >= 2304: +2-4 %, profiles/r2r_group.log), row-major
+// otherwise (N = 768: 3 tile columns, no gain)
+int g_group_m = [] { const char* e = getenv("EEGF_GEMM_GROUP"); return e ? atoi(e) : -1; }();
+int group_for(int N) { return g_group_m >= 0 ? g_group_m : ((N + 255) / 256 >= 8 ? 4 : 0); }
+// Logical tile t (after xcd_remap: consecutive t share an XCD) -> (tile row, tile column).  Grouped
+// raster: G row panels x all column tiles per group, column-major inside the group, so the ~32 tiles
+// an XCD runs at once touch G A-panels and ~32/G B-panels instead of ~3 A-panels and every B-panel.
+DEV void tile_coords(const BigArgs& g, int t, int tiles_m, int tiles_n, int& tm, int& tn) {
+  if (g.group_m <= 0) {
+    tm = t / tiles_n;
+    tn = t % tiles_n;
+    return;
+  }
+  const int per = g.group_m * tiles_n, grp = t / per, r = t % per;
+  const int rows = min(g.group_m, tiles_m - grp * g.group_m);
+  tm = grp * g.group_m + r % rows;
+  tn = r / rows;
+}
 // Phase timestamps (100 MHz s_memrealtime) of one workgroup: 0 start, 1 prologue done, 2 K-loop done,
 // 3 epilogue issued; slot 4 = the CU it ran on (8 int64 per workgroup) -- tools/gemm_phases.py turns them into per-phase times and dispatch gaps
 DEV void ts_mark(const BigArgs& g, int k) {
@@ -275,7 +295,8 @@ __global__ void __launch_bounds__(NT, 1) gemm_big_kernel(BigArgs g) {
   const int wm = wave >> 2, wn = wave & 3;
   const int tiles_n = (g.N + TN - 1) / TN, tiles_m = (g.M + TM - 1) / TM;
   const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int tm = t / tiles_n, tn = t % tiles_n;
+  int tm, tn;
+  tile_coords(g, t, tiles_m, tiles_n, tm, tn);
   const int m0 = tm * TM, n0 = tn * TN;
 
   f32x4 acc[8][4];
@@ -460,7 +481,8 @@ __global__ void __launch_bounds__(NT, 1) gemm8_kernel(BigArgs g) {
   const int wm = wave >> 2, wn = wave & 3;
   const int tiles_n = (g.N + TN - 1) / TN, tiles_m = (g.M + TM - 1) / TM;
   const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int tm = t / tiles_n, tn = t % tiles_n;
+  int tm, tn;
+  tile_coords(g, t, tiles_m, tiles_n, tm, tn);
   const int m0 = tm * TM, n0 = tn * TN;
   int kbeg = 0, kend = g.K;
   if (g.ksplit > 0) { kbeg = blockIdx.y * g.ksplit; kend = min(g.K, kbeg + g.ksplit); }
@@ -664,7 +686,8 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
   const int wm = wave >> 1, wn = wave & 1;
   const int tiles_n = (g.N + TN - 1) / TN, tiles_m = (g.M + TM - 1) / TM;
   const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int tm = t / tiles_n, tn = t % tiles_n;
+  int tm, tn;
+  tile_coords(g, t, tiles_m, tiles_n, tm, tn);
   const int m0 = tm * TM, n0 = tn * TN;
   int kbeg = 0, kend = g.K;
   if (g.ksplit > 0) { kbeg = blockIdx.y * g.ksplit; kend = min(g.K, kbeg + g.ksplit); }
@@ -887,7 +910,8 @@ __global__ void __launch_bounds__(NT4, 2) gemm4h_kernel(BigArgs g) {
   const int wm = wave >> 1, wn = wave & 1;
   const int tiles_n = (g.N + TNH - 1) / TNH, tiles_m = (g.M + TM - 1) / TM;
   const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int tm = t / tiles_n, tn = t % tiles_n;
+  int tm, tn;
+  tile_coords(g, t, tiles_m, tiles_n, tm, tn);
   const int m0 = tm * TM, n0 = tn * TNH;
   const int nk = g.K / BK4;
 
@@ -1023,7 +1047,6 @@ __global__ void __launch_bounds__(NT4, 2) gemm4h_kernel(BigArgs g) {
 }
 
 int g_gemm4h = [] { const char* e = getenv("EEGF_GEMM4H"); return e ? atoi(e) : 2; }();   // eegf_tune key 8
-
 template <bool AKC, bool BKC, int EPI, typename TO>
 int launch_big(const BigArgs& a, int splits, hipStream_t s) {
   const int tiles = ((a.M + TM - 1) / TM) * ((a.N + TN - 1) / TN);
@@ -1135,7 +1158,7 @@ int eegf_gemm_big_wgrad_bias(int M, int N, int K, const void* A, long lda, const
   float* slabs = (float*)workspace;
   float* part = slabs + (splits > 1 ? (long)splits * M * N : 0);
   BigArgs a{(const bf16*)A, (const bf16*)B, splits > 1 ? (void*)slabs : (void*)C, nullptr, nullptr, lda, ldb, ldc, 0,
-            M, N, K, 1.0f, beta, 1.0f, splits > 1 ? ks : 0, nullptr, part, g_ts_buf};
+            M, N, K, 1.0f, beta, 1.0f, splits > 1 ? ks : 0, nullptr, part, g_ts_buf, group_for(N)};
   const int tiles = ((M + TM - 1) / TM) * ((N + TN - 1) / TN);
   hipLaunchKernelGGL((gemm4w_kernel<false, false, EPI_NONE, float, true>), dim3(tiles, splits), dim3(NT4), 0,
                      stream, a);
@@ -1160,7 +1183,7 @@ int eegf_gemm_big(int a_kc, int b_kc, int epi, int out_f32, int M, int N, int K,
   if (lda % 8 || ldb % 8 || ldc % 8 || (aux && ldaux % 8)) return 1;
   if ((((uintptr_t)A | (uintptr_t)B | (uintptr_t)C | (uintptr_t)aux) & 15) != 0) return 1;
   BigArgs a{(const bf16*)A, (const bf16*)B, C, bias, (bf16*)aux, lda, ldb, ldc, ldaux, M, N, K, alpha, beta,
-            epi_scale, 0, a_colsum, nullptr, g_ts_buf};
+            epi_scale, 0, a_colsum, nullptr, g_ts_buf, group_for(N)};
   if (a_colsum && (!a_kc || out_f32)) return 1;
   if (out_f32) {
     if (a_kc || b_kc || epi != EPI_NONE || M < 256 || N < 256 || K < 4096 || ldc % 4) return 1;
@@ -1229,6 +1252,7 @@ extern "C" int eegf_tune(int key, int value) {
   }
   if (key == 2) { const int o = g_attn256_mode; g_attn256_mode = value; return o; }
   if (key == 8) { const int o = g_gemm4h; g_gemm4h = value; return o; }
+  if (key == 9) { const int o = g_group_m; g_group_m = value; return o; }
   if (key == 7) { const int o = g_ln_bwd_rpb; if (value < 4 || value > 1024 || value % 4) return EEGF_ERR_ARG; g_ln_bwd_rpb = value; return o; }
   if (key == 6) { const int o = g_ln_rpw; if (value < 1 || value > 64) return EEGF_ERR_ARG; g_ln_rpw = value; return o; }
   return EEGF_ERR_ARG;

@@ -534,3 +534,4 @@ def test_gemm_4h_dgrad(epi, M, N, K):
         _check(out, ref, torch.bfloat16)
     finally:
         _tune(8, old)
+

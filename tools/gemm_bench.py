@@ -87,13 +87,16 @@ def run(name, M, N, Kd, layout, epi, iters=20):
             for v in VARIANTS:
                 # -1: default routing; 0: 2-phase 8-wave; 4: 8-phase 8-wave; 8: 4-wave (key 1 = 6);
                 # 9: default routing with the 256x128 two-workgroup kernel for every short-K GEMM (key 8)
-                lib.eegf_tune(1, -1 if v in (-1, 9) else {8: 6}.get(v, v))
-                lib.eegf_tune(8, 1 if v == 9 else 2 if v == -1 else 0)
+                # 20 + G: default routing with the grouped tile raster of G row panels (key 9)
+                lib.eegf_tune(1, -1 if v in (-1, 9) or v >= 20 else {8: 6}.get(v, v))
+                lib.eegf_tune(8, 1 if v == 9 else 2 if (v == -1 or v >= 20) else 0)
+                lib.eegf_tune(9, v - 20 if 20 <= v < 40 else -1 if v == -1 else 0)
                 f()
                 torch.cuda.synchronize()
                 r[v].append(timed(f, iters))
         lib.eegf_tune(1, -1)
         lib.eegf_tune(8, 2)
+        lib.eegf_tune(9, -1)
         med = {v: sorted(x)[len(x) // 2] for v, x in r.items()}
         tt = timed(tf, iters)
         print(f"{name:16s} {M}x{N}x{Kd} " + " | ".join(f"v{v} {tf_(med[v]):6.1f}" for v in med)
