@@ -267,7 +267,10 @@ DEV u32x4s philox4x32_r(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint
     uint32_t hi0, hi1;
     uint32_t lo0 = mulhilo(0xD2511F53u, c0, &hi0);
     uint32_t lo1 = mulhilo(0xCD9E8D57u, c2, &hi1);
-    uint32_t n0 = hi1 ^ c1 ^ k0, n1 = lo1, n2 = hi0 ^ c3 ^ k1, n3 = lo0;
+    // three-input XORs as one v_bitop3_b32 each (truth table 0x96; hipcc emits two v_xor_b32 for
+    // a ^ b ^ c): 2 instead of 4 bitwise VALU ops per round beside the two v_mad_u64_u32
+    uint32_t n0 = __builtin_amdgcn_bitop3_b32(hi1, c1, k0, 0x96), n1 = lo1;
+    uint32_t n2 = __builtin_amdgcn_bitop3_b32(hi0, c3, k1, 0x96), n3 = lo0;
     c0 = n0; c1 = n1; c2 = n2; c3 = n3;
     k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
   }

@@ -143,9 +143,36 @@ DEV bf16x8 rd_col_rm(const bf16* t, int r0, int c0, int lane) {
   return r;
 }
 
-template <bool LOAD, int NTH = NT, int TNT = TN>
+template <bool LOAD, int NTH = NT, int TNT = TN, bool BATCHED = false>
 DEV void tile_io(bf16* lds, bf16* gp, long ld, int m0, int n0, int M, int N, int tid) {
   constexpr int LDCT = TNT + 8, CPR = TNT / 8;      // epilogue tile row stride, 16-B chunks per row
+  constexpr int ITER = (TM * TNT / 8) / NTH;
+  if (BATCHED && LOAD && m0 + TM <= M && n0 + TNT <= N) {
+    // interior tile: BATCH loads in flight before the first use.  The guarded loop below compiles
+    // to load -> s_waitcnt vmcnt(0) -> ds_write per 16-B chunk, i.e. one full memory round trip per
+    // chunk (16 per thread for the aux tile of the activation-product input gradient)
+    // (batch sized to the registers the kernels leave free in their epilogues: 8 waves of 128x64 and
+    // the two-workgroup 256x128 kernel 4, the 4-wave 256x256 kernel 8)
+    constexpr int BATCH = (NTH >= 512 || TNT < TN) ? 4 : 8;
+#pragma unroll
+    for (int k0 = 0; k0 < ITER; k0 += BATCH) {
+      u32x4 v[BATCH];
+#pragma unroll
+      for (int b = 0; b < BATCH; ++b) {
+        const int c = tid + NTH * (k0 + b);
+        const int r = c / CPR, cc = (c % CPR) * 8;
+        v[b] = LOAD ? ld16(gp + (long)(m0 + r) * ld + n0 + cc) : ld16(lds + r * LDCT + cc);
+      }
+#pragma unroll
+      for (int b = 0; b < BATCH; ++b) {
+        const int c = tid + NTH * (k0 + b);
+        const int r = c / CPR, cc = (c % CPR) * 8;
+        if (LOAD) st16(lds + r * LDCT + cc, v[b]);
+        else st16(gp + (long)(m0 + r) * ld + n0 + cc, v[b]);
+      }
+    }
+    return;
+  }
 #pragma unroll 4
   for (int k = 0; k < (TM * TNT / 8) / NTH; ++k) {
     const int c = tid + NTH * k;
@@ -204,17 +231,30 @@ DEV void big_epilogue(const BigArgs& g, f32x4 (&acc)[8][NJ], bf16* lds, int m0, 
   // LDS-staged bf16 epilogue: every global access is a full 16-B-per-lane row segment
   bf16* ct = lds;
   bf16* Cb = (bf16*)g.C;
+  // the lane's bias values for all NJ column groups in one batch of 16-B loads (one wait): loaded per
+  // column group inside the loop below, each group paid a full L2 round trip before its first use
+  constexpr bool BIAS_PRE = HAS_BIAS && TNT == TN;   // the 256x128 kernel has no registers to spare
+  f32x4 biasv[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    biasv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (BIAS_PRE) {
+      const int n = n0 + wn * WN + j * 16 + 4 * (lane >> 4);
+      if (n + 3 < g.N && ((uintptr_t)(g.bias + n) & 15) == 0) biasv[j] = *(const f32x4*)(g.bias + n);
+      else
+        for (int r = 0; r < 4; ++r) biasv[j][r] = (n + r < g.N) ? g.bias[n + r] : 0.f;
+    }
+  }
   if (AUX_IN || g.beta != 0.f) {
-    tile_io<true, NTH, TNT>(ct, AUX_IN ? g.aux : Cb, AUX_IN ? g.ldaux : g.ldc, m0, n0, g.M, g.N, tid);
+    tile_io<true, NTH, TNT, AUX_IN>(ct, AUX_IN ? g.aux : Cb, AUX_IN ? g.ldaux : g.ldc, m0, n0, g.M, g.N, tid);
     __syncthreads();
   }
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int nl = wn * WN + j * 16 + 4 * (lane >> 4);
-    const int n = n0 + nl;
-    float bias[4] = {0.f, 0.f, 0.f, 0.f};
-    if (HAS_BIAS)
-      for (int r = 0; r < 4; ++r) bias[r] = (n + r < g.N) ? g.bias[n + r] : 0.f;
+    float bias[4] = {biasv[j][0], biasv[j][1], biasv[j][2], biasv[j][3]};
+    if (HAS_BIAS && !BIAS_PRE)
+      for (int r = 0; r < 4; ++r) bias[r] = (n0 + nl + r < g.N) ? g.bias[n0 + nl + r] : 0.f;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       bf16* lp = ct + (wm * 128 + i * 16 + (lane & 15)) * LDC + nl;

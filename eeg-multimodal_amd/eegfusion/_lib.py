@@ -10,7 +10,8 @@ import os
 from pathlib import Path
 
 _LIB = None
-LIB_PATH = Path(__file__).resolve().parent / "libeegfusion.so"
+# EEGF_LIB: an alternative build of the same library for A/B timing (tools/); default the in-tree one
+LIB_PATH = Path(os.environ.get("EEGF_LIB") or Path(__file__).resolve().parent / "libeegfusion.so").resolve()
 
 F32, BF16 = 0, 1
 ERR_ARG = -1
