@@ -147,12 +147,13 @@ template <bool LOAD, int NTH = NT, int TNT = TN, bool BATCHED = false>
 DEV void tile_io(bf16* lds, bf16* gp, long ld, int m0, int n0, int M, int N, int tid) {
   constexpr int LDCT = TNT + 8, CPR = TNT / 8;      // epilogue tile row stride, 16-B chunks per row
   constexpr int ITER = (TM * TNT / 8) / NTH;
-  if (BATCHED && LOAD && m0 + TM <= M && n0 + TNT <= N) {
+  if (BATCHED && m0 + TM <= M && n0 + TNT <= N) {
     // interior tile: BATCH loads in flight before the first use.  The guarded loop below compiles
     // to load -> s_waitcnt vmcnt(0) -> ds_write per 16-B chunk, i.e. one full memory round trip per
-    // chunk (16 per thread for the aux tile of the activation-product input gradient)
-    // (batch sized to the registers the kernels leave free in their epilogues: 8 waves of 128x64 and
-    // the two-workgroup 256x128 kernel 4, the 4-wave 256x256 kernel 8)
+    // chunk (16 per thread for the aux tile of the activation-product input gradient).  Batch sized
+    // to the registers left free while the accumulators are live: 4 for the 8-wave and the
+    // two-workgroup kernels, 8 for the 4-wave 256x256 kernel.  (Batching the final LDS -> global
+    // store the same way measured no change: profiles/r2x_lib_ab.log.)
     constexpr int BATCH = (NTH >= 512 || TNT < TN) ? 4 : 8;
 #pragma unroll
     for (int k0 = 0; k0 < ITER; k0 += BATCH) {

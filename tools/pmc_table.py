@@ -28,17 +28,21 @@ N_SIMD = 1024
 
 # bench.py roofline groups -> kernel-name fragments (mangled or demangled) + grid filters
 GROUPS = {     # bf16 instantiations appear mangled in rocprofv3's CSV (DF16b), the others demangled
-    "dgrad_cs": ("gemm8_kernelILb1ELb0ELi0EDF16bLi4ELb1E",),
-    "ffn1_fwd": ("gemm8_kernelILb1ELb1ELi2EDF16bLi4E", "gemm8_kernelILb1ELb1ELi8EDF16bLi4E"),
-    "qkv_fwd": ("gemm8_kernelILb1ELb1ELi1EDF16bLi4E",),
+    "ffn1_fwd": ("gemm8_kernelILb1ELb1ELi2EDF16bLb0E", "gemm8_kernelILb1ELb1ELi8EDF16bLb0E"),
+    "qkv_fwd": ("gemm8_kernelILb1ELb1ELi1EDF16bLb0E",),
     "ffn2_fwd": ("gemm4w_kernelILb1ELb1ELi1EDF16bLb0E",),
-    "dgrad_qkv_ffn1": ("gemm4w_kernelILb1ELb0ELi0EDF16bLb0ELb0E",),
-    "dgrad_out": ("gemm8_kernelILb1ELb0ELi0EDF16bLi4ELb0E",),
-    "dgrad_ffn2": ("gemm8_kernelILb1ELb0ELi9EDF16bLi4E",),
-    "wgrad": ("gemm4w_kernel<false, false, 0, float, false", "gemm4w_kernelILb0ELb0ELi0EfLb0E"),
+    "dgrad_qkv_ffn1": ("gemm4w_kernelILb1ELb0ELi0EDF16bLb0E",),
+    "ao_fwd": ("gemm4h_kernelILb1ELi1E", "gemm4h_kernel<true, 1>"),
+    "dgrad_out": ("gemm4h_kernelILb0ELi0E", "gemm4h_kernel<false, 0>"),
+    "dgrad_ffn2": ("gemm8_kernelILb1ELb0ELi9EDF16bLb0E",),
+    "wgrad": ("gemm4w_kernel<false, false, 0, float, true", "gemm4w_kernelILb0ELb0ELi0EfLb1E"),
     "attn_fwd": ("attn_fwd256_kernel",),
-    "attn_bwd": ("attn_bwd_kernel", "attn_bwd256_kernel"),
+    "attn_bwd": ("attn_bwd256_kernel",),
+    "ln_fwd": ("ln_fwd_kernel",),
+    "ln_bwd": ("ln_bwd_kernel",),
 }
+# bench.py probes the QKV and FFN1 input gradients separately; they share one kernel and grid here
+ALIASES = {"dgrad_qkv": "dgrad_qkv_ffn1", "dgrad_ffn1": "dgrad_qkv_ffn1"}
 
 
 def short(name):
@@ -150,6 +154,9 @@ def main():
         groups[g] = {"launches_per_step": w, "avg_us": wavg("avg_us"), "mfma_busy": wavg("mfma_busy"),
                      "hbm_bytes_per_launch": wavg("hbm_bytes"), "clock_ghz": wavg("clock_ghz"),
                      "lds_conflict_frac": wavg("lds_conflict_frac"), "round": tag}
+    for a, g in ALIASES.items():
+        if g in groups:
+            groups[a] = dict(groups[g], alias_of=g)
     (ROOT / "profiles" / f"pmc_{tag}.json").write_text(json.dumps(groups, indent=1) + "\n")
     print(json.dumps(groups, indent=1))
 
