@@ -198,7 +198,7 @@ DEV void st4(bf16* p, const float (&v)[4]) { bf16x4 x; x[0] = (bf16)v[0]; x[1] =
 // 4 waves of 128x128); NTH threads.
 template <int EPI, typename TO, int NJ = 4, int NTH = NT, int TNT = TN>
 DEV void big_epilogue(const BigArgs& g, f32x4 (&acc)[8][NJ], bf16* lds, int m0, int n0, int tid, int lane, int wm,
-                      int wn) {
+                      int wn, int split = -1) {   // split: the split-K slab (-1: blockIdx.y)
   constexpr int WN = 16 * NJ;
   constexpr int LDC = TNT + 8;
   constexpr bool HAS_BIAS = EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_TANH ||
@@ -206,7 +206,7 @@ DEV void big_epilogue(const BigArgs& g, f32x4 (&acc)[8][NJ], bf16* lds, int m0, 
   constexpr bool AUX_IN = EPI == EPI_DGELU || EPI == EPI_DRELU || EPI == EPI_DTANH || EPI == EPI_MUL_AUX;
   if constexpr (sizeof(TO) == 4) {
     // fp32 output (weight gradients): direct 16-B stores of 4 consecutive columns; split-K slabs
-    float* Cf = (float*)g.C + (g.ksplit > 0 ? (long)blockIdx.y * g.M * g.N : 0);
+    float* Cf = (float*)g.C + (g.ksplit > 0 ? (long)(split >= 0 ? split : (int)blockIdx.y) * g.M * g.N : 0);
     const long ldc = g.ksplit > 0 ? g.N : g.ldc;
     const float beta = g.ksplit > 0 ? 0.f : g.beta;
 #pragma unroll
@@ -725,13 +725,25 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
-  const int tiles_n = (g.N + TN - 1) / TN, tiles_m = (g.M + TM - 1) / TM;
-  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int tiles_n = (g.N + TN - 1) / TN, tiles_m = (g.M + TM - 1) / TM, ntiles = tiles_m * tiles_n;
+  // split-K (weight gradients): the (split, tile) pairs are numbered XCD-major over the whole grid, so
+  // the tiles of one split -- which share that split's K-slices of A (across tile columns) and of B
+  // (across tile rows) -- run side by side on one XCD and its L2 serves the re-reads.  Numbered per
+  // split (blockIdx.y) instead, a split's tiles land on all 8 XCDs: L2 hit 0.27-0.34 and 3x the
+  // algorithmic HBM bytes at 6-6.8 TB/s, i.e. HBM-bound (profiles/r2y_pmc_table.md)
+  int t, split = 0;
+  if (gridDim.y > 1) {
+    const int tt = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
+    split = tt / ntiles;
+    t = tt % ntiles;
+  } else {
+    t = xcd_remap(blockIdx.x, ntiles);
+  }
   int tm, tn;
   tile_coords(g, t, tiles_m, tiles_n, tm, tn);
   const int m0 = tm * TM, n0 = tn * TN;
   int kbeg = 0, kend = g.K;
-  if (g.ksplit > 0) { kbeg = blockIdx.y * g.ksplit; kend = min(g.K, kbeg + g.ksplit); }
+  if (g.ksplit > 0) { kbeg = split * g.ksplit; kend = min(g.K, kbeg + g.ksplit); }
   const int nk = (kend - kbeg) / BK4;
 
   // staging: 8 LDS-DMAs per thread per K-tile (4 A + 4 B), each wave-instruction 16 rows x 64 B, in
@@ -912,12 +924,12 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
       v += __shfl_xor(v, 16, 64);
       v += __shfl_xor(v, 32, 64);
       const int m = m0 + wm * 128 + 16 * (4 * wn + j) + lane;
-      if (lane < 16 && m < g.M) g.rowsum_part[(long)blockIdx.y * g.M + m] = v;
+      if (lane < 16 && m < g.M) g.rowsum_part[(long)split * g.M + m] = v;
     }
   }
   __syncthreads();
   ts_mark(g, 2);
-  big_epilogue<EPI, TO, 8, NT4>(g, acc, lds, m0, n0, tid, lane, wm, wn);
+  big_epilogue<EPI, TO, 8, NT4>(g, acc, lds, m0, n0, tid, lane, wm, wn, split);
   ts_mark(g, 3);
 }
 
