@@ -299,14 +299,24 @@ DEV void drop_mask4(uint64_t seed, uint64_t offset, uint64_t e4, float p, float 
 // Philox4x32-7 (Random123: BigCrush-clean at 7 rounds), eight 16-bit draws per call.  Element e
 // is kept iff halfword (e & 7) of philox7(e >> 3, offset; seed) >= thr16 = (uint32)(p * 65536)
 // (halfword k = bits 16*(k&1).. of word k>>1).  Returns the 8 keep bits (bit k = element 8c+k).
+// Both halfwords of a word against thr16 at once: saturating packed subtract of (thr16 - 1), then
+// min with 1 -> 0 / 1 in bits 0 and 16.  (Written as asm: hipcc turns the elementwise builtins back
+// into 8 v_cmp + v_cndmask pairs with SGPR-mask hazards -- 14 VALU per call here vs ~21 + s_nops.)
+DEV uint32_t pk_keep01(uint32_t w, uint32_t thrm1x2, uint32_t ones) {
+  uint32_t d, m;
+  asm("v_pk_sub_u16 %0, %1, %2 clamp" : "=v"(d) : "v"(w), "v"(thrm1x2));
+  asm("v_pk_min_u16 %0, %1, %2" : "=v"(m) : "v"(d), "v"(ones));
+  return m;
+}
 DEV uint32_t keep_bits8(uint64_t seed, uint64_t offset, uint64_t call, uint32_t thr16) {
   const u32x4s r = philox4x32_r<7>((uint32_t)call, (uint32_t)(call >> 32), (uint32_t)offset,
                                    (uint32_t)(offset >> 32), (uint32_t)seed, (uint32_t)(seed >> 32));
-  const uint32_t w[4] = {r.x, r.y, r.z, r.w};
-  uint32_t bits = 0;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) bits |= (uint32_t)(((w[k >> 1] >> (16 * (k & 1))) & 0xFFFFu) >= thr16) << k;
-  return bits;
+  const uint32_t tm = (thr16 - 1u) & 0xFFFFu, tm2 = tm | (tm << 16), ones = 0x00010001u;
+  // word j's halfword keep flags land at bits 2j (low half) and 16 + 2j (high half)
+  const uint32_t b = pk_keep01(r.x, tm2, ones) | (pk_keep01(r.y, tm2, ones) << 2) |
+                     (pk_keep01(r.z, tm2, ones) << 4) | (pk_keep01(r.w, tm2, ones) << 6);
+  const uint32_t bits = (b & 0x55u) | (b >> 15);     // bit k = halfword k
+  return thr16 ? bits : 0xFFu;                       // thr16 = 0 (p < 2^-16): every element kept
 }
 DEV uint32_t thr16_of(float p) { return (uint32_t)fminf(p * 65536.0f, 65535.0f); }
 
