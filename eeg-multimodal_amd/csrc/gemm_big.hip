@@ -1284,6 +1284,7 @@ int eegf_gemm_big_colsum_tiles(int M, int N, int K) {
 }
 
 extern int g_attn256_mode;     // attention.hip
+extern int g_ln_fwd768;        // layernorm.hip
 
 // Tuning / A-B hook (returns the old value; test and benchmark state, include/eegfusion.h lists the
 // keys): 1 = 256x256 GEMM kernel (-1 automatic routing (default), 0 2-phase, 4 8-phase, 6 4-wave);
@@ -1307,6 +1308,7 @@ extern "C" int eegf_tune(int key, int value) {
   if (key == 8) { const int o = g_gemm4h; g_gemm4h = value; return o; }
   if (key == 9) { const int o = g_group_m; g_group_m = value; return o; }
   if (key == 7) { const int o = g_ln_bwd_rpb; if (value < 4 || value > 1024 || value % 4) return EEGF_ERR_ARG; g_ln_bwd_rpb = value; return o; }
+  if (key == 10) { const int o = g_ln_fwd768; g_ln_fwd768 = value; return o; }
   if (key == 6) { const int o = g_ln_rpw; if (value < 1 || value > 64) return EEGF_ERR_ARG; g_ln_rpw = value; return o; }
   return EEGF_ERR_ARG;
 }

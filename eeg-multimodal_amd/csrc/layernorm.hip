@@ -13,6 +13,8 @@
 
 int g_ln_bwd_rpb = 64;  // rows per workgroup of eegf_ln_bwd for rows >= 65536 (eegf_tune key 7)
 int g_ln_rpw = 16;  // max rows per wave of eegf_ln_fwd (eegf_tune key 6); see eegf_ln_fwd
+// eegf_tune key 10: bf16 width-768 rows on ln_fwd768_kernel (1, default) or the generic kernel (0)
+int g_ln_fwd768 = 1;
 
 namespace {
 
@@ -140,6 +142,119 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(LnFwdArgs a) {
       }
       V4<T>::store(y + col, o);
     }
+    if (lane == 0) {
+      if (a.mean) a.mean[row] = mean;
+      if (a.rstd) a.rstd[row] = rstd;
+    }
+  }
+}
+
+// bf16 rows of 768 (the BERT hidden LayerNorms): 16-B accesses for columns 0..511 (lane l owns 8l ..
+// 8l + 7) and 8-B accesses for 512..767 (lane l owns 512 + 4l .. + 3), so 2 / 3 of the row moves in
+// 1-KB wave-instructions (ln_fwd_kernel's 4-column lane chunks move 512 B per instruction).  The
+// dropout stream is the same function of (row, column): columns 8l .. 8l + 7 are exactly call
+// row * 96 + l (no cross-lane exchange), columns 512 + 4l .. are half of call row * 96 + 64 + l / 2.
+DEV void ld8bf(const bf16* p, float (&v)[8]) {
+  const bf16x8 x = *(const bf16x8*)p;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = (float)x[e];
+}
+DEV void st8bf(bf16* p, const float (&v)[8]) {
+  bf16x8 x;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) x[e] = (bf16)v[e];
+  *(bf16x8*)p = x;
+}
+__global__ void __launch_bounds__(256, 4) ln_fwd768_kernel(LnFwdArgs a) {   // 4 waves per SIMD: <= 128 VGPRs
+  constexpr int W = 768;
+  const int lane = threadIdx.x & 63;
+  const long row0 = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * a.rpw;
+  if (row0 >= a.rows) return;
+  const long rend = row0 + a.rpw < a.rows ? row0 + a.rpw : a.rows;
+  const bool drop = a.drop_mode != 0 && a.p > 0.f;
+  const float dscale = drop ? 1.0f / (1.0f - a.p) : 1.0f;
+  const uint32_t thr = thr16_of(a.p);
+  const int ca = 8 * lane, cb = 512 + 4 * lane;      // the lane's column groups
+  const bf16* X = (const bf16*)a.x;
+  const bf16* Rr = (const bf16*)a.r;
+  bf16x8 pxa, pra = {};
+  bf16x4 pxb, prb = {};
+  pxa = *(const bf16x8*)(X + row0 * W + ca);
+  pxb = *(const bf16x4*)(X + row0 * W + cb);
+  if (Rr) { pra = *(const bf16x8*)(Rr + row0 * W + ca); prb = *(const bf16x4*)(Rr + row0 * W + cb); }
+  for (long row = row0; row < rend; ++row) {
+    const bf16x8 cxa = pxa, cra = pra;
+    const bf16x4 cxb = pxb, crb = prb;
+    if (row + 1 < rend) {
+      pxa = *(const bf16x8*)(X + (row + 1) * W + ca);
+      pxb = *(const bf16x4*)(X + (row + 1) * W + cb);
+      if (Rr) { pra = *(const bf16x8*)(Rr + (row + 1) * W + ca); prb = *(const bf16x4*)(Rr + (row + 1) * W + cb); }
+    }
+    uint32_t ka = 0xFFu, kb = 0xFu;                   // keep bits: ka bit e <-> ca + e, kb bit e <-> cb + e
+    if (drop) {
+      ka = keep_bits8(a.seed, a.offset, (uint64_t)row * 96 + lane, thr);
+      kb = (keep_bits8(a.seed, a.offset, (uint64_t)row * 96 + 64 + (lane >> 1), thr) >> (4 * (lane & 1))) & 0xFu;
+    }
+    float v[12];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (float)cxa[e];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[8 + e] = (float)cxb[e];
+    if (drop && a.drop_mode == 1) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] *= ((ka >> e) & 1u) ? dscale : 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[8 + e] *= ((kb >> e) & 1u) ? dscale : 0.f;
+    }
+    if (Rr) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += (float)cra[e];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[8 + e] += (float)crb[e];
+    }
+    if (a.table) {
+      const float* tp = a.table + (row % a.table_period) * W;
+      const f32x4 t0 = *(const f32x4*)(tp + ca), t1 = *(const f32x4*)(tp + ca + 4), t2 = *(const f32x4*)(tp + cb);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { v[e] += t0[e]; v[4 + e] += t1[e]; v[8 + e] += t2[e]; }
+    }
+    if (a.table2) {
+      const f32x4 t0 = *(const f32x4*)(a.table2 + ca), t1 = *(const f32x4*)(a.table2 + ca + 4),
+                  t2 = *(const f32x4*)(a.table2 + cb);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { v[e] += t0[e]; v[4 + e] += t1[e]; v[8 + e] += t2[e]; }
+    }
+    if (a.s) {
+      bf16* sp = (bf16*)a.s + row * W;
+      float va[8] = {v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]};
+      st8bf(sp + ca, va);
+      V4<bf16>::store(sp + cb, f32x4{v[8], v[9], v[10], v[11]});
+    }
+    float sum = 0.f;
+#pragma unroll
+    for (int e = 0; e < 12; ++e) sum += v[e];
+    const float mean = wave_sum(sum) * (1.0f / W);
+    float sq = 0.f;
+#pragma unroll
+    for (int e = 0; e < 12; ++e) { const float d = v[e] - mean; sq += d * d; }
+    const float rstd = rsqrtf(wave_sum(sq) * (1.0f / W) + a.eps);
+    const f32x4 g0 = *(const f32x4*)(a.gamma + ca), g1 = *(const f32x4*)(a.gamma + ca + 4), g2 = *(const f32x4*)(a.gamma + cb);
+    const f32x4 b0 = *(const f32x4*)(a.beta + ca), b1 = *(const f32x4*)(a.beta + ca + 4), b2 = *(const f32x4*)(a.beta + cb);
+    const float gm[12] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3], g2[0], g2[1], g2[2], g2[3]};
+    const float bt[12] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3], b2[0], b2[1], b2[2], b2[3]};
+    float o[12];
+#pragma unroll
+    for (int e = 0; e < 12; ++e) o[e] = (v[e] - mean) * rstd * gm[e] + bt[e];
+    if (drop && a.drop_mode == 2) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] *= ((ka >> e) & 1u) ? dscale : 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[8 + e] *= ((kb >> e) & 1u) ? dscale : 0.f;
+    }
+    bf16* y = (bf16*)a.y + row * W;
+    float oa[8] = {o[0], o[1], o[2], o[3], o[4], o[5], o[6], o[7]};
+    st8bf(y + ca, oa);
+    V4<bf16>::store(y + cb, f32x4{o[8], o[9], o[10], o[11]});
     if (lane == 0) {
       if (a.mean) a.mean[row] = mean;
       if (a.rstd) a.rstd[row] = rstd;
@@ -394,6 +509,13 @@ extern "C" int eegf_ln_fwd(int dtype, long rows, int width, const void* x, const
   // 65536 x 768 bf16 (tools/ln_bench.py): 86 -> 67 us without, 97 -> 88 us with the residual store
   while (a.rpw * 2 <= g_ln_rpw && rows / (4L * a.rpw * 2) >= 1024) a.rpw *= 2;
   if (dtype == EEGF_F32) return ln_fwd_t<float>(width / 256, a, stream);
+  if (dtype == EEGF_BF16 && width == 768 && g_ln_fwd768 &&
+      ((((uintptr_t)x | (uintptr_t)r | (uintptr_t)y | (uintptr_t)s_out | (uintptr_t)table | (uintptr_t)table2 |
+         (uintptr_t)gamma | (uintptr_t)beta) & 15) == 0)) {
+    const dim3 grid((unsigned)((a.rows + 4L * a.rpw - 1) / (4L * a.rpw)));
+    hipLaunchKernelGGL(ln_fwd768_kernel, grid, dim3(256), 0, stream, a);
+    return (int)hipGetLastError();
+  }
   if (dtype == EEGF_BF16) return ln_fwd_t<bf16>(width / 256, a, stream);
   return EEGF_ERR_ARG;
 }

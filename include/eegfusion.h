@@ -69,7 +69,9 @@ int eegf_gemm(int dtype, int out_dtype, int a_kcontig, int b_kcontig, int epi,
  *   key 8: 256x128 two-workgroups-per-CU GEMM for K < 2048 bf16 outputs: 0 off, 1 every such GEMM,
  *          2 (default) N <= 768 only;
  *   key 9: tile raster of the 256-row GEMMs: -1 (default) groups of 4 row panels when N >= 2048,
- *          row-major otherwise; 0 row-major; G > 0 groups of G row panels walked column by column. */
+ *          row-major otherwise; 0 row-major; G > 0 groups of G row panels walked column by column;
+ *   key 10: bf16 768-wide rows of eegf_ln_fwd on the 16-B-access kernel (1, default) or the generic
+ *          4-columns-per-lane kernel (0). */
 int eegf_tune(int key, int value);
 /* Diagnostics (no reference counterpart): every following 256-row GEMM launch of the 8-wave / 4-wave
  * kernels writes 4 s_memrealtime stamps per workgroup (start, prologue done, K-loop done, epilogue
