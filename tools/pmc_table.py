@@ -38,7 +38,7 @@ GROUPS = {     # bf16 instantiations appear mangled in rocprofv3's CSV (DF16b), 
     "wgrad": ("gemm4w_kernel<false, false, 0, float, true", "gemm4w_kernelILb0ELb0ELi0EfLb1E"),
     "attn_fwd": ("attn_fwd256_kernel",),
     "attn_bwd": ("attn_bwd256_kernel",),
-    "ln_fwd": ("ln_fwd_kernel",),
+    "ln_fwd": ("ln_fwd_kernel", "ln_fwd768_kernel"),
     "ln_bwd": ("ln_bwd_kernel",),
 }
 # bench.py probes the QKV and FFN1 input gradients separately; they share one kernel and grid here
