@@ -1169,12 +1169,33 @@ __global__ void __launch_bounds__(256) big_splitk_reduce(const float* __restrict
 }
 
 // db[m] += sum over splits of part[s][m] (fixed order: bitwise reproducible)
-__global__ void __launch_bounds__(256) rowsum_reduce(const float* __restrict__ part, int splits, int M, float* db) {
-  const int m = blockIdx.x * 256 + threadIdx.x;
+DEV void rowsum_reduce_at(const float* __restrict__ part, int splits, int M, float* db, int m) {
   if (m >= M) return;
   float v = 0.f;
   for (int s = 0; s < splits; ++s) v += part[(long)s * M + m];
   db[m] += v;
+}
+__global__ void __launch_bounds__(256) rowsum_reduce(const float* __restrict__ part, int splits, int M, float* db) {
+  rowsum_reduce_at(part, splits, M, db, blockIdx.x * 256 + threadIdx.x);
+}
+// the weight gradient's slab reduction and the bias gradient's row-sum reduction in one launch: blocks
+// below nslab reduce the slabs (as big_splitk_reduce), the rest the row sums (as rowsum_reduce) -- two
+// independent fixed-order sums, one launch instead of two per weight gradient (48 per step)
+__global__ void __launch_bounds__(256) splitk_rowsum_reduce(const float* __restrict__ slabs, int splits, long MN, int N,
+                                                            float* C, long ldc, float beta, int nslab,
+                                                            const float* __restrict__ part, int M, float* db) {
+  if ((int)blockIdx.x >= nslab) {
+    rowsum_reduce_at(part, splits, M, db, ((int)blockIdx.x - nslab) * 256 + threadIdx.x);
+    return;
+  }
+  const long i4 = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i4 >= MN) return;
+  f32x4 o = {0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < splits; ++s) o += *(const f32x4*)(slabs + (long)s * MN + i4);
+  const long m = i4 / N, n = i4 % N;
+  float* c = C + m * ldc + n;
+  if (beta != 0.f) o += beta * *(const f32x4*)c;
+  *(f32x4*)c = o;
 }
 
 // split count of the weight-gradient GEMM (fp32 slabs over K = tokens): the count that fills whole
@@ -1215,13 +1236,15 @@ int eegf_gemm_big_wgrad_bias(int M, int N, int K, const void* A, long lda, const
   const int tiles = ((M + TM - 1) / TM) * ((N + TN - 1) / TN);
   hipLaunchKernelGGL((gemm4w_kernel<false, false, EPI_NONE, float, true>), dim3(tiles, splits), dim3(NT4), 0,
                      stream, a);
+  const int nrow = (M + 255) / 256;
   if (splits > 1) {
     const long MN = (long)M * N;
-    hipLaunchKernelGGL(big_splitk_reduce, dim3((unsigned)((MN / 4 + 255) / 256)), dim3(256), 0, stream,
-                       (const float*)slabs, splits, MN, N, C, ldc, beta);
+    const int nslab = (int)((MN / 4 + 255) / 256);
+    hipLaunchKernelGGL(splitk_rowsum_reduce, dim3((unsigned)(nslab + nrow)), dim3(256), 0, stream, (const float*)slabs,
+                       splits, MN, N, C, ldc, beta, nslab, (const float*)part, M, db);
+  } else {
+    hipLaunchKernelGGL(rowsum_reduce, dim3((unsigned)nrow), dim3(256), 0, stream, (const float*)part, splits, M, db);
   }
-  hipLaunchKernelGGL(rowsum_reduce, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, stream, (const float*)part, splits,
-                     M, db);
   return (int)hipGetLastError();
 }
 
