@@ -59,7 +59,7 @@ KERNEL_GROUPS = {
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=40)   # ~2.8 s timed: long enough for an smi sampler to see the GPU busy
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
     ap.add_argument("--variant", default="prigumbel", choices=["prigumbel", "priconcat"])
