@@ -29,9 +29,11 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import hashlib
 import subprocess
 import sys
 import time
+import types
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent
@@ -68,9 +70,16 @@ def parse_args(argv=None):
     ap.add_argument("--eps-mode", default="newfrac", choices=["newfrac", "new"])
     ap.add_argument("--feawei", type=int, default=0, help="feawei feature pass over this many synthetic samples")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-batch", type=int, default=16)
-    ap.add_argument("--cpu-iters", type=int, default=3)
+    ap.add_argument("--cpu-batch", type=int, default=256, help="CPU-baseline batch (BASELINE.md §3: 256)")
+    ap.add_argument("--cpu-iters", type=int, default=1, help="CPU-baseline timed iterations after one warm-up")
     ap.add_argument("--master-port", type=int, default=29531)
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend for N > 1: nccl (= RCCL, one GPU per rank) or gloo (device "
+                         "tensors through host memory; lets N ranks share one GPU to exercise the DDP body "
+                         "where only one GPU exists — its timing is not an RCCL measurement)")
+    ap.add_argument("--check-replicas", action="store_true",
+                    help="after the timed loop, all-gather a SHA-256 of every rank's fp32 master weights and Adam "
+                         "moments and report whether the replicas are bitwise identical")
     ap.add_argument("--selftest", action="store_true",
                     help="launcher / process-group check only (gloo, CPU): rank 0 prints the world size")
     return ap.parse_args(argv)
@@ -103,14 +112,18 @@ def cpu_model() -> str:
 def cpu_baseline(variant: str, batch: int, iters: int) -> dict:
     """The CPU oracle (torch fp32 restatement, oracle/fusion_oracle.py; pinned against the reference's
     own outputs by tests/test_oracle_golden.py) timed on the host cores on a bounded sample of the
-    same iteration.  Threads = the CPUs this process may run on (sched_getaffinity), capped by
-    OMP_NUM_THREADS (the GPU box's CPU share)."""
+    same iteration: the bench's batch (256), dropout 0.1 at every reference site as on the GPU leg,
+    PriConcat with the honoured feature_all_lap mechanism, one warm-up iteration then `iters` timed.
+    Threads = the CPUs this process may run on (sched_getaffinity), capped by OMP_NUM_THREADS (the
+    GPU box's CPU share)."""
     import torch
+    import torch.nn.functional as F
     from oracle import fusion_oracle as O
     avail = len(os.sched_getaffinity(0))
     threads = min(avail, int(os.environ.get("OMP_NUM_THREADS", avail)) or avail)
     torch.set_num_threads(threads)
     g = torch.Generator().manual_seed(0)
+    O.set_dropout_replay(lambda site, x: F.dropout(x, 0.1, training=True))
     shapes = O.param_shapes("W", "prigumbel" if variant == "prigumbel" else "priconcat")
     p = {}
     for k, s in shapes.items():
@@ -152,21 +165,27 @@ def cpu_baseline(variant: str, batch: int, iters: int) -> dict:
             mopt.step()
         else:
             mopt.zero_grad()
-            pc = O.PathConfig(contract="W", variant="priconcat")
-            torch.nn.functional.cross_entropy(O.forward(p, batch_d, pc), labels).backward()
+            pc = O.PathConfig(contract="W", variant="priconcat", honor_dp_mode=True)
+            row = lap.sample((batch,)).view(batch)
+            torch.nn.functional.cross_entropy(O.forward(p, batch_d, pc, row_noise=row), labels).backward()
             mopt.step()
 
-    iteration()                                        # warm-up
-    t0 = time.perf_counter()
-    for _ in range(iters):
-        iteration()
-    dt = time.perf_counter() - t0
+    try:
+        t0 = time.perf_counter()
+        iteration()                                    # warm-up (allocations, thread pool)
+        warm = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            iteration()
+        dt = time.perf_counter() - t0
+    finally:
+        O.set_dropout_replay(None)
     return {"value": round(batch * iters / dt, 4), "unit": "samples/s", "cores": threads, "kind": "port",
-            "cpu_model": cpu_model(), "cpus_available": avail,
-            "sample": f"oracle/fusion_oracle.py {variant} iteration (torch CPU fp32, dropout 0), batch {batch}, "
-                      f"64x256 EEG + 32-d action, {iters} timed iterations after 1 warm-up, {dt:.1f} s; "
-                      f"batch {batch} not 256: one B=256 iteration takes ~45 s on 16 cores, too long for the "
-                      f"default run's few-minute budget (BASELINE.md §3)"}
+            "cpu_model": cpu_model(), "cpus_available": avail, "seconds_per_iteration": round(dt / iters, 2),
+            "warmup_seconds": round(warm, 2),
+            "sample": f"oracle/fusion_oracle.py {variant} iteration (torch CPU fp32, dropout 0.1"
+                      f"{', feature_all_lap honoured' if variant != 'prigumbel' else ''}), batch {batch}, "
+                      f"64x256 EEG + 32-d action, {iters} timed iteration(s) after 1 warm-up, {dt:.1f} s timed"}
 
 
 def load_profile_json(name: str, tag: str):
@@ -223,14 +242,21 @@ def main():
         if w > 1:
             dist.destroy_process_group()
         return
+    # nccl: one GPU per rank (LOCAL_RANK); gloo may put several ranks on one GPU (device_count()
+    # does not initialise the GPU)
+    ndev = torch.cuda.device_count() if args.dist_backend == "gloo" else 0
+    dev_idx = local % max(1, ndev) if args.dist_backend == "gloo" else local
     if world_env > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(dev_idx)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_idx))
+        else:
+            dist.init_process_group("gloo")
         world, backend = dist.get_world_size(), dist.get_backend()
         if world != args.gpus:
             print(f"bench.py: process group has {world} ranks, --gpus {args.gpus}", file=sys.stderr)
             sys.exit(2)
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", dev_idx)
 
     from eegfusion.modules import PriConcatModel, PriGumbelModel
     from eegfusion.trainer import GradReducer, PriGumbelTrainer, SinglePassTrainer
@@ -240,10 +266,13 @@ def main():
     if args.variant == "prigumbel":
         model = PriGumbelModel(sweep[0], contract="W", eps_mode=args.eps_mode, dropout=0.1, seed=980616 + rank)
     else:
-        model = PriConcatModel(None, contract="W", dropout=0.1, seed=980616 + rank)
+        # configs[1] "PriConcat eps=1.0": the feature_all_lap mechanism honoured so eps
+        # takes effect (main_0430.py:118 passes dp_mode=None, which would make it an identity)
+        model = PriConcatModel(types.SimpleNamespace(EPSILON=1.0), dp_mode="feature_all_lap", honor_dp_mode=True,
+                               contract="W", dropout=0.1, seed=980616 + rank)
     model = model.to(dev).set_compute_dtype(torch.bfloat16)
     eng = model.engine
-    reducer = GradReducer()
+    reducer = GradReducer(scale_in_optimizer=True)     # 1/N applied inside the fused Adam
     trainer_cls = PriGumbelTrainer if args.variant == "prigumbel" else SinglePassTrainer
 
     B = args.batch
@@ -309,6 +338,21 @@ def main():
         per_eps.append({"eps": eps, "samples_per_s": round(world * B * args.steps / dt, 2),
                         "ms_per_step": round(dt / args.steps * 1e3, 3), "loss": float(loss[-1].item())})
 
+    replicas = None
+    if args.check_replicas:
+        torch.cuda.synchronize()
+        h = hashlib.sha256(eng.a.master.cpu().numpy().tobytes())
+        for opt in (getattr(trainer, "model_opt", None), getattr(trainer, "dp_opt", None), getattr(trainer, "opt", None)):
+            if opt is not None:
+                h.update(opt.m.cpu().numpy().tobytes())
+                h.update(opt.v.cpu().numpy().tobytes())
+        digests = [None] * world
+        if world > 1:
+            dist.all_gather_object(digests, h.hexdigest())
+        else:
+            digests = [h.hexdigest()]
+        replicas = {"identical": len(set(digests)) == 1, "sha256": digests[0][:16], "ranks": world}
+
     if rank == 0:
         steps = args.steps * len(sweep)
         value = world * B * steps / total_dt
@@ -353,6 +397,8 @@ def main():
         if len(sweep) > 1 or feawei is not None:
             out["sweep"] = per_eps
             out["feawei"] = feawei
+        if replicas is not None:
+            out["replicas"] = replicas
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.variant, args.cpu_batch, args.cpu_iters)
         print(json.dumps(out), flush=True)

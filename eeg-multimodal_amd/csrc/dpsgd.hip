@@ -83,7 +83,8 @@ __global__ void __launch_bounds__(256) rowsum_kernel(int S, int n, const float* 
 template <typename T>
 __global__ void __launch_bounds__(256) seg_sqnorm_kernel(int Tn, int W, const T* __restrict__ dy, long ldd,
                                                          const T* __restrict__ xs, long ldx, const float* __restrict__ mean,
-                                                         const float* __restrict__ rstd, float beta, float* __restrict__ out) {
+                                                         const float* __restrict__ rstd, int bias_term, float beta,
+                                                         float* __restrict__ out) {
   __shared__ float red[4];
   const int s = blockIdx.x;
   const long row0 = (long)s * Tn;
@@ -95,7 +96,7 @@ __global__ void __launch_bounds__(256) seg_sqnorm_kernel(int Tn, int W, const T*
       a += d;
       if (xs) g += d * (to_f32(xs[(row0 + t) * ldx + c]) - mean[row0 + t]) * rstd[row0 + t];
     }
-    v += a * a + g * g;
+    v += (bias_term ? a * a : 0.f) + g * g;
   }
   v = wave_sum(v);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
@@ -189,15 +190,17 @@ extern "C" int eegf_ghost_norm(int dtype, int S, int T, int Dx, int Dy, const vo
 }
 
 extern "C" int eegf_seg_sqnorm(int dtype, int S, int T, int W, const void* dy, long ldd, const void* xs, long ldx,
-                               const float* mean, const float* rstd, float beta, float* out, hipStream_t stream) {
+                               const float* mean, const float* rstd, int bias_term, float beta, float* out,
+                               hipStream_t stream) {
   if (S <= 0 || T <= 0 || W <= 0 || !dy || !out) return EEGF_ERR_ARG;
   if (xs && (!mean || !rstd)) return EEGF_ERR_ARG;
+  if (!xs && !bias_term) return EEGF_ERR_ARG;
   if (dtype == EEGF_F32)
     hipLaunchKernelGGL(seg_sqnorm_kernel<float>, dim3(S), dim3(256), 0, stream, T, W, (const float*)dy, ldd,
-                       (const float*)xs, ldx, mean, rstd, beta, out);
+                       (const float*)xs, ldx, mean, rstd, bias_term, beta, out);
   else if (dtype == EEGF_BF16)
     hipLaunchKernelGGL(seg_sqnorm_kernel<bf16>, dim3(S), dim3(256), 0, stream, T, W, (const bf16*)dy, ldd,
-                       (const bf16*)xs, ldx, mean, rstd, beta, out);
+                       (const bf16*)xs, ldx, mean, rstd, bias_term, beta, out);
   else return EEGF_ERR_ARG;
   return (int)hipGetLastError();
 }

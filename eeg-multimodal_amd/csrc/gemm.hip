@@ -505,7 +505,9 @@ static int gemm_impl(int dtype, int out_dtype, int a_kcontig, int b_kcontig, int
   if (batch == 1 && workspace && tiles < 512 && (K >= 4096 || (tiles <= 256 && K >= 512))) {
     const int kt = dtype == EEGF_F32 ? 32 : 64;
     int splits = 1;
-    const int min_slice = K >= 4096 ? 1024 : 256;
+    // fp32 batch-row GEMMs (decoder / head, 48-96 tiles): slices down to 128 so ~200 workgroups fill
+    // the CUs (one 64x64 fp32 tile over K = 768 is ~5 us of MFMA on one CU)
+    const int min_slice = K >= 4096 ? 1024 : (dtype == EEGF_F32 ? 128 : 256);
     while (splits * tiles < 512 && K / (splits * 2) >= min_slice) splits *= 2;
     while (splits > 1 && (long)splits * M * N * 4 > ws_bytes) splits /= 2;
     if (splits > 1) {

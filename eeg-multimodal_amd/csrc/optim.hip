@@ -3,9 +3,11 @@
 // Replaces torch.optim.Adam(params, lr) (past_acc.py:159-160, train.py:77, base_train.py:170-171):
 // one launch updates a contiguous range of the fp32 master arena (the two reference optimizers
 // own disjoint ranges: model params and DP), and optionally refreshes the bf16 compute shadow
-// of the same range in the same pass (no separate cast kernel on the hot path).
+// of the same range in the same pass (no separate cast kernel on the hot path).  grad_scale folds the
+// data-parallel 1/N average into the read of the all-reduced gradient sum (no separate scaling pass
+// over the gradient arena; g * (1/N) in fp32 is the product torch's mul_ would store).
 // Arithmetic follows torch's single-tensor Adam (torch/optim/adam.py _single_tensor_adam):
-//   g += wd*p; m = b1*m + (1-b1)*g; v = b2*v + (1-b2)*g^2;
+//   g = grad_scale*g + wd*p; m = b1*m + (1-b1)*g; v = b2*v + (1-b2)*g^2;
 //   p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps)     (m via lerp, as torch)
 #include "common.h"
 #include "eegfusion_internal.h"
@@ -15,7 +17,7 @@ namespace {
 __global__ void __launch_bounds__(256) adam_kernel(long n, float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v,
                                                    bf16* __restrict__ shadow, float b1, float b2, float eps, float wd,
-                                                   float step_size, float sqrt_bc2) {
+                                                   float gscale, float step_size, float sqrt_bc2) {
   const long i4 = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
   if (i4 >= n) return;
   if (i4 + 4 <= n) {
@@ -23,7 +25,7 @@ __global__ void __launch_bounds__(256) adam_kernel(long n, float* __restrict__ p
     f32x4 mv = *(const f32x4*)(m + i4), vv = *(const f32x4*)(v + i4);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      float gr = gv[e];
+      float gr = gv[e] * gscale;
       if (wd != 0.f) gr += wd * pv[e];
       mv[e] = mv[e] + (1.f - b1) * (gr - mv[e]);              // exp_avg.lerp_(grad, 1-beta1)
       vv[e] = b2 * vv[e] + (1.f - b2) * gr * gr;
@@ -40,7 +42,7 @@ __global__ void __launch_bounds__(256) adam_kernel(long n, float* __restrict__ p
     }
   } else {
     for (long i = i4; i < n; ++i) {
-      float gr = g[i];
+      float gr = g[i] * gscale;
       if (wd != 0.f) gr += wd * p[i];
       m[i] = m[i] + (1.f - b1) * (gr - m[i]);
       v[i] = b2 * v[i] + (1.f - b2) * gr * gr;
@@ -70,7 +72,7 @@ __global__ void __launch_bounds__(256) key_bias_kernel(long n, const long long* 
 }  // namespace
 
 extern "C" int eegf_adam(long n, float* p, const float* g, float* m, float* v, void* bf16_shadow, float lr, float beta1,
-                         float beta2, float eps, float weight_decay, int step, hipStream_t stream) {
+                         float beta2, float eps, float weight_decay, float grad_scale, int step, hipStream_t stream) {
   if (n <= 0 || !p || !g || !m || !v || step <= 0) return EEGF_ERR_ARG;
   if ((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) != 0) return EEGF_ERR_ARG;
   if (bf16_shadow && ((uintptr_t)bf16_shadow & 7) != 0) return EEGF_ERR_ARG;
@@ -78,7 +80,7 @@ extern "C" int eegf_adam(long n, float* p, const float* g, float* m, float* v, v
   const float step_size = (float)(lr / bc1), sqrt_bc2 = (float)sqrt(bc2);
   const long blocks = (n + 1023) / 1024;
   hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, n, p, g, m, v, (bf16*)bf16_shadow,
-                     beta1, beta2, eps, weight_decay, step_size, sqrt_bc2);
+                     beta1, beta2, eps, weight_decay, grad_scale, step_size, sqrt_bc2);
   return (int)hipGetLastError();
 }
 

@@ -63,7 +63,7 @@ SIGNATURES: dict[str, list] = {
                         vp, i64, vp, i64, vp, i64, vp, vp],
     "eegf_cross_entropy": [i32, i32, i32, vp, vp, i32, f32, vp, vp, vp, vp],
     "eegf_feawei_init": [i32, vp, i64, f32, i32, vp, vp, vp],
-    "eegf_adam": [i64, vp, vp, vp, vp, vp, f32, f32, f32, f32, f32, i32, vp],
+    "eegf_adam": [i64, vp, vp, vp, vp, vp, f32, f32, f32, f32, f32, f32, i32, vp],
     "eegf_cast_f32_bf16": [i64, vp, vp, vp],
     "eegf_axpby": [i32, i64, f32, vp, f32, vp, vp],
     "eegf_tanh_bwd": [i32, i64, vp, vp, vp, vp],
@@ -77,7 +77,7 @@ SIGNATURES: dict[str, list] = {
     # DP-SGD (dpsgd.hip)
     "eegf_ghost_norm_workspace": [i32, i32],
     "eegf_ghost_norm": [i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, f32, vp, vp],
-    "eegf_seg_sqnorm": [i32, i32, i32, i32, vp, i64, vp, i64, vp, vp, f32, vp, vp],
+    "eegf_seg_sqnorm": [i32, i32, i32, i32, vp, i64, vp, i64, vp, vp, i32, f32, vp, vp],
     "eegf_row_sqnorm": [i32, i32, i32, vp, i64, i32, vp, i64, vp, vp],
     "eegf_dp_clip_rows": [i32, i32, vp, f32, vp, vp, vp],
     "eegf_dp_noise": [i64, vp, f32, f32, u64, u64, vp],

@@ -27,6 +27,7 @@ Gaussian noise and the 1/expected-batch scale in one pass per parameter.
 """
 from __future__ import annotations
 
+import logging
 import math
 
 import torch
@@ -36,6 +37,8 @@ from torch.utils.data import DataLoader, Sampler
 from . import _lib
 from ._lib import call
 from .privacy import create_accountant, get_noise_multiplier
+
+log = logging.getLogger(__name__)
 
 _UNSUPPORTED = ("multi_head_decoder.", "multi_head_decoderlayer.", "bert.embeddings.", "eeg_encoder.", "DP")
 
@@ -147,17 +150,25 @@ def private_backward(model, saved, dlogits, need: set[str]):
     dp["last_norms"], dp["last_clip"] = psn, clip
 
 
+def _draw_seed() -> int:
+    return int(torch.randint(0, 2 ** 62, (), dtype=torch.int64).item())
+
+
 class DPOptimizer:
     """opacus DPOptimizer over the wrapped optimizer: step() = add N(0, (sigma C)^2) noise to every
     trainable parameter's (clipped-sum) gradient and divide by the expected batch size, count one
     accountant step, then the original step."""
 
     def __init__(self, optimizer, *, noise_multiplier: float, max_grad_norm: float, expected_batch_size: int,
-                 seed: int = 980616, on_step=None):
+                 seed: int | None = None, on_step=None):
         self.original_optimizer = optimizer
         self.noise_multiplier, self.max_grad_norm = float(noise_multiplier), float(max_grad_norm)
         self.expected_batch_size = int(expected_batch_size)
-        self.seed, self.steps, self.on_step = seed, 0, on_step
+        # opacus draws its noise from torch's advancing generator: take the Philox key from the global
+        # torch RNG (so set_seed(...) decides it and two optimizers in one process differ); a fixed
+        # seed is an explicit test option
+        self.seed = _draw_seed() if seed is None else int(seed)
+        self.steps, self.on_step = 0, on_step
 
     @property
     def param_groups(self):
@@ -202,7 +213,7 @@ class DPOptimizer:
 class PrivacyEngine:
     """opacus PrivacyEngine stand-in (make_private / make_private_with_epsilon / get_epsilon)."""
 
-    def __init__(self, *, accountant: str = "rdp", secure_mode: bool = False, seed: int = 980616):
+    def __init__(self, *, accountant: str = "rdp", secure_mode: bool = False, seed: int | None = None):
         if secure_mode:
             raise NotImplementedError("secure_mode (cryptographic RNG) is not provided")
         self.accountant = create_accountant(accountant)
@@ -228,6 +239,12 @@ class PrivacyEngine:
         sigma = get_noise_multiplier(target_epsilon=target_epsilon, target_delta=target_delta, sample_rate=sample_rate,
                                      epochs=epochs, accountant=self.accountant.mechanism(),
                                      epsilon_tolerance=epsilon_tolerance)
+        # opacus >= 1.3 defaults to the PRV accountant; this build implements RDP only, so sigma can
+        # differ from such a run: say which one chose it
+        log.info("make_private_with_epsilon: noise_multiplier %.6f from the %s accountant (target eps %g, delta %g, "
+                 "sample rate %g, %d epochs)", sigma, self.accountant.mechanism(), target_epsilon, target_delta,
+                 sample_rate, epochs)
+        self.last_noise_multiplier = sigma
         return self.make_private(module=module, optimizer=optimizer, data_loader=data_loader, noise_multiplier=sigma,
                                  max_grad_norm=max_grad_norm, **kw)
 

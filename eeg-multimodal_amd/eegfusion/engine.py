@@ -213,6 +213,7 @@ class FusionEngine:
         N, K = w.shape
         ldaux = aux.shape[-1] if aux is not None else 0
         if bias_grad is not None and self.psn is not None:
+            self._psn_mark(bias_grad, "a fused bias gradient")
             self._psn_bias(dy, M, N, ldd or N)
             bias_grad = None
         if bias_grad is not None:
@@ -250,8 +251,10 @@ class FusionEngine:
         g = gw if gw is not None else self.G(name)
         N, K = g.shape
         if self.psn is not None:
+            self._psn_mark(g, name)
             self._psn_linear(dy, x, M, N, K, ldd or N, ldx or K)
             if gb is not None:
+                self._psn_mark(gb, bias or name + " (bias)")
                 self._psn_bias(dy, M, N, ldd or N)
             return
         ev = self._ev_start("wgrad" if M >= 4096 else None)
@@ -277,11 +280,25 @@ class FusionEngine:
         if self.psn is not None:
             if period != 1:
                 raise NotImplementedError(f"eegfusion DP-SGD: per-sample norms of {name} (periodic sum)")
+            self._psn_mark(o, name)
             self._psn_bias(dy, rows, width, ld or width)
             return
         self.colsum(dy, ld or width, rows, width, o, period)
 
     # ---------------------------------------------------- DP-SGD per-sample gradient norms (dpsgd.hip)
+    def _psn_mark(self, dst, name):
+        """The norm pass adds each gradient site's own squared per-sample norm, which is the
+        parameter's per-sample norm only when the site is the parameter's sole contribution
+        (sum_k ||g_k||^2 != ||sum_k g_k||^2).  Disjoint slices of one parameter (the decoder's in_proj
+        Q / K|V blocks) are distinct destinations; a destination reached twice (e.g. a shared
+        visual_encoder in IICA / TISC) is refused instead of under-clipping silently."""
+        seen = self.psn.setdefault("seen", set())
+        key = (dst.data_ptr(), dst.numel())
+        if key in seen:
+            raise NotImplementedError(f"eegfusion DP-SGD: {name} receives gradient from two sites of the graph; "
+                                      "per-sample norms of a shared parameter are not implemented")
+        seen.add(key)
+
     def _psn_rows(self, M):
         """rows per sample of a gradient site with M rows: 1 (head / pooler / decoder) or T (BERT)"""
         ps = self.psn
@@ -304,13 +321,14 @@ class FusionEngine:
         call("eegf_ghost_norm", _code(dy), ps["B"], T, K, N, P(x), ldx, P(dy), ldd, P(ws), n, 1.0, P(ps["out"]),
              _stream())
 
-    def _psn_bias(self, dy, M, W, ld, ln=None):
+    def _psn_bias(self, dy, M, W, ld, ln=None, bias_term=True):
         """squared per-sample norms of a bias gradient dy.sum(0) (dy [M, W]); ln = (s, mean, rstd) adds
-        the LayerNorm gamma term sum_t dy_t * xhat_t"""
+        the LayerNorm gamma term sum_t dy_t * xhat_t; bias_term=False leaves out the dy.sum(0) term
+        (LayerNorm beta frozen)"""
         ps, T = self.psn, self._psn_rows(M)
         xs, mean, rstd = ln if ln is not None else (None, None, None)
-        call("eegf_seg_sqnorm", _code(dy), ps["B"], T, W, P(dy), ld, P(xs), W, P(mean), P(rstd), 1.0, P(ps["out"]),
-             _stream())
+        call("eegf_seg_sqnorm", _code(dy), ps["B"], T, W, P(dy), ld, P(xs), W, P(mean), P(rstd), int(bias_term), 1.0,
+             P(ps["out"]), _stream())
 
     def colsum(self, src, ld, rows, width, dst, period=1):
         """dst += column sums of src (rows x width, row stride ld); deferred to the end of the backward
@@ -371,10 +389,15 @@ class FusionEngine:
         call("eegf_ln_bwd", _code(dy), rows, HID, P(dy), P(s), P(mean), P(rstd), P(self.F(pre + ".weight")), float(p),
              int(mode if p > 0 else 0), self.cfg.seed, rng, P(dx), P(dr), P(part), P(part[nb * HID:]), _stream())
         if self.psn is not None:
-            if self.need(pre + ".weight") or self.need(pre + ".bias"):
+            gamma, beta = self.need(pre + ".weight"), self.need(pre + ".bias")
+            if gamma or beta:
                 if mode == 2 and p > 0:
                     raise NotImplementedError("eegfusion DP-SGD: per-sample norms of a post-LN-dropout LayerNorm")
-                self._psn_bias(dy, rows, HID, HID, ln=(s, mean, rstd))
+                if gamma:
+                    self._psn_mark(self.G(pre + ".weight"), pre + ".weight")
+                if beta:
+                    self._psn_mark(self.G(pre + ".bias"), pre + ".bias")
+                self._psn_bias(dy, rows, HID, HID, ln=(s, mean, rstd) if gamma else None, bias_term=beta)
             return
         self.bgrad(part[: nb * HID], pre + ".weight", nb, HID)
         self.bgrad(part[nb * HID:], pre + ".bias", nb, HID)

@@ -40,7 +40,7 @@ class Adam(torch.optim.Optimizer):
                 st["step"] += 1
                 call("eegf_adam", p.numel(), p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(),
                      st["exp_avg_sq"].data_ptr(), None, float(group["lr"]), float(b1), float(b2), float(group["eps"]),
-                     float(group["weight_decay"]), st["step"], torch.cuda.current_stream().cuda_stream)
+                     float(group["weight_decay"]), 1.0, st["step"], torch.cuda.current_stream().cuda_stream)
                 a = ParamArena.owner(p)
                 if a is not None:
                     a.invalidate_shadow()

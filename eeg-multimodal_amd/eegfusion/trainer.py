@@ -52,7 +52,8 @@ class FlatAdam:
     def zero_grad(self):
         self.e.a.grad[self.lo:self.hi].zero_()
 
-    def step(self):
+    def step(self, grad_scale: float = 1.0):
+        """grad_scale multiplies the gradient as Adam reads it (1/N over an all-reduced sum)."""
         a = self.e.a
         self.t += 1
         sh = None
@@ -63,7 +64,8 @@ class FlatAdam:
             o = lo - self.lo
             call("eegf_adam", hi - lo, a.master[lo:].data_ptr(), a.grad[lo:].data_ptr(), self.m[o:].data_ptr(),
                  self.v[o:].data_ptr(), None if sh is None else a.shadow[lo:].data_ptr(), float(self.lr),
-                 float(self.betas[0]), float(self.betas[1]), float(self.eps), float(self.wd), self.t, _s())
+                 float(self.betas[0]), float(self.betas[1]), float(self.eps), float(self.wd), float(grad_scale),
+                 self.t, _s())
 
 
 class GradReducer:
@@ -78,16 +80,20 @@ class GradReducer:
         all_reduce is issued at once (async_op) so RCCL runs it on its own stream while the
         remaining layers' backward kernels run; `finish` reduces what is left (biases, LayerNorm,
         embeddings: their column sums are deferred to the end of the backward), makes the compute
-        stream wait for every outstanding collective, and scales the range by 1/N.
+        stream wait for every outstanding collective, and scales the range by 1/N — or, with
+        scale_in_optimizer=True, leaves the SUM in place and the trainers pass `grad_scale` = 1/N to
+        the fused Adam, which applies it as it reads the gradient (no extra pass over the ~0.47 GB
+        gradient arena per step; bitwise the same update).
     Only parameters in `names` are reduced: the unused decoder template layer and (contract W) the
     word embeddings (31 M of 148 M elements) never enter a bucket.  The issue order is the same on
     every rank (same backward sequence), as RCCL requires.  With world_size 1 nothing is launched,
     but the ranges are still recorded (`self.log`), so a single-GPU test can check coverage.
     """
 
-    def __init__(self, bucket_elems: int = 32 << 20):
+    def __init__(self, bucket_elems: int = 32 << 20, scale_in_optimizer: bool = False):
         self.bucket = bucket_elems
         self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+        self.scale_in_optimizer = bool(scale_in_optimizer)
         self.works, self.todo, self.log = [], set(), []
         self.arena = None
 
@@ -96,7 +102,13 @@ class GradReducer:
             return
         for i in range(0, g.numel(), self.bucket):
             dist.all_reduce(g[i: i + self.bucket], op=dist.ReduceOp.SUM)
-        g.mul_(1.0 / self.world)
+        if not self.scale_in_optimizer:
+            g.mul_(1.0 / self.world)
+
+    @property
+    def grad_scale(self) -> float:
+        """the factor Adam must apply to the reduced gradients (1/N when the reducer leaves sums)"""
+        return 1.0 / self.world if self.scale_in_optimizer else 1.0
 
     @staticmethod
     def ranges(arena, names) -> list[tuple[int, int]]:
@@ -128,7 +140,7 @@ class GradReducer:
         for w in self.works:
             w.wait()                    # compute stream waits for the RCCL stream (no host sync)
         self.works = []
-        if self.world > 1:
+        if self.world > 1 and not self.scale_in_optimizer:
             self.arena.grad[lo:hi].mul_(1.0 / self.world)
 
 
@@ -161,7 +173,7 @@ class PriGumbelTrainer:
         e.needs_grad = {"DP"}
         e.backward(sv, dl, head_only=True)
         self.reduce(e.a.grad[self.dp_opt.lo:self.dp_opt.hi])
-        self.dp_opt.step()
+        self.dp_opt.step(self.reduce.grad_scale)
         # ---- pass 2: model parameters (hard=True)
         logits, sv = e.forward(batch, hard=True, training=True, save=True)
         dl = self._ce(logits, labels, 1)
@@ -175,7 +187,7 @@ class PriGumbelTrainer:
             e.grad_ready = None
         e.needs_grad = None
         self.reduce.finish(self.model_opt.lo, self.model_opt.hi)
-        self.model_opt.step()
+        self.model_opt.step(self.reduce.grad_scale)
         return self.loss, self.correct
 
 
@@ -207,7 +219,7 @@ class SinglePassTrainer:
             e.grad_ready = None
         e.needs_grad = None
         self.reduce.finish(0, e.a.numel)
-        self.opt.step()
+        self.opt.step(self.reduce.grad_scale)
         return self.loss, self.correct
 
 
@@ -242,6 +254,6 @@ class PriGumbelV1Trainer:
         e.v1_wloss(1.0, self.loss[1:])     # before finish(): w is all-reduced (sum / N) with the vectors
         e.needs_grad = None
         self.reduce.finish(0, e.a.numel)
-        self.opt.step()
+        self.opt.step(self.reduce.grad_scale)
         self.loss[:1].mul_(self.alpha)
         return self.loss, self.correct

@@ -292,9 +292,10 @@ int eegf_tanh_bwd(int dtype, long n, const void* dy, const void* y, void* dx, hi
 int eegf_dropout(int dtype, long n, int group, float p, unsigned long long seed, unsigned long long offset,
                  void* x, hipStream_t stream);
 
-/* torch.optim.Adam step over a contiguous fp32 range (+ optional bf16 shadow refresh). */
+/* torch.optim.Adam step over a contiguous fp32 range (+ optional bf16 shadow refresh); the gradient
+ * read is g * grad_scale (1 for a plain step, 1/N to average an all-reduced sum over N ranks). */
 int eegf_adam(long n, float* p, const float* g, float* m, float* v, void* bf16_shadow, float lr,
-              float beta1, float beta2, float eps, float weight_decay, int step, hipStream_t stream);
+              float beta1, float beta2, float eps, float weight_decay, float grad_scale, int step, hipStream_t stream);
 int eegf_cast_f32_bf16(long n, const float* src, void* dst, hipStream_t stream);
 /* attention_mask (int64, 1 = keep) -> additive key bias (0 / -1e30) */
 int eegf_key_bias(long n, const long long* mask, float* bias, hipStream_t stream);
@@ -318,11 +319,12 @@ long eegf_ghost_norm_workspace(int S, int T);
  * DY [S*T, Dy] row-major with leading dimensions; Dx, Dy % 32 == 0. */
 int eegf_ghost_norm(int dtype, int S, int T, int Dx, int Dy, const void* X, long ldx, const void* DY, long ldy,
                     float* ws, long ws_elems, float beta, float* out, hipStream_t stream);
-/* Per-sample column sums over T rows: out[s] = beta*out[s] + sum_c (sum_t dy[t,c])^2 (a bias) and, with
- * LayerNorm statistics (xs = pre-LN sum, mean, rstd; nullable), + sum_c (sum_t dy[t,c] xhat[t,c])^2
- * (LN gamma).  T = 1 gives per-row norms. */
+/* Per-sample column sums over T rows: out[s] = beta*out[s] + [bias_term] sum_c (sum_t dy[t,c])^2 (a bias
+ * or LN beta) and, with LayerNorm statistics (xs = pre-LN sum, mean, rstd; nullable),
+ * + sum_c (sum_t dy[t,c] xhat[t,c])^2 (LN gamma).  Each term only for a trainable parameter; xs == NULL
+ * with bias_term == 0 is an argument error.  T = 1 gives per-row norms. */
 int eegf_seg_sqnorm(int dtype, int S, int T, int W, const void* dy, long ldd, const void* xs, long ldx,
-                    const float* mean, const float* rstd, float beta, float* out, hipStream_t stream);
+                    const float* mean, const float* rstd, int bias_term, float beta, float* out, hipStream_t stream);
 /* One row per sample (head / pooler / visual Linear): out[s] += ||a_s||^2 * (b ? ||b_s||^2 : 1). */
 int eegf_row_sqnorm(int dtype, int S, int Wa, const void* a, long lda, int Wb, const void* b, long ldb, float* out,
                     hipStream_t stream);

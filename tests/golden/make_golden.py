@@ -551,9 +551,91 @@ def gen_modal_variants():
                                 eps=1.0, contract="T", B=B, L=L, seed=SEED), out)
 
 
+def c1_split(n=64, L=512, seed=70):
+    """A synthetic split in the reference's feature formats for configs[0] (train.py -bs 32): token ids
+    with real lengths drawn around the measured 33-65 distribution (mean 51.3), CLS/SEP,
+    EEG-digit-like ids; CLIP-like vectors (std 0.5); labels ~ Bernoulli(0.66) with two NaN rows
+    (data.py:29-32 maps them to 0).  Returned as arrays (the fixture stores these, and the test writes
+    the CSV / pickles from them)."""
+    g = torch.Generator().manual_seed(seed)
+    lens = (torch.randn(n, generator=g) * 7.0 + 51.3).round().clamp(33, 65).long()
+    ids = torch.zeros(n, L, dtype=torch.long)
+    mask = torch.zeros(n, L, dtype=torch.long)
+    for b in range(n):
+        k = int(lens[b])
+        ids[b, :k] = torch.cat([torch.tensor([101]), torch.randint(1015, 1025, (k - 2,), generator=g),
+                                torch.tensor([102])])
+        mask[b, :k] = 1
+    clip = (torch.randn(n, 512, generator=g) * 0.5).float()
+    labels = (torch.rand(n, generator=g) < 0.66).double()
+    labels[[5, 40]] = float("nan")
+    return ids, mask, clip, labels
+
+
+def write_split(d: Path, prefix: str, ids, mask, clip, labels):
+    """the reference's formats: feature/{prefix}_EEG.csv (an 'EEG' text column + 'label'),
+    feature/action/{prefix}_clip_v2.pickle (ndarray [N, 512] f32), feature/EEG/{prefix}_bert.pickle
+    (list of BatchEncoding with 1-D 'input_ids' / 'attention_mask' lists)."""
+    import pickle
+
+    import pandas as pd
+    from transformers import BatchEncoding
+    (d / "action").mkdir(parents=True, exist_ok=True)
+    (d / "EEG").mkdir(parents=True, exist_ok=True)
+    pd.DataFrame({"EEG": [" ".join(map(str, r[r > 0].tolist())) for r in ids],
+                  "label": labels.numpy()}).to_csv(d / f"{prefix}_EEG.csv", index=False)
+    with open(d / "action" / f"{prefix}_clip_v2.pickle", "wb") as f:
+        pickle.dump(clip.numpy(), f)
+    enc = [BatchEncoding({"input_ids": ids[i].tolist(), "attention_mask": mask[i].tolist()}) for i in range(len(ids))]
+    with open(d / "EEG" / f"{prefix}_bert.pickle", "wb") as f:
+        pickle.dump(enc, f)
+
+
+def gen_c1_batch32(ref_model):
+    """configs[0]: model.py ConcatModel under train.py's loss (CrossEntropyLoss(reduction='none'), .sum(),
+    train.py:69,110-111) at batch 32, contract T (L = 512 padded token ids).  The split is read back
+    through the reference's own data.MultiModalDataset_ti (data.py:7-34) from files in its formats, so
+    the loader is pinned too.  Per-sample logits / CE of all 64 samples (batches of 32 in dataset order;
+    no op couples samples, so a sample's logits do not depend on its batch), the CE-sum loss and every
+    parameter gradient of the first dataset-order batch.  Deterministic weights, dropout p = 0."""
+    import tempfile
+
+    import data as ref_data
+    torch.manual_seed(71)
+    ids, mask, clip, labels = c1_split()
+    with tempfile.TemporaryDirectory() as td:
+        write_split(Path(td), "train", ids, mask, clip, labels)
+        ds = ref_data.MultiModalDataset_ti(f"{td}/train_EEG.csv", f"{td}/action/train_clip_v2.pickle",
+                                           f"{td}/EEG/train_bert.pickle")
+        items = [ds[i] for i in range(len(ds))]
+    m = prepare(ref_model.ConcatModel(), "T")
+    crit = nn.CrossEntropyLoss(reduction="none")
+    logits_all, ce_all, loss0 = [], [], None
+    for b0 in (0, 32):
+        (frame, vmask, tids, tmask), lab = torch.utils.data.default_collate(items[b0:b0 + 32])
+        lab = lab.view(-1)
+        logits = m((frame, vmask, tids, tmask), hard=True)
+        ce = crit(logits, lab)
+        if b0 == 0:
+            loss0 = ce.sum()
+            loss0.backward()
+        logits_all.append(logits.detach())
+        ce_all.append(ce.detach())
+    loaded_labels = torch.cat([it[1] for it in items]).view(-1)
+    cfg = dict(contract="T", variant="concat", seed=SEED, B=32, N=64, L=512, loss="CE sum (train.py:69,110-111)")
+    save("c1_batch32", cfg, dict(title_input=ids, text_mask=mask, frame_input=clip.unsqueeze(1),
+                                 labels_csv=labels, labels=loaded_labels, logits_all=torch.cat(logits_all),
+                                 ce_all=torch.cat(ce_all), loss=loss0.detach(), **grad_record(m)))
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
     past_acc, main_0430, ref_model = import_reference()
+    if len(sys.argv) > 1:                       # e.g. `make_golden.py c1_batch32`: only those fixtures
+        for name in sys.argv[1:]:
+            fn = globals()[f"gen_{name}"]
+            fn(ref_model) if name == "c1_batch32" else fn()
+        sys.exit(0)
     np.savez_compressed(HERE / "w_values_dp.npz", DP=w_values_dp())
     gen_gate_head(past_acc, ref_model, main_0430)
     gen_prigumbel_full(past_acc, hard=False, tag="soft")
@@ -567,3 +649,5 @@ if __name__ == "__main__":
     gen_feawei_features()
     gen_prigumbel_v1()
     gen_modal_variants()
+    # round 3
+    gen_c1_batch32(ref_model)

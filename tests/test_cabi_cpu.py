@@ -36,4 +36,4 @@ def test_argument_errors_return_status_without_gpu():
     assert lib.eegf_gemm(0, 0, 1, 1, 0, 0, 4, 4, 1, None, 4, 0, None, 4, 0, None, 4, 0, None, 0, None, 0, 0,
                          1.0, 0.0, 1.0, None, 0, None) == _lib.ERR_ARG
     assert lib.eegf_attn_fwd(1, 2, 11, 256, None, 2304, None, 0.125, 0.0, 0, 0, None, 768, None, None, None) == _lib.ERR_ARG
-    assert lib.eegf_adam(0, None, None, None, None, None, 1e-3, 0.9, 0.999, 1e-8, 0.0, 1, None) == _lib.ERR_ARG
+    assert lib.eegf_adam(0, None, None, None, None, None, 1e-3, 0.9, 0.999, 1e-8, 0.0, 1.0, 1, None) == _lib.ERR_ARG

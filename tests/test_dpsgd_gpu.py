@@ -69,20 +69,26 @@ def _zero_by_symmetry(name):
     return name.endswith("attention.self.key.bias")
 
 
-def _engine_model(contract, prefixes, C):
+def _engine_model(contract, prefixes, C, dropout=0.0):
     from eegfusion.dpsgd import GradSampleModule
     from eegfusion.modules import PriConcatModel
     torch.manual_seed(0)
-    m = PriConcatModel(types.SimpleNamespace(EPSILON=1.0), contract=contract, dropout=0.0)
+    m = PriConcatModel(types.SimpleNamespace(EPSILON=1.0), contract=contract, dropout=dropout)
     m.load_state_dict(det_params(contract, "priconcat", None, requires_grad=False), strict=False)
     for n, q in m.named_parameters():
         q.requires_grad = n.startswith(prefixes)
     return GradSampleModule(m.cuda().train(), max_grad_norm=C)
 
 
-@pytest.mark.parametrize("cfg", ["main_0430_T", "base_train_W"])
+# LayerNorm gammas trainable with their betas frozen (the beta term must not enter the norm)
+GAMMA_ONLY = ("bert.encoder.layer.11.attention.output.LayerNorm.weight", "bert.encoder.layer.11.output.LayerNorm.weight",
+              "fc_layers.", "classifier.")
+
+
+@pytest.mark.parametrize("cfg", ["main_0430_T", "base_train_W", "gamma_only_W"])
 def test_per_sample_norms_and_clipped_sum(cfg):
-    contract, prefixes = ("T", MAIN_0430) if cfg == "main_0430_T" else ("W", BASE_TRAIN)
+    contract, prefixes = {"main_0430_T": ("T", MAIN_0430), "base_train_W": ("W", BASE_TRAIN),
+                          "gamma_only_W": ("W", GAMMA_ONLY)}[cfg]
     batch, labels = _token_batch() if contract == "T" else _window_batch()
     train, grads = _oracle_per_sample(contract, batch, labels, prefixes)
     norms = torch.stack([torch.sqrt(sum((g[k].double() ** 2).sum() for k in train)) for g in grads])
@@ -109,6 +115,66 @@ def test_per_sample_norms_and_clipped_sum(cfg):
     assert all(named[k].grad.abs().max() < 1e-6 for k in train if _zero_by_symmetry(k))
     frozen = [n for n, q in named.items() if not q.requires_grad and q.grad is not None]
     assert not frozen, frozen[:3]
+
+
+def test_private_backward_with_dropout():
+    """The reference pretrain runs in train mode with dropout 0.1 (main_0430.py:176-187): the norm pass
+    and the clipped-sum pass must replay the same hidden / attention dropout masks.  With C huge
+    (clip = 1) the private gradient is the sum of the per-sample gradients; those are rebuilt by
+    ordinary engine backwards of one sample's CE over the same forward (the same Philox offset,
+    so the same masks), and the per-sample norms must match them, fp32 at 1e-4."""
+    batch, labels = _window_batch()
+    wm = _engine_model("W", BASE_TRAIN, 1e9, dropout=0.1)
+    m = wm._module
+    eeg, act, lab = batch["eeg"].to(DEV), batch["act"].to(DEV), labels.to(DEV)
+    r0 = m.engine.rng_counter
+    torch.nn.functional.cross_entropy(m.forward_window(eeg, act, True), lab).backward()
+    torch.cuda.synchronize()
+    named = dict(m.named_parameters())
+    train = [n for n, q in named.items() if q.requires_grad]
+    priv = {k: named[k].grad.detach().double().cpu().clone() for k in train}
+    psn = m._dp["last_norms"].double().cpu().clone()
+    dp_state, m._dp = m._dp, None
+    per = []
+    try:
+        for b in range(labels.shape[0]):
+            for q in m.parameters():
+                q.grad = None
+            m.engine.rng_counter = r0
+            logits = m.forward_window(eeg, act, True)
+            torch.nn.functional.cross_entropy(logits[b:b + 1], lab[b:b + 1]).backward()
+            torch.cuda.synchronize()
+            per.append({k: named[k].grad.detach().double().cpu().clone() for k in train})
+    finally:
+        m._dp = dp_state
+    norms = torch.stack([sum((g[k] ** 2).sum() for k in train if not _zero_by_symmetry(k)) for g in per])
+    assert rel_err(psn, norms) < 1e-4, (psn, norms)
+    bad = [(k, rel_err(priv[k], sum(g[k] for g in per))) for k in train if not _zero_by_symmetry(k)]
+    bad = [x for x in bad if x[1] > 1e-4]
+    assert not bad, bad[:5]
+
+
+@pytest.mark.parametrize("cls", ["IICA_LapDropout", "TISC_LapDropout"])
+def test_shared_visual_encoder_refused(cls):
+    """visual_encoder reached from two sites (IICA: both image tokens; TISC: the action token and the
+    encoder input) cannot take the per-site norm sum: the norm pass must refuse, not under-clip."""
+    from eegfusion import modules
+    from eegfusion.dpsgd import GradSampleModule
+    torch.manual_seed(0)
+    m = getattr(modules, cls)(dropout=0.0)
+    for n, q in m.named_parameters():
+        q.requires_grad = n.startswith(("visual_encoder.", "fc_layers.", "classifier."))
+    wm = GradSampleModule(m.cuda().train(), max_grad_norm=1.0)
+    g = torch.Generator().manual_seed(3)
+    img = [(torch.randn(2, 1, 512, generator=g) * 0.5).to(DEV) for _ in range(2)]
+    one = torch.ones(2, 1, dtype=torch.long, device=DEV)
+    if cls == "IICA_LapDropout":
+        logits = wm(img[0], one, img[1], one, 1.0, False)
+    else:
+        batch, _ = _token_batch(B=2, L=128)
+        logits = wm(batch["title_input"].to(DEV), batch["text_mask"].to(DEV), img[1], one, 1.0, True)
+    with pytest.raises(NotImplementedError, match="two sites"):
+        torch.nn.functional.cross_entropy(logits, torch.tensor([1, 0], device=DEV)).backward()
 
 
 def test_dp_optimizer_sigma0_exact_and_noise_statistics():
@@ -211,11 +277,20 @@ def test_norm_kernels_vs_float64(dt, T):
     rstd = torch.rand(S * T, device=DEV) + 0.5
     out2 = torch.zeros(S, device=DEV)
     _lib.call("eegf_seg_sqnorm", code, S, T, Dy, DY.data_ptr(), Dy, xs.data_ptr(), Dy, mean.data_ptr(),
-              rstd.data_ptr(), 0.0, out2.data_ptr(), s)
+              rstd.data_ptr(), 1, 0.0, out2.data_ptr(), s)
     xh = (xs.double() - mean.double()[:, None]) * rstd.double()[:, None]
-    ref2 = (y64.sum(1) ** 2).sum(1) + ((DY.double() * xh).view(S, T, Dy).sum(1) ** 2).sum(1)
+    bias_t = (y64.sum(1) ** 2).sum(1)
+    gamma_t = ((DY.double() * xh).view(S, T, Dy).sum(1) ** 2).sum(1)
     torch.cuda.synchronize()
-    assert rel_err(out2.cpu(), ref2.cpu()) < tol
+    assert rel_err(out2.cpu(), (bias_t + gamma_t).cpu()) < tol
+    # gamma-only (LN bias frozen) and bias-only (no LN statistics) terms
+    _lib.call("eegf_seg_sqnorm", code, S, T, Dy, DY.data_ptr(), Dy, xs.data_ptr(), Dy, mean.data_ptr(),
+              rstd.data_ptr(), 0, 0.0, out2.data_ptr(), s)
+    torch.cuda.synchronize()
+    assert rel_err(out2.cpu(), gamma_t.cpu()) < tol
+    _lib.call("eegf_seg_sqnorm", code, S, T, Dy, DY.data_ptr(), Dy, None, 0, None, None, 1, 0.0, out2.data_ptr(), s)
+    torch.cuda.synchronize()
+    assert rel_err(out2.cpu(), bias_t.cpu()) < tol
     # one row per sample
     a = torch.randn(S, 100, device=DEV).to(dt)
     b = torch.randn(S, 40 * T, device=DEV).to(dt)[:, :70]

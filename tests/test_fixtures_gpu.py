@@ -16,7 +16,7 @@ import numpy as np
 import pytest
 import torch
 
-from goldens import check_grads, det_params, load, rel_err, w_values_dp
+from goldens import check_grads, delta_bound, det_params, load, rel_err, w_values_dp
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -204,11 +204,13 @@ def test_three_iterations_trainer():
             continue
         n = key.split(":", 1)[1]
         d = ((after[n].detach() - before[n]) / cfg["lr"]).reshape(-1).cpu().numpy()
+        b0 = before[n].reshape(-1).cpu().numpy()
         if key.startswith("dval:"):
-            d = d[fx["dpos:" + n]]
+            d, b0 = d[fx["dpos:" + n]], b0[fx["dpos:" + n]]
         ref = fx[key]
         big = np.abs(ref) > 0.05
-        assert big.any() and np.abs(d[big] - ref[big]).max() < 5e-3, (n, np.abs(d[big] - ref[big]).max())
+        bound = delta_bound(b0, 5e-3, cfg["lr"])
+        assert big.any() and (np.abs(d[big] - ref[big]) <= bound[big]).all(), (n, np.abs(d[big] - ref[big]).max())
         checked += 1
     assert checked >= 16
 

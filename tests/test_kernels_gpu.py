@@ -440,9 +440,20 @@ def test_adam_matches_torch():
         p_ref.grad = g.clone()
         opt.step()
         lib.call("eegf_adam", n, p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), shadow.data_ptr(), 1e-3, 0.9,
-                 0.999, 1e-8, 0.01, step, _s())
+                 0.999, 1e-8, 0.01, 1.0, step, _s())
     torch.cuda.synchronize()
     assert (p - p_ref.detach()).abs().max().item() < 1e-6
+    # grad_scale: a step over an all-reduced sum of 4 ranks equals the step over the averaged gradient
+    # bitwise (the 1/N product is the fp32 product torch's mul_ stores)
+    p2, m2, v2 = p.clone(), m.clone(), v.clone()
+    g = torch.randn(n, device="cuda")
+    g4 = g.mul(0.25)
+    lib.call("eegf_adam", n, p.data_ptr(), g4.data_ptr(), m.data_ptr(), v.data_ptr(), None, 1e-3, 0.9,
+             0.999, 1e-8, 0.01, 1.0, 4, _s())
+    lib.call("eegf_adam", n, p2.data_ptr(), g.data_ptr(), m2.data_ptr(), v2.data_ptr(), None, 1e-3, 0.9,
+             0.999, 1e-8, 0.01, 0.25, 4, _s())
+    torch.cuda.synchronize()
+    assert torch.equal(p, p2) and torch.equal(m, m2) and torch.equal(v, v2)
     assert (shadow.float() - p).abs().max().item() <= 1e-2 * p.abs().max().item()
 
 

@@ -4,13 +4,16 @@ The 256x256 bf16 kernels route only on large shapes: M >= 2048 rows for gemm8 / 
 with fused bias column sums, K >= 4096 token rows for the split-K weight gradients, L = 256 for the
 persistent attention.  The B <= 4 parity tests never reach them.  Here:
 
-  * B = 16 (R = 4096 tokens: every production route is taken, profiles/r2_b16_kernel_stats.md lists
-    the kernels), bf16 engine vs the fp32 CPU oracle on injected Laplace/Gumbel draws, dropout 0, for
-    PriGumbel soft, PriGumbel hard and PriConcat.  Bounds (bf16 precision, not a parity claim):
-    logits within 5e-2 relative, worst parameter-gradient cosine >= 0.99;
+  * B = 16 (R = 4096 tokens: every production route is taken — test_b16_takes_the_bench_routes checks
+    that the B = 16 step launches every production kernel the B = 256 bench step launches), bf16
+    engine vs the fp32 CPU oracle on injected Laplace/Gumbel draws, dropout 0, for PriGumbel soft,
+    PriGumbel hard and PriConcat.  Bounds (bf16 precision, not a parity claim), set at measured minus
+    margin (profiles/r3a_gpu_tests.log: logits rel <= 4.0e-3, worst gradient cosine >= 0.99842 over
+    the ~190 parameter gradients): logits within 1e-2 relative, worst parameter-gradient cosine >= 0.997;
   * B = 256 and B = 512 (configs[2]/[4] per-GPU sizes), PriGumbel with dropout on: everything finite,
-    bf16 vs fp32 engine on the same inputs and the same Philox streams: cosine >= 0.99 on the
-    logits, the DP gradient and the 12 fused QKV weight gradients;
+    bf16 vs fp32 engine on the same inputs and the same Philox streams (measured: logits cosine
+    1.000000, worst of DP + 36 Q/K/V gradients 0.99796 at B = 256): logits cosine >= 0.9999, the DP
+    gradient and the 36 Q/K/V weight gradients >= 0.996;
   * B = 256 training: the pass-2 loss strictly decreases over 5 PriGumbelTrainer iterations at lr 2e-5
     (draws fixed per step so the objective is one function), parameters and gradients finite.  At lr
     1e-4 (measured r2a) Adam's first, sign-like step of 1e-4 on all 117 M parameters overshoots:
@@ -64,7 +67,7 @@ def test_b16_bf16_production_routing_vs_oracle(variant, hard):
     logits = m.forward_window(eeg.to(DEV), act.to(DEV), hard)
     torch.nn.functional.cross_entropy(logits, labels.to(DEV)).backward()
     torch.cuda.synchronize()
-    assert rel_err(logits.detach().cpu(), ref.detach()) < 5e-2
+    assert rel_err(logits.detach().cpu(), ref.detach()) < 1e-2
     worst = []
     for n, t in m.named_parameters():
         if n not in p or p[n].grad is None or t.grad is None:
@@ -75,8 +78,55 @@ def test_b16_bf16_production_routing_vs_oracle(variant, hard):
             continue                      # structurally ~0 (attention key biases): fp residue only
         worst.append((_cos(a, b), n))
     worst.sort()
+    print(f"\n[b16 {variant} hard={hard}] logits rel {rel_err(logits.detach().cpu(), ref.detach()):.3e} "
+          f"cos {_cos(logits.detach().cpu(), ref.detach()):.6f}; worst grad cos {worst[:4]}")
     assert len(worst) > 150
-    assert worst[0][0] >= 0.99, worst[:5]
+    assert worst[0][0] >= 0.997, worst[:5]
+
+
+def _kernel_names(fn):
+    """the set of GPU kernel names one call of fn launches (torch.profiler's ROCm tracer sees every
+    kernel of the process, the ctypes library's included)"""
+    from torch.profiler import ProfilerActivity, profile
+    torch.cuda.synchronize()
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        fn()
+        torch.cuda.synchronize()
+    return {e.name for e in prof.events() if e.device_type == torch.autograd.DeviceType.CUDA}
+
+
+def _prod_kernels(names):
+    # the BERT-stack production kernels: GEMMs, attention, LayerNorm (the batch-row fp32 decoder /
+    # head GEMMs pick their tile by M = B and are not the routes in question)
+    return {n for n in names if any(k in n for k in ("gemm8", "gemm4", "attn", "ln_fwd", "ln_bwd", "splitk",
+                                                       "colsum", "adam"))}
+
+
+def test_b16_takes_the_bench_routes():
+    """the B = 16 parity tests stand for the B = 256 bench only if they reach the
+    same kernels.  One PriGumbelTrainer step (bf16, dropout 0.1) at B = 16 and at B = 256: every
+    production kernel the B = 256 step launches is launched at B = 16 too."""
+    from eegfusion.modules import PriGumbelModel
+    from eegfusion.trainer import PriGumbelTrainer
+    torch.manual_seed(4)
+    m = PriGumbelModel(1.0, contract="W", dropout=0.1).cuda().set_compute_dtype(torch.bfloat16)
+    tr = PriGumbelTrainer(m.engine, lr=1e-6)
+    sets = {}
+    for B in (16, 256):
+        g = torch.Generator(device=DEV).manual_seed(B)
+        batch = {"eeg": torch.randn(B, 64, 256, generator=g, device=DEV),
+                 "act": torch.randn(B, 32, generator=g, device=DEV) * 0.5}
+        labels = (torch.rand(B, generator=g, device=DEV) < 0.66).long()
+        tr.step(batch, labels)                           # warm (workspaces sized)
+        sets[B] = _kernel_names(lambda: tr.step(batch, labels))
+    big, small = _prod_kernels(sets[256]), _prod_kernels(sets[16])
+    print("\n[routes] B=256 production kernels:", len(big), "B=16:", len(small))
+    for n in sorted(big):
+        print("   ", "ok " if n in small else "MISSING", n[:160])
+    for n in sorted(small - big):
+        print("    B16-only", n[:160])
+    assert len(big) >= 8, sorted(big)
+    assert big <= small, sorted(big - small)
 
 
 def _run(m, eeg, act, labels, hard, rng0):
@@ -108,8 +158,10 @@ def test_full_size_bf16_vs_fp32_engine(B):
     m.set_compute_dtype(torch.float32)
     lf, gf, ff = _run(m, eeg, act, labels, True, 1 << 20)
     assert fb and ff and torch.isfinite(lb).all() and torch.isfinite(lf).all()
-    assert _cos(lb, lf) >= 0.99
-    bad = [(n, _cos(gb[n], gf[n])) for n in gb if _cos(gb[n], gf[n]) < 0.99]
+    cos = sorted((_cos(gb[n], gf[n]), n) for n in gb)
+    print(f"\n[B={B}] logits cos {_cos(lb, lf):.6f}; worst grad cos {cos[:4]}")
+    assert _cos(lb, lf) >= 0.9999
+    bad = [(n, _cos(gb[n], gf[n])) for n in gb if _cos(gb[n], gf[n]) < 0.996]
     assert not bad, bad[:5]
 
 

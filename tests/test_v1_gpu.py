@@ -67,9 +67,9 @@ def test_v1_trainer_fused_loss(ci):
     orig_step = tr.opt.step
     grads = {}
 
-    def capture():
+    def capture(grad_scale=1.0):
         grads.update({n: eng.G(n).detach().clone() for n in ("w", "fc1.weight", "fc2.bias", "classifier.weight")})
-        orig_step()
+        orig_step(grad_scale)
 
     tr.opt.step = capture
     loss, _ = tr.step(batch, torch.from_numpy(f["labels"]).to(DEV), training=not c["hard"])
