@@ -6,8 +6,9 @@ The module tree reproduces the reference's attribute names and state_dict keys e
 `fc_layers.{0,2}.*`, `classifier.*`, `DP`), so `load_state_dict` of a reference checkpoint works and
 callers that touch `.bert.encoder.layer[-1]`, `.fc_layers`, `.classifier`, `.DP`, `.eps`
 (train.py:139, main_0430.py:144-151) keep working.  The submodules are parameter holders only:
-every parameter is a view into the engine's ParamArena and every FLOP runs in libeegfusion.so.
-There is no CPU compute path: forward on CPU tensors raises.
+every parameter is a view into the engine's ParamArena and, for a model on the GPU, every FLOP runs
+in libeegfusion.so.  A model left in host memory (configs[0]'s no-GPU plumbing run) computes with
+plain torch ops (eegfusion/cpu_path.py, the "ti" models); a device model never falls back to it.
 """
 from __future__ import annotations
 
@@ -245,7 +246,20 @@ class FusionModel(nn.Module):
             if t is not None and not t.is_cuda:
                 raise RuntimeError("eegfusion: inputs must be device tensors (no CPU path)")
 
+    def _host(self, *ts) -> bool:
+        """True when the model lives in host memory (cpu_path); mixed host/device operands raise"""
+        if self._arena.device.type != "cpu":
+            return False
+        if any(t is not None and t.is_cuda for t in ts):
+            raise RuntimeError("eegfusion: the model is in host memory but the inputs are device tensors; "
+                               "call model.cuda()")
+        return True
+
     def _run(self, batch: dict, hard: bool) -> torch.Tensor:
+        if self._host(*batch.values()):
+            from .cpu_path import forward as host_forward
+            self._engine.cfg.eps = float(self.eps)
+            return host_forward(self, batch, bool(hard))
         self._check_device(*batch.values())
         self._engine.cfg.eps = float(self.eps)
         params = [p for p in self.parameters() if p.requires_grad]
@@ -319,6 +333,10 @@ class ConcatModel(FusionModel):
     def feature(self, x):
         frame_input, vedio_mask, title_input, text_mask = x
         batch = self._token_batch(frame_input, vedio_mask, title_input, text_mask)
+        if self._host(*batch.values()):
+            from .cpu_path import forward as host_forward
+            with torch.no_grad():
+                return host_forward(self, batch, True, return_feature=True)[2]
         self._check_device(*batch.values())
         with torch.no_grad():
             _, sv = self._engine.forward(batch, True, self.training, save=False)
@@ -370,6 +388,21 @@ class TICA_LapDropout(FusionModel):
     def forward(self, eeg_txt_input, eeg_txt_mask, act_img_input, act_img_mask, epsilon, hard):
         self.eps = torch.tensor(float(epsilon))
         return self._run(self._token_batch(act_img_input, act_img_mask, eeg_txt_input, eeg_txt_mask), hard)
+
+
+class TICA_NonPrivate(FusionModel):
+    """python/src/custom_models/models.py:309-352 — TICA_NonPrivate(bert_coef); forward(eeg_txt_input,
+    eeg_txt_mask, act_img_input, act_img_mask): the TICA encoders, concat + min-max, fc head, no privacy
+    stage and no DP parameter (model.py's ConcatModel computation under the TICA signature; base_train's
+    'NDP' baseline)."""
+
+    def __init__(self, bert_coef: str = "bert-base-uncased", contract: str = "T", **kw):
+        super().__init__("concat", contract=contract, with_dp=False, **kw)
+        if bert_coef and os.path.exists(str(bert_coef)):
+            load_bert_weights(self, bert_coef)
+
+    def forward(self, eeg_txt_input, eeg_txt_mask, act_img_input, act_img_mask):
+        return self._run(self._token_batch(act_img_input, act_img_mask, eeg_txt_input, eeg_txt_mask), True)
 
 
 def _tokens(x):

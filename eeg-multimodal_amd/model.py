@@ -4,7 +4,8 @@
 x = (frame_input [B,1,512] f32, vedio_mask [B,1], title_input [B,512] i64, text_mask [B,512] i64)
 and returns logits [B,2].  `BertModel.from_pretrained('bert-base-uncased')` cannot run offline:
 BERT starts from the BERT initialiser (normal(0, 0.02)); set EEGF_BERT_WEIGHTS to a local
-safetensors file / HF directory to load pretrained weights.
+safetensors file / HF directory to load pretrained weights.  On a machine without a GPU the model
+stays in host memory and runs the torch-op host path (eegfusion/cpu_path.py).
 """
 import os
 
@@ -15,11 +16,14 @@ from eegfusion.modules import load_bert_weights
 
 
 def get_model(cfg):
-    """model.py:8-12"""
+    """model.py:8-12.  The reference moves the model to CUDA unconditionally; here it goes to the GPU
+    when one is present and stays in host memory otherwise (configs[0]'s no-GPU plumbing run,
+    SURVEY §8(f)#1), where it computes with torch ops (eegfusion/cpu_path.py)."""
     if cfg.data_name == 'EEG':
         model = ConcatModel()
-    model.eps = torch.tensor(cfg.eps).cuda()
-    return model.cuda()
+    dev = torch.device("cuda" if torch.cuda.is_available() else "cpu")
+    model.eps = torch.tensor(cfg.eps).to(dev)
+    return model.to(dev)
 
 
 class ConcatModel(_ConcatModel):

@@ -5,7 +5,8 @@ checkpoint (model.pth) and the per-epoch results file (results.pth).
 
 Differences, all forced by the image: torchmetrics is absent, so the metrics come from
 eegfusion.metrics (on-device restatements of its multiclass defaults); results.pth is read back
-with torch.load(weights_only=True).  The model runs on the MI355X engine only (no CPU path).
+with torch.load(weights_only=True).  `.cuda()` becomes `.to(DEVICE)`: the MI355X engine when a GPU is
+present, else the host path (configs[0], "CPU PyTorch via train.py").
 The reference's quirks are kept: labels are collected in a separate shuffled pass over the
 validation loader (train.py:83-86) and evaluation re-shuffles (train.py:122-136).
 """
@@ -51,8 +52,12 @@ def parse_args(argv=None):
     return parser.parse_args(argv)
 
 
+DEVICE = torch.device("cuda" if torch.cuda.is_available() else "cpu")   # the reference's .cuda(); host
+# memory where no GPU exists (configs[0]'s plumbing run: model.get_model keeps the model there too)
+
+
 def _to_cuda(inputs):
-    return list(i.cuda() for i in inputs) if isinstance(inputs, (list, tuple)) else inputs.cuda()
+    return list(i.to(DEVICE) for i in inputs) if isinstance(inputs, (list, tuple)) else inputs.to(DEVICE)
 
 
 def main(cfg):
@@ -76,18 +81,18 @@ def main(cfg):
     unknown = [m for m in cfg.metrics.split(',') if m not in METRICS]
     if unknown:
         raise ValueError(f"unsupported metrics {unknown}; available: {sorted(METRICS)}")
-    metrics = {i: METRICS[i](task="multiclass", num_classes=cfg.n_class).cuda() for i in cfg.metrics.split(',')}
+    metrics = {i: METRICS[i](task="multiclass", num_classes=cfg.n_class).to(DEVICE) for i in cfg.metrics.split(',')}
     best_acc = 0.0
 
     for inputs, labels in val_loader:
-        results['labels'].append(labels.cuda().view(-1))
+        results['labels'].append(labels.to(DEVICE).view(-1))
     results['labels'] = torch.cat(results['labels'])
 
     for epoch in range(cfg.n_epochs):
         model.train()
         for i, (inputs, labels) in enumerate(train_loader):
             inputs = _to_cuda(inputs)
-            labels = labels.view(-1).cuda()
+            labels = labels.view(-1).to(DEVICE)
             model_optimizer.zero_grad()
             for _ in range(cfg.n_para):
                 loss = criterion(model(inputs, hard=True), labels)
@@ -103,7 +108,7 @@ def main(cfg):
             with torch.no_grad():
                 for inputs, labels in val_loader:
                     inputs = _to_cuda(inputs)
-                    labels = labels.view(-1).cuda()
+                    labels = labels.view(-1).to(DEVICE)
                     for _ in range(cfg.n_eval):
                         logits = model(inputs, hard=True)
                         eval_metrics['logits'].append(logits)

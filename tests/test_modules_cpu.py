@@ -67,11 +67,14 @@ def test_load_state_dict_keeps_arena_binding():
     assert m.classifier.weight.data_ptr() == m.arena.view("classifier.weight").data_ptr()
 
 
-def test_no_cpu_compute_path():
-    from eegfusion.modules import PriGumbelModel
-    m = PriGumbelModel(1.0, contract="W")
-    with pytest.raises(RuntimeError, match="GPU"):
-        m.forward_window(torch.zeros(1, 64, 256), torch.zeros(1, 32), True)
+def test_host_path_scope():
+    """the host path (configs[0] plumbing) covers the "ti" models only; the other pairings and DP-SGD
+    say they need the GPU instead of computing something else"""
+    from eegfusion.modules import TTCA_LapDropout
+    m = TTCA_LapDropout("bert-base-uncased")
+    ids = torch.ones(1, 8, dtype=torch.long)
+    with pytest.raises(NotImplementedError, match="GPU"):
+        m(ids, ids, ids, ids, 1.0, True)
 
 
 def test_half_conversion_refused():
