@@ -184,8 +184,11 @@ __global__ void __launch_bounds__(512) attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float v = s[f][r] * a.scale;
-        if (kb) v += kb[k0 + 16 * f + 4 * g + r];
-        if (VL && k0 + 16 * f + 4 * g + r >= len) v = NEG;           // keys past the sequence
+        const int key = k0 + 16 * f + 4 * g + r;
+        // the key-bias row holds a.L entries: keys past the sequence are never read (a ragged or
+        // uniform length below the 64-key block would read the next row / past the buffer)
+        if (kb && (!VL || key < len)) v += kb[key];
+        if (VL && key >= len) v = NEG;                                   // keys past the sequence
         s[f][r] = v;
         tmax = fmaxf(tmax, v);
       }
@@ -281,8 +284,10 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(AttnArgs a) {
   float kbv[2];
 #pragma unroll
   for (int f = 0; f < 2; ++f) {
-    kbv[f] = kbias ? kbias[kw0 + 16 * f + li] : 0.f;
-    if (VL && kw0 + 16 * f + li >= len) kbv[f] = NEG;              // keys past the sequence: p = 0
+    // keys past the sequence: p = 0, and their bias is never read (the 256-key block of a uniform
+    // launch with L < 256 would read the next row's bias / past the end of the buffer)
+    const int key = kw0 + 16 * f + li;
+    kbv[f] = (VL && key >= len) ? NEG : (kbias ? kbias[key] : 0.f);
   }
 
   f32x4 dk[2][4], dv[2][4];
