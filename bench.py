@@ -70,8 +70,12 @@ def parse_args(argv=None):
     ap.add_argument("--eps-mode", default="newfrac", choices=["newfrac", "new"])
     ap.add_argument("--feawei", type=int, default=0, help="feawei feature pass over this many synthetic samples")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-batch", type=int, default=256, help="CPU-baseline batch (BASELINE.md §3: 256)")
-    ap.add_argument("--cpu-iters", type=int, default=1, help="CPU-baseline timed iterations after one warm-up")
+    ap.add_argument("--cpu-batch", type=int, default=16,
+                    help="CPU-baseline batch of the live sample (bounded: ~10-30 s of CPU work)")
+    ap.add_argument("--cpu-iters", type=int, default=2, help="CPU-baseline timed iterations after one warm-up")
+    ap.add_argument("--cpu-baseline-only", action="store_true",
+                    help="time only the CPU baseline (e.g. --cpu-batch 256 --cpu-iters 3, BASELINE.md §3) and print "
+                         "its JSON; profiles/" + "cpu_baseline_b256.json holds that run for the bench line")
     ap.add_argument("--master-port", type=int, default=29531)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N > 1: nccl (= RCCL, one GPU per rank) or gloo (device "
@@ -110,6 +114,9 @@ def cpu_model() -> str:
 
 
 def cpu_baseline(variant: str, batch: int, iters: int) -> dict:
+    def progress(msg):
+        print(f"[bench cpu_baseline] {msg}", file=sys.stderr, flush=True)
+
     """The CPU oracle (torch fp32 restatement, oracle/fusion_oracle.py; pinned against the reference's
     own outputs by tests/test_oracle_golden.py) timed on the host cores on a bounded sample of the
     same iteration: the bench's batch (256), dropout 0.1 at every reference site as on the GPU leg,
@@ -171,12 +178,14 @@ def cpu_baseline(variant: str, batch: int, iters: int) -> dict:
             mopt.step()
 
     try:
+        progress(f"{variant} batch {batch}, {threads} threads: warm-up")
         t0 = time.perf_counter()
         iteration()                                    # warm-up (allocations, thread pool)
         warm = time.perf_counter() - t0
         t0 = time.perf_counter()
-        for _ in range(iters):
+        for i in range(iters):
             iteration()
+            progress(f"iteration {i + 1}/{iters}: {time.perf_counter() - t0:.1f} s")
         dt = time.perf_counter() - t0
     finally:
         O.set_dropout_replay(None)
@@ -223,6 +232,9 @@ def main():
 
     sys.path.insert(0, str(ROOT / "eeg-multimodal_amd"))
     sys.path.insert(0, str(ROOT))
+    if args.cpu_baseline_only:
+        print(json.dumps(cpu_baseline(args.variant, args.cpu_batch, args.cpu_iters)), flush=True)
+        return
     import torch
     import torch.distributed as dist
 
@@ -400,7 +412,13 @@ def main():
         if replicas is not None:
             out["replicas"] = replicas
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.variant, args.cpu_batch, args.cpu_iters)
+            cb = cpu_baseline(args.variant, args.cpu_batch, args.cpu_iters)
+            # the BASELINE.md §3 sample (batch 256, 1 warm-up + 3 timed) measured on a GPU box's host by
+            # `bench.py --cpu-baseline-only --cpu-batch 256 --cpu-iters 3`: too long for the default run
+            ref = load_profile_json("cpu_baseline_b256.json", args.variant)
+            if ref:
+                cb["batch256_measured"] = ref
+            out["cpu_baseline"] = cb
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
