@@ -9,7 +9,10 @@
  *   - all pointers are caller-owned device pointers (row-major, contiguous unless a leading
  *     dimension / stride argument says otherwise); sizes are in elements;
  *   - no allocation, no host synchronisation, no global state: a caller may capture any sequence
- *     of calls into a hipGraph;
+ *     of calls into a hipGraph.  Two diagnostics are the exception, declared as such below and used
+ *     by tests / benchmarks only: eegf_tune (process-global kernel-routing keys, A/B switches with
+ *     production defaults; set them before launching, not concurrently with launches on other
+ *     threads) and eegf_gemm_big_timestamps (a process-global stamp buffer, off by default);
  *   - work is enqueued on `stream`;
  *   - returns 0 on success, EEGF_ERR_ARG (<0) on an argument error (nothing launched), or the
  *     hipError_t of the launch; never throws.
@@ -71,7 +74,12 @@ int eegf_gemm(int dtype, int out_dtype, int a_kcontig, int b_kcontig, int epi,
  *   key 9: tile raster of the 256-row GEMMs: -1 (default) groups of 4 row panels when N >= 2048,
  *          row-major otherwise; 0 row-major; G > 0 groups of G row panels walked column by column;
  *   key 10: bf16 768-wide rows of eegf_ln_fwd on the 16-B-access kernel (1, default) or the generic
- *          4-columns-per-lane kernel (0). */
+ *          4-columns-per-lane kernel (0);
+ *   key 11: the persistent 256x256 bf16 GEMM (one workgroup per CU over the tiles, the next tile's
+ *          operands staged under the current epilogue) for full-tile bf16-output GEMMs with epilogue
+ *          NONE (beta 0) / BIAS / BIAS_GELU / BIAS_GELU_D / MUL_AUX: 0 off, 1 every such GEMM,
+ *          2 K < 2048 only.
+ * Process-global (see the contract above): test / benchmark state, not for production callers. */
 int eegf_tune(int key, int value);
 /* Diagnostics (no reference counterpart): every following 256-row GEMM launch of the 8-wave / 4-wave
  * kernels writes 4 s_memrealtime stamps per workgroup (start, prologue done, K-loop done, epilogue
