@@ -45,7 +45,7 @@ METRIC = "samples/sec at batch 256, 64ch×256 EEG + 32-d action, 1/2/4/8 GPUs"
 PMC_FILE = "pmc_r2am.json"          # profiles/: tools/pmc_table.py output (HBM bytes, MFMA busy per group)
 # probed kernel groups (HIP events around each launch on the launch stream, engine.probe)
 KERNEL_GROUPS = {
-    "ffn1_fwd": "BertIntermediate GEMM + bias + GELU (+GELU' saved in pass 2), 65536x3072x768",
+    "ffn1_fwd": "BertIntermediate GEMM + bias + GELU (+GELU' saved in pass 2), 65536x3072x768 (persistent kernel)",
     "qkv_fwd": "fused Q|K|V projection GEMM + bias, 65536x2304x768",
     "ffn2_fwd": "BertOutput GEMM + bias, 65536x768x3072",
     "attn_fwd": "fused self-attention forward (QK^T, softmax, dropout, PV), 256x12 heads x 256^2 x 64",

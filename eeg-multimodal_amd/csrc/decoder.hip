@@ -95,14 +95,17 @@ __global__ void __launch_bounds__(256) xrow_dot_kernel(const T* __restrict__ mem
 // A = memory rows straight from global (16 B per lane, 64 B row segments), B = v_hi / v_lo from LDS
 // (heads padded 12 -> 16 with zeros).
 constexpr int XR = 4;       // 64-row blocks per xrow_dot_mfma workgroup
+constexpr int XW = 8;       // waves per xrow_dot_mfma workgroup (16-row blocks w, w + 8, ...): one
+                            // workgroup per batch row at S = 256, so the CU's memory parallelism is
+                            // its waves' loads in flight -- 4 waves held ~2.2 TB/s (profiles/r2am)
 template <typename TV>
-__global__ void __launch_bounds__(256) xrow_dot_mfma_kernel(const bf16* __restrict__ mem, const TV* __restrict__ vec,
+__global__ void __launch_bounds__(64 * XW) xrow_dot_mfma_kernel(const bf16* __restrict__ mem, const TV* __restrict__ vec,
                                                             const float* __restrict__ kbias, int S,
                                                             float* __restrict__ out) {
   constexpr int LDV = E + 8;
   __shared__ __attribute__((aligned(16))) bf16 vt[2][16 * LDV];
   const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, li = lane & 15;
-  for (int i = tid; i < 16 * E; i += 256) {
+  for (int i = tid; i < 16 * E; i += 64 * XW) {
     const int h = i / E, c = i % E;
     const float x = h < NH ? to_f32(vec[((long)b * NH + h) * E + c]) : 0.f;
     const bf16 hi = (bf16)x;
@@ -113,11 +116,11 @@ __global__ void __launch_bounds__(256) xrow_dot_mfma_kernel(const bf16* __restri
   const bf16* vh = vt[0] + li * LDV + 8 * g;
   const bf16* vl = vt[1] + li * LDV + 8 * g;
   // the workgroup covers XR row blocks of 64 (amortises the v staging): wave w takes 16-row blocks
-  // w, w + 4, ...
-  for (int j0 = blockIdx.x * 64 * XR + wave * 16; j0 < min(S, (int)(blockIdx.x + 1) * 64 * XR); j0 += 64) {
+  // w, w + XW, ...; the whole 768-wide row segment's 24 loads are issued before the first MFMA
+  for (int j0 = blockIdx.x * 64 * XR + wave * 16; j0 < min(S, (int)(blockIdx.x + 1) * 64 * XR); j0 += 16 * XW) {
     const bf16* row = mem + ((long)b * S + min(j0 + li, S - 1)) * E + 8 * g;
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 8
+#pragma unroll
     for (int kc = 0; kc < E / 32; ++kc) {
       const bf16x8 a = *(const bf16x8*)(row + 32 * kc);
       acc = mma16(a, *(const bf16x8*)(vh + 32 * kc), acc);
@@ -136,7 +139,7 @@ __global__ void __launch_bounds__(256) xrow_dot_mfma_kernel(const bf16* __restri
 template <typename T, typename TV>
 void launch_xrow_dot(const T* mem, const TV* vec, const float* kbias, int B, int S, float* out, hipStream_t st) {
   if constexpr (sizeof(T) == 2)
-    hipLaunchKernelGGL((xrow_dot_mfma_kernel<TV>), dim3((S + 64 * XR - 1) / (64 * XR), B), dim3(256), 0, st, mem, vec,
+    hipLaunchKernelGGL((xrow_dot_mfma_kernel<TV>), dim3((S + 64 * XR - 1) / (64 * XR), B), dim3(64 * XW), 0, st, mem, vec,
                        kbias, S, out);
   else
     hipLaunchKernelGGL((xrow_dot_kernel<T, TV>), dim3((S + 63) / 64, B), dim3(256), 0, st, mem, vec, kbias, S, out);

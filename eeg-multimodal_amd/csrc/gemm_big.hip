@@ -934,6 +934,242 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Persistent 4-wave 256x256 bf16-output kernel: gemm4w's K-loop, one workgroup per CU looping over
+// output tiles, with the next tile's first NSLOT4 K-tiles staged into the (then idle) LDS ring BEFORE
+// the current tile's epilogue.  The non-persistent kernel pays, per tile, the HBM latency of its
+// prologue and an epilogue during which the CU's MFMAs and loads idle (one workgroup per CU: the
+// ring fills all of LDS); here the epilogue (bias / GELU / GELU' VALU and the output stores) runs
+// under the next tile's operand fetch.  The epilogue is therefore written straight from the
+// accumulators (8-B stores: every 128-B output line is filled by consecutive stores of one wave, so
+// L2 merges them) and its inputs (bias, aux / C tiles) are read by asm loads issued before the
+// prefetch, retired by one counted vmcnt: a compiler-visible load would make hipcc's waitcnt pass
+// (blind to the asm LDS-DMA) wait for the prefetch too.  Full tiles only (M, N % 256 == 0).
+// Tile order: round r of workgroup b takes logical tile r * grid + xcd_remap(b): each round an XCD
+// runs a contiguous block of logical tiles, which tile_coords' grouped raster keeps on few A panels.
+// the lane's 8 bias quads (columns n, n + 16, ... n + 112) in ONE asm statement that also retires them:
+// the outputs exist only once the statement completes, so hipcc can neither read nor move them early
+// (a compiler-visible load would instead make hipcc's waitcnt pass, blind to the asm LDS-DMA, wait for
+// the next tile's prefetch at the first use)
+DEV void load_bias8(f32x4 (&b)[8], const float* p) {
+  asm volatile(
+      "global_load_dwordx4 %0, %8, off\n\tglobal_load_dwordx4 %1, %8, off offset:64\n\t"
+      "global_load_dwordx4 %2, %8, off offset:128\n\tglobal_load_dwordx4 %3, %8, off offset:192\n\t"
+      "global_load_dwordx4 %4, %8, off offset:256\n\tglobal_load_dwordx4 %5, %8, off offset:320\n\t"
+      "global_load_dwordx4 %6, %8, off offset:384\n\tglobal_load_dwordx4 %7, %8, off offset:448\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=&v"(b[0]), "=&v"(b[1]), "=&v"(b[2]), "=&v"(b[3]), "=&v"(b[4]), "=&v"(b[5]), "=&v"(b[6]), "=&v"(b[7])
+      : "v"(p)
+      : "memory");
+}
+
+template <bool BKC, int EPI>
+__global__ void __launch_bounds__(NT4, 1) gemm4p_kernel(BigArgs g) {
+  constexpr bool AKC = true;
+  constexpr int LDS4 = NSLOT4 * SLOT4;
+  constexpr bool HAS_BIAS = EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_D;
+  // an aux INPUT tile (EPI_MUL_AUX) or beta * C is not taken: 128 registers of loads would have to be
+  // retired under the prefetch by a counted wait hipcc cannot see (a first version read them through
+  // separate asm loads and got wrong results: hipcc moved the registers before the wait)
+  __shared__ __attribute__((aligned(16))) bf16 lds[LDS4];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int tiles_n = g.N / TN, tiles_m = g.M / TM, ntiles = tiles_m * tiles_n;
+  const int G = gridDim.x;
+  const int nk = g.K / BK4;
+  int L = xcd_remap(blockIdx.x, G);
+  if (L >= ntiles) return;
+
+  // per-lane staging offsets (full tiles: no row / column clamp, so one set serves every tile)
+  uint32_t voffA[4], voffB[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int r = (wave * 4 + j) * 16 + (lane >> 2);
+    voffA[j] = (uint32_t)(((long)r * g.lda + ((lane & 3) ^ sw4(r)) * 8) * 2);
+    if (BKC) {
+      voffB[j] = (uint32_t)(((long)r * g.ldb + ((lane & 3) ^ sw4(r)) * 8) * 2);
+    } else {
+      const int k = (wave * 4 + j) * 2 + (lane >> 5);
+      voffB[j] = (uint32_t)(((long)k * g.ldb + ((lane & 31) ^ swz_k(k)) * 8) * 2);
+    }
+  }
+  const long stepB = BKC ? BK4 : (long)BK4 * g.ldb;
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr_of(lds));
+  auto stage_part = [&](const bf16* bA, const bf16* bB, int slot, int j) {
+    const bool kc = j < 4 ? AKC : BKC;
+    const uint32_t dst = lds0 + 2u * (slot * SLOT4 + (j < 4 ? 0 : TM * BK4) +
+                                      (wave * 4 + (j & 3)) * (kc ? 16 * BK4 : 2 * TN));
+    if (j < 4) glds16_asm_sa(bA, voffA[j & 3], dst);
+    else glds16_asm_sa(bB, voffB[j & 3], dst);
+  };
+  auto tile_base = [&](int l, const bf16*& bA, const bf16*& bB, int& m0, int& n0) {
+    int tm, tn;
+    tile_coords(g, l, tiles_m, tiles_n, tm, tn);
+    m0 = __builtin_amdgcn_readfirstlane(tm * TM);
+    n0 = __builtin_amdgcn_readfirstlane(tn * TN);
+    bA = g.A + (long)m0 * g.lda;
+    bB = BKC ? g.B + (long)n0 * g.ldb : g.B + n0;
+  };
+  auto stage_first = [&](const bf16* bA, const bf16* bB) {   // K-tiles 0 .. NSLOT4-1 -> slots 0 .. 4
+    for (int kt = 0; kt < NSLOT4; ++kt)
+      if (kt < nk)
+        for (int j = 0; j < 8; ++j) stage_part(bA + kt * BK4, bB + kt * stepB, kt, j);
+  };
+  const int fr = lane & 15, fq = lane >> 4;
+  const int offA = (wm * 128 + fr) * BK4 + ((fq ^ sw4(fr)) << 3);
+  const int offB = TM * BK4 + (wn * 128 + fr) * BK4 + ((fq ^ sw4(fr)) << 3);
+  int tB0[8], tB1[8];
+  if (!BKC) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int q = fr >> 2, p4 = fr & 3;
+      const int col = wn * 128 + 16 * i + 4 * p4, ch = col >> 3, off = col & 7;
+      const int ka = 8 * fq + q, kb = ka + 4;
+      tB0[i] = TM * BK4 + ka * TN + (((ch ^ swz_k(ka)) << 3) | off);
+      tB1[i] = TM * BK4 + kb * TN + (((ch ^ swz_k(kb)) << 3) | off);
+    }
+  }
+  auto rdA = [&](const bf16* img, int i) { return *(const bf16x8*)(img + offA + i * 16 * BK4); };
+  auto rdB = [&](const bf16* img, int i) {
+    return BKC ? *(const bf16x8*)(img + offB + i * 16 * BK4) : rd_col_off(img, tB0[i], tB1[i]);
+  };
+
+  const bf16* baseA;
+  const bf16* baseB;
+  int m0, n0;
+  tile_base(L, baseA, baseB, m0, n0);
+  stage_first(baseA, baseB);
+  f32x4 acc[8][8];
+  for (;;) {
+    // K-tiles 0 and 1 retired (older epilogue stores still counted only make this wait stricter)
+    vm_wait_tiles(max(0, min(nk, NSLOT4) - 2));
+    raw_barrier();
+    bf16x8 fa[2][8], fb[2][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      fa[0][i] = rdA(lds, i);
+      fb[0][i] = rdB(lds, i);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    raw_barrier();
+
+    auto ktile = [&](auto Hc, int k, int slot, int nslot, auto Ic, auto Tc) __attribute__((always_inline)) {
+      constexpr int H = decltype(Hc)::value;
+      constexpr bool INIT = decltype(Ic)::value, TAIL = decltype(Tc)::value;
+      const bool more = !TAIL || k + 1 < nk, st = !TAIL || k + NSLOT4 < nk;
+      const bf16* nimg = lds + nslot * SLOT4;
+      const bf16* sA = baseA + (k + NSLOT4) * BK4;
+      const bf16* sB = baseB + (k + NSLOT4) * stepB;
+      auto mma = [&](int s, int jj) {
+        if (INIT) mma16_acc0(acc[s][jj], fb[H][jj], fa[H][s]);
+        else mma16_acc(acc[s][jj], fb[H][jj], fa[H][s]);
+      };
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        mma(s, 0);
+        if (more) fa[H ^ 1][s] = rdA(nimg, s);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(s, 1);
+        if (more) fb[H ^ 1][s] = rdB(nimg, s);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(s, 2);
+        if (st) stage_part(sA, sB, slot, s);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(s, 3);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(s, 4);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(s, 5);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(s, 6);
+        mma(s, 7);
+      }
+      if (!TAIL) vm_wait_tiles(NSLOT4 - 2);
+      else vm_wait_tiles(max(0, min(nk - 1, k + NSLOT4) - (k + 2)));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      raw_barrier();
+    };
+    using C0 = std::integral_constant<int, 0>;
+    using C1 = std::integral_constant<int, 1>;
+    using F = std::false_type;
+    using T = std::true_type;
+    auto nxt = [](int sl) { return sl == NSLOT4 - 1 ? 0 : sl + 1; };
+    int slot = 0;
+    if (nk > NSLOT4) ktile(C0{}, 0, slot, nxt(slot), T{}, F{});
+    else ktile(C0{}, 0, slot, nxt(slot), T{}, T{});
+    slot = nxt(slot);
+    int kt = 1;
+    for (; kt + 1 + NSLOT4 < nk; kt += 2) {
+      ktile(C1{}, kt, slot, nxt(slot), F{}, F{});
+      slot = nxt(slot);
+      ktile(C0{}, kt + 1, slot, nxt(slot), F{}, F{});
+      slot = nxt(slot);
+    }
+    for (; kt < nk; kt += 2) {
+      ktile(C1{}, kt, slot, nxt(slot), F{}, T{});
+      slot = nxt(slot);
+      if (kt + 1 < nk) {
+        ktile(C0{}, kt + 1, slot, nxt(slot), F{}, T{});
+        slot = nxt(slot);
+      }
+    }
+    // every wave is past its last ring read (the final K-tile's barrier): the ring is free
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+
+    // the bias (8 quads, L2-resident) before the prefetch, retired at once
+    const int mrow = m0 + wm * 128 + (lane & 15);
+    const int ncol = n0 + wn * 128 + 4 * (lane >> 4);
+    f32x4 biasv[8];
+    if (HAS_BIAS) load_bias8(biasv, g.bias + ncol);
+    const int Ln = L + G;
+    const bool more_tiles = Ln < ntiles;
+    int m0n = 0, n0n = 0;
+    const bf16* nA = nullptr;
+    const bf16* nB = nullptr;
+    if (more_tiles) {
+      tile_base(Ln, nA, nB, m0n, n0n);
+      stage_first(nA, nB);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+
+    bf16* Cb = (bf16*)g.C;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const long m = mrow + 16 * i;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int n = ncol + 16 * j;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = g.alpha * acc[i][j][r] + (HAS_BIAS ? biasv[j][r] : 0.f);
+        bf16x4 o, o2;
+        if (EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_D) {
+          f32x2 gl0, gl1, gd0, gd1;
+          gelu2(f32x2{v[0], v[1]}, gl0, EPI == EPI_BIAS_GELU_D ? &gd0 : nullptr);
+          gelu2(f32x2{v[2], v[3]}, gl1, EPI == EPI_BIAS_GELU_D ? &gd1 : nullptr);
+          if (EPI == EPI_BIAS_GELU_D) {
+            o2[0] = (bf16)gd0.x; o2[1] = (bf16)gd0.y; o2[2] = (bf16)gd1.x; o2[3] = (bf16)gd1.y;
+          } else {
+            o2[0] = (bf16)v[0]; o2[1] = (bf16)v[1]; o2[2] = (bf16)v[2]; o2[3] = (bf16)v[3];   // pre-activation
+          }
+          o[0] = (bf16)gl0.x; o[1] = (bf16)gl0.y; o[2] = (bf16)gl1.x; o[3] = (bf16)gl1.y;
+          if (EPI == EPI_BIAS_GELU_D || g.aux) *(bf16x4*)(g.aux + m * g.ldaux + n) = o2;
+        } else {
+          o[0] = (bf16)v[0]; o[1] = (bf16)v[1]; o[2] = (bf16)v[2]; o[3] = (bf16)v[3];
+        }
+        *(bf16x4*)(Cb + m * g.ldc + n) = o;
+      }
+    }
+    if (!more_tiles) break;
+    L = Ln;
+    m0 = m0n;
+    n0 = n0n;
+    baseA = nA;
+    baseB = nB;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // 4-wave 256x128 kernel for the K = 768 bf16-output GEMMs with heavy epilogues (QKV and FFN1
 // forward with bias / GELU / GELU', the out-projection, the input gradients with an activation
 // product): the same K-loop as gemm4w (asm LDS-DMA in the saddr form, next K-tile's fragments read
@@ -1100,9 +1336,33 @@ __global__ void __launch_bounds__(NT4, 2) gemm4h_kernel(BigArgs g) {
 }
 
 int g_gemm4h = [] { const char* e = getenv("EEGF_GEMM4H"); return e ? atoi(e) : 2; }();   // eegf_tune key 8
+// eegf_tune key 11: the persistent kernel (gemm4p_kernel) for the bf16-output GEMMs it takes: 0 off,
+// 1 every eligible shape, 2 the ones it won in the interleaved A/B (profiles/r3f_p_ab.log): the GELU /
+// GELU' forward GEMMs and the plain (EPI_NONE) input gradients; the bias-only forward GEMMs lost
+// (QKV 265 -> 293 us, out-projection 84 -> 91, FFN2 261 -> 273)
+int g_gemm4p = [] { const char* e = getenv("EEGF_GEMM4P"); return e ? atoi(e) : 2; }();   // step A/B: 67.00 -> 66.39 ms (r3g_step_ab.log)
+int cu_count() {
+  static const int cus = [] {
+    int dev = 0, n = 256;
+    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    return n > 0 ? n : 256;
+  }();
+  return cus;
+}
 template <bool AKC, bool BKC, int EPI, typename TO>
 int launch_big(const BigArgs& a, int splits, hipStream_t s) {
   const int tiles = ((a.M + TM - 1) / TM) * ((a.N + TN - 1) / TN);
+  if constexpr (AKC && sizeof(TO) == 2 && (EPI == EPI_NONE || EPI == EPI_BIAS || EPI == EPI_BIAS_GELU ||
+                                           EPI == EPI_BIAS_GELU_D)) {
+    const bool won = EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_D || (EPI == EPI_NONE && !BKC && a.K >= 2048);
+    const bool p_ok = g_gemm4p == 1 || (g_gemm4p == 2 && won);
+    if (p_ok && g_gemm8 < 0 && splits == 1 && !a.colsum_part && a.M % TM == 0 && a.N % TN == 0 && a.beta == 0.f &&
+        a.K % BK4 == 0 && (((uintptr_t)a.bias) & 15) == 0) {
+      hipLaunchKernelGGL((gemm4p_kernel<BKC, EPI>), dim3(tiles < cu_count() ? tiles : cu_count()), dim3(NT4), 0, s,
+                         a);
+      return (int)hipGetLastError();
+    }
+  }
   if (g_gemm8 < 0) {
     // default schedule (tools/gemm_bench.py --ab, profiles/r1s2_gemm_ab.log): the 8-phase lockstep
     // schedule with one vmcnt per K-tile for the input-gradient GEMMs (+10-25 %) and the forward
@@ -1332,6 +1592,7 @@ extern "C" int eegf_tune(int key, int value) {
   if (key == 9) { const int o = g_group_m; g_group_m = value; return o; }
   if (key == 7) { const int o = g_ln_bwd_rpb; if (value < 4 || value > 1024 || value % 4) return EEGF_ERR_ARG; g_ln_bwd_rpb = value; return o; }
   if (key == 10) { const int o = g_ln_fwd768; g_ln_fwd768 = value; return o; }
+  if (key == 11) { const int o = g_gemm4p; if (value < 0 || value > 2) return EEGF_ERR_ARG; g_gemm4p = value; return o; }
   if (key == 6) { const int o = g_ln_rpw; if (value < 1 || value > 64) return EEGF_ERR_ARG; g_ln_rpw = value; return o; }
   return EEGF_ERR_ARG;
 }

@@ -535,3 +535,81 @@ def test_gemm_4h_dgrad(epi, M, N, K):
     finally:
         _tune(8, old)
 
+
+
+# the persistent kernel (eegf_tune key 11): full tiles only; production-sized grids loop several rounds,
+# K below the ring depth (3 and 1 K-tiles) prefetches fewer K-tiles, a 24-tile grid runs one round
+P_SHAPES = [(65536, 2304, 768), (4096, 768, 768), (8192, 3072, 96), (2048, 1024, 32), (16384, 768, 3072)]
+
+
+@pytest.mark.parametrize("epi", ["bias", "bias_gelu", "bias_gelu_d", "gelu_noaux", "none"])
+@pytest.mark.parametrize("M,N,K", P_SHAPES)
+def test_gemm_persistent_fwd(epi, M, N, K):
+    """gemm4p_kernel (persistent, next tile's K-tiles staged under the epilogue, direct stores) on the
+    forward layout against a float64 reference, and bit for bit against the default routing (the same
+    MFMA K-order and the same epilogue arithmetic)."""
+    k = _k()
+    torch.manual_seed(26)
+    x = (torch.randn(M, K, device="cuda") * 0.3).to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda") * 0.3).to(torch.bfloat16)
+    b = torch.randn(N, device="cuda")
+    e = "bias_gelu" if epi == "gelu_noaux" else epi
+    outs = []
+    for key in (1, 0):
+        old = _tune(11, key)
+        try:
+            aux = torch.full((M, N), float("nan"), device="cuda", dtype=torch.bfloat16) \
+                if epi in ("bias_gelu", "bias_gelu_d") else None
+            out = k.linear(x, w, None if epi == "none" else b, epi=e, aux=aux)
+            torch.cuda.synchronize()
+            outs.append((out, aux))
+        finally:
+            _tune(11, old)
+    out, aux = outs[0]
+    ref, pre = _ref_epi(x.double() @ w.double().t(), e, None if epi == "none" else b, None, 1.0)
+    _check(out, ref, torch.bfloat16)
+    if aux is not None:
+        _check(aux, pre, torch.bfloat16)
+    if K >= 256:      # the default routing's kernels share the K order from here on (BK 32 / 64 alike)
+        assert torch.equal(out, outs[1][0])
+        if aux is not None:
+            assert torch.equal(aux, outs[1][1])
+
+
+@pytest.mark.parametrize("epi", ["none", "mul_aux"])
+@pytest.mark.parametrize("M,N,K", P_SHAPES)
+def test_gemm_persistent_dgrad(epi, M, N, K):
+    """gemm4p_kernel with a k-major B (input gradient); the aux product (mul_aux) is routed to the other
+    kernels under key 11 and must come out the same."""
+    k = _k()
+    torch.manual_seed(27)
+    dy = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(K, N, device="cuda") * 0.1).to(torch.bfloat16)
+    aux = torch.randn(M, N, device="cuda").to(torch.bfloat16) if epi != "none" else None
+    old = _tune(11, 1)
+    try:
+        out = k.linear_dgrad(dy, w, epi=epi, aux=aux)
+        torch.cuda.synchronize()
+    finally:
+        _tune(11, old)
+    ref, _ = _ref_epi(dy.double() @ w.double(), epi, None, aux, 1.0)
+    _check(out, ref, torch.bfloat16)
+
+
+def test_gemm_persistent_falls_back_on_ragged_shapes():
+    """N % 256 != 0 / beta != 0: key 11 leaves those shapes on the other kernels (same results)."""
+    k = _k()
+    torch.manual_seed(28)
+    M, N, K = 4352, 808, 768
+    x = (torch.randn(M, K, device="cuda") * 0.3).to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda") * 0.3).to(torch.bfloat16)
+    b = torch.randn(N, device="cuda")
+    outs = []
+    for key in (1, 0):
+        old = _tune(11, key)
+        try:
+            outs.append(k.linear(x, w, b, epi="bias"))
+            torch.cuda.synchronize()
+        finally:
+            _tune(11, old)
+    assert torch.equal(outs[0], outs[1])

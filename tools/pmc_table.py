@@ -12,7 +12,10 @@ GEMM shapes that share a kernel symbol stay apart.  Per group and per launch:
               over the 8 XCDs — MI355X_MICROARCH.md, cycle constants and DVFS notes)
   hbm_bytes = 2 x FETCH_SIZE x 1024 + WRITE_SIZE x 1024   (gfx950: FETCH_SIZE counts half the bytes of
               16-B-per-lane streaming reads — MI355X_MICROARCH.md §HBM)
-  clock_ghz = GRBM_GUI_ACTIVE / 8 / duration
+  clock_ghz = GRBM_GUI_ACTIVE / 8 / duration, per dispatch with both from the SAME pass (median over
+              dispatches), and only for kernels of >= 50 us: GRBM_GUI_ACTIVE counts the counter window,
+              which for short kernels is longer than the kernel (the r2 tables divided one pass's
+              counter by another pass's durations and printed impossible > 3 GHz rows)
 
 Writes profiles/<tag>_pmc_table.md and profiles/pmc_<tag>.json (read by bench.py: roofline traffic and
 mfma_busy of the named kernel groups).
@@ -28,10 +31,11 @@ N_SIMD = 1024
 
 # bench.py roofline groups -> kernel-name fragments (mangled or demangled) + grid filters
 GROUPS = {     # bf16 instantiations appear mangled in rocprofv3's CSV (DF16b), the others demangled
-    "ffn1_fwd": ("gemm8_kernelILb1ELb1ELi2EDF16bLb0E", "gemm8_kernelILb1ELb1ELi8EDF16bLb0E"),
+    "ffn1_fwd": ("gemm8_kernelILb1ELb1ELi2EDF16bLb0E", "gemm8_kernelILb1ELb1ELi8EDF16bLb0E",
+                 "gemm4p_kernelILb1ELi2E", "gemm4p_kernelILb1ELi8E", "gemm4p_kernel<true, 2>", "gemm4p_kernel<true, 8>"),
     "qkv_fwd": ("gemm8_kernelILb1ELb1ELi1EDF16bLb0E",),
     "ffn2_fwd": ("gemm4w_kernelILb1ELb1ELi1EDF16bLb0E",),
-    "dgrad_qkv_ffn1": ("gemm4w_kernelILb1ELb0ELi0EDF16bLb0E",),
+    "dgrad_qkv_ffn1": ("gemm4w_kernelILb1ELb0ELi0EDF16bLb0E", "gemm4p_kernelILb0ELi0E", "gemm4p_kernel<false, 0>"),
     "ao_fwd": ("gemm4h_kernelILb1ELi1E", "gemm4h_kernel<true, 1>"),
     "dgrad_out": ("gemm4h_kernelILb0ELi0E", "gemm4h_kernel<false, 0>"),
     "dgrad_ffn2": ("gemm8_kernelILb1ELb0ELi9EDF16bLb0E",),
@@ -77,10 +81,13 @@ def main():
     cnt = defaultdict(lambda: defaultdict(int))       # (name, grid) -> launches seen per counter
     tsum = defaultdict(float)
     tn = defaultdict(int)
+    clk = defaultdict(list)                           # (name, grid) -> same-pass GUI/8/duration samples
     for d in dirs:
         per, dur = read_pass(d)
         for k, e in per.items():
             key = (e["_name"], e["_grid"])
+            if "GRBM_GUI_ACTIVE" in e and dur.get(k):
+                clk[key].append(e["GRBM_GUI_ACTIVE"] / 8 / dur[k])
             for c, v in e.items():
                 if not c.startswith("_"):
                     agg[key][c] += v
@@ -104,12 +111,14 @@ def main():
         fetch, write = avg(key, "FETCH_SIZE"), avg(key, "WRITE_SIZE")
         hbm = 2 * fetch * 1024 + write * 1024 if fetch is not None and write is not None else None
         cyc = gui / 8 if gui else None
+        cs = sorted(clk[key])
+        clock = cs[len(cs) // 2] if cs and t_ns >= 50e3 else None
         rows.append({
             "kernel": key[0], "grid": key[1], "avg_us": t_ns / 1e3,
             "ms_per_step": tsum[key] / tn[key] * (tn[key] / len(dirs)) / steps / 1e6 if tn[key] else None,
             "launches_per_step": tn[key] / len(dirs) / steps,
             "mfma_busy": busy / (N_SIMD * cyc) if busy is not None and cyc else None,
-            "clock_ghz": cyc / t_ns if cyc else None,
+            "clock_ghz": clock,
             "valu_insts": avg(key, "SQ_INSTS_VALU"), "mfma_insts": avg(key, "SQ_INSTS_MFMA"),
             "lds_conflict_frac": (avg(key, "SQ_LDS_BANK_CONFLICT") / avg(key, "SQ_LDS_IDX_ACTIVE")
                                   if avg(key, "SQ_LDS_IDX_ACTIVE") else None),
@@ -127,7 +136,7 @@ def main():
            f"bench.py PriGumbel B=256 bf16, {steps:g} iterations traced per pass; passes: "
            + ", ".join(Path(d).name for d in dirs), "",
            "mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (1024 x GRBM_GUI_ACTIVE/8); HBM = 2 x FETCH_SIZE + WRITE_SIZE; "
-           "clock = GRBM_GUI_ACTIVE/8 / duration (durations are from the profiled passes)", "",
+           "clock = GRBM_GUI_ACTIVE/8 / duration per dispatch, both from the same pass (median; kernels >= 50 us only)", "",
            "| ms/step | launches/step | avg us | mfma_busy | clock GHz | VALU/MFMA insts | LDS conflict | HBM MB/launch "
            "| HBM GB/s | L2 hit | kernel (grid) |",
            "|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|---|"]
