@@ -25,6 +25,10 @@ SHAPES = [
     ("ffn1_dgrad", R, 768, 3072, "dgrad", "none"),
     ("qkv_dgrad", R, 768, 2304, "dgrad", "none"),
     ("ao_dgrad", R, 768, 768, "dgrad", "none"),
+    # the step's BERT input gradients accumulate into the residual gradient (beta = 1)
+    ("ffn1_dgrad_acc", R, 768, 3072, "dgrad", "none+acc"),
+    ("qkv_dgrad_acc", R, 768, 2304, "dgrad", "none+acc"),
+    ("ao_dgrad_acc", R, 768, 768, "dgrad", "none+acc"),
     ("qkv_wgrad", 2304, 768, R, "wgrad", "none"),
     ("ffn1_wgrad", 3072, 768, R, "wgrad", "none"),
     ("ffn2_wgrad", 768, 3072, R, "wgrad", "none"),
@@ -50,11 +54,14 @@ def run(name, M, N, Kd, layout, epi, iters=20):
         bb = bias.to(dt)
         tf = lambda: torch.nn.functional.linear(A, B, bb)
     elif layout == "dgrad":
+        beta = 1.0 if epi.endswith("+acc") else 0.0
+        epi = epi.split("+")[0]
         A = torch.randn(M, Kd, device=dev, dtype=dt)
         B = torch.randn(Kd, N, device=dev, dtype=dt) * 0.05
-        C = torch.empty(M, N, device=dev, dtype=dt)
+        C = torch.randn(M, N, device=dev, dtype=dt) * 0.01
         aux = torch.randn(M, N, device=dev, dtype=dt) if epi != "none" else None
-        f = lambda: K.gemm(A, B, C, M=M, N=N, K=Kd, a_kc=1, b_kc=0, lda=Kd, ldb=N, ldc=N, epi=epi, aux=aux, ldaux=N)
+        f = lambda: K.gemm(A, B, C, M=M, N=N, K=Kd, a_kc=1, b_kc=0, lda=Kd, ldb=N, ldc=N, epi=epi, aux=aux, ldaux=N,
+                           beta=beta)
         tf = lambda: A @ B
     else:
         A = torch.randn(Kd, M, device=dev, dtype=dt)
