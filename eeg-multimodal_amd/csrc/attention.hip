@@ -33,42 +33,46 @@ struct AttnArgs {
   const int* cu;                    // varlen (packed rows): sequence b = rows cu[b] .. cu[b+1]-1, L = max length
 };
 
-// Dropout mask of the probabilities P[q][key] of head (b,h): element ((b*H+h)*L + q)*L + key of
-// the site's keep_bits8 stream (common.h), so forward and backward agree.
-DEV uint64_t attn_elem(const AttnArgs& a, int b, int h, long q, long key) {
-  return (((uint64_t)b * a.H + h) * a.L + q) * a.L + key;
+// Dropout numbering of the attention probabilities (every attention kernel, so forward and backward
+// agree): element (b, h, q, key) with key = 32 c + 16 j + 4 u + r is kept iff halfword 4 j + r of the
+// Philox-7 call attn_call(b, h, q, c, u) is >= thr16 (keep_bits8 / philox4x32_r<7>, common.h).  The
+// eight draws of a call are exactly the keys one MFMA lane (g = u) holds for query q in the forward's
+// S^T layout (rows 4g + r of the 16-key blocks 2c and 2c + 1, i.e. one pack_acc fragment), so the
+// forward applies them to its own probabilities with no cross-lane exchange.
+DEV uint64_t attn_call(const AttnArgs& a, int b, int h, long q, long c, int u) {
+  return (((uint64_t)b * a.H + h) * a.L + q) * (uint64_t)(4 * ((a.L + 31) >> 5)) + 4 * c + u;
 }
-// Forward layout: lane (g, li) needs keys 16f+4g..16f+4g+3 (f = 0..3) of query q: nibble (g&1) of
-// the call for key octet 2f + (g>>1).  Lanes g and g^1 (16 apart) need the same 4 calls: each
-// draws two (f = 2(g&1), 2(g&1)+1) and swaps the partner's nibbles with one shuffle.
+// Forward layout: lane (g, li) of query q needs keys k0 + 16 f + 4 g + r (f = 0..3, k0 % 64 == 0):
+// nib[f] bit r.  Calls (q, k0 / 32 + cc, g), cc = 0, 1, hold f = 2 cc (halfwords 0-3) and 2 cc + 1 (4-7).
 DEV void attn_mask_fwd(const AttnArgs& a, int b, int h, long q, long k0, int g, uint32_t thr, uint32_t (&nib)[4]) {
-  const int par = g & 1;
-  uint32_t mine[2], give = 0;
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int f = 2 * par + t;
-    const uint32_t bits = keep_bits8(a.seed, a.offset, attn_elem(a, b, h, q, k0 + 16 * f + 8 * (g >> 1)) >> 3, thr);
-    mine[t] = (bits >> (4 * par)) & 0xFu;
-    give |= ((bits >> (4 * (par ^ 1))) & 0xFu) << (4 * t);
+  for (int cc = 0; cc < 2; ++cc) {
+    const uint32_t bits = keep_bits8(a.seed, a.offset, attn_call(a, b, h, q, (k0 >> 5) + cc, g), thr);
+    nib[2 * cc] = bits & 0xFu;
+    nib[2 * cc + 1] = bits >> 4;
   }
-  const uint32_t got = (uint32_t)__shfl_xor((int)give, 16, 64);
-  nib[2 * par] = mine[0];
-  nib[2 * par + 1] = mine[1];
-  nib[2 * (par ^ 1)] = got & 0xFu;
-  nib[2 * (par ^ 1) + 1] = (got >> 4) & 0xFu;
 }
-// Backward layout: lane (g, li) needs mask[q0 + 16qf + 4g + r][kb + li] for qf = 0,1, r = 0..3.
-// Lane (g, m = li>>3, s = li&7) draws the key-octet-m row of query q0 + 16(s>>2) + 4g + (s&3); the
-// 8 lanes of the octet then gather bit (li&7) of each other's rows.
-DEV void attn_mask_bwd(const AttnArgs& a, int b, int h, long q0, long kb, int lane, uint32_t thr, uint32_t& m8) {
-  const int g = lane >> 4, li = lane & 15, mo = li >> 3, s = li & 7;
-  const uint32_t row = keep_bits8(a.seed, a.offset,
-                                  attn_elem(a, b, h, q0 + 16 * (s >> 2) + 4 * g + (s & 3), kb + 8 * mo) >> 3, thr);
-  m8 = 0;
+// Backward layout: lane (g, li) needs mask[q0 + 16 qf + 4 g + r][kw + 16 f + li] as bit t = 4 qf + r of
+// m8[f] (kw % 32 == 0).  The eight queries' calls of key group u = li >> 2 serve the whole lane quad
+// (li & ~3 .. +3): lane al = li & 3 draws those of queries t = 2 al, 2 al + 1 and the quad exchanges
+// the bytes; lane al keeps bit 4 f + al of every byte (key kw + 16 f + 4 u + al).
+DEV void attn_mask_bwd(const AttnArgs& a, int b, int h, long q0, long kw, int lane, uint32_t thr, uint32_t (&m8)[2]) {
+  const int g = lane >> 4, li = lane & 15, u = li >> 2, al = li & 3;
+  uint32_t pair = 0;
 #pragma unroll
-  for (int t = 0; t < 8; ++t) {
-    const uint32_t rt = (uint32_t)__shfl((int)row, (lane & ~7) | t, 64);
-    m8 |= ((rt >> s) & 1u) << t;               // bit t <-> (qf = t>>2, r = t&3)
+  for (int k = 0; k < 2; ++k) {
+    const int t = 2 * al + k;
+    pair |= keep_bits8(a.seed, a.offset, attn_call(a, b, h, q0 + 16 * (t >> 2) + 4 * g + (t & 3), kw >> 5, u), thr)
+            << (8 * k);
+  }
+  m8[0] = m8[1] = 0;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const uint32_t v = (uint32_t)__shfl((int)pair, (lane & ~3) | s, 64);    // bytes of queries 2 s, 2 s + 1
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int f = 0; f < 2; ++f) m8[f] |= ((v >> (8 * k + 4 * f + al)) & 1u) << (2 * s + k);
   }
 }
 
@@ -326,10 +330,12 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(AttnArgs a) {
     f32x4 p[2][2], ds[2][2];
     uint32_t m8[2] = {0xFFu, 0xFFu};
     if (a.p > 0.f) {
+      if (a.bits) {
 #pragma unroll
-      for (int f = 0; f < 2; ++f) {
-        if (a.bits) m8[f] = load_bits_bwd(a.bits + (((long)b * a.H + h) * a.L + q0) * (a.L / 32), a.L / 32, kw0 + 16 * f, g, li);
-        else attn_mask_bwd(a, b, h, q0, kw0 + 16 * f, lane, thr, m8[f]);
+        for (int f = 0; f < 2; ++f)
+          m8[f] = load_bits_bwd(a.bits + (((long)b * a.H + h) * a.L + q0) * (a.L / 32), a.L / 32, kw0 + 16 * f, g, li);
+      } else {
+        attn_mask_bwd(a, b, h, q0, kw0, lane, thr, m8);
       }
     }
 #pragma unroll

@@ -319,6 +319,21 @@ DEV uint32_t keep_bits8(uint64_t seed, uint64_t offset, uint64_t call, uint32_t 
   return thr16 ? bits : 0xFFu;                       // thr16 = 0 (p < 2^-16): every element kept
 }
 DEV uint32_t thr16_of(float p) { return (uint32_t)fminf(p * 65536.0f, 65535.0f); }
+// The same eight keep decisions as 0 / 1 halfword multipliers (word j -> halfwords 2j, 2j + 1), for
+// applying a call's draws to eight packed bf16 values at once with v_pk_mul_lo_u16 (thr16 > 0)
+DEV u32x4 keep01x8(uint64_t seed, uint64_t offset, uint64_t call, uint32_t thr16) {
+  const u32x4s r = philox4x32_r<7>((uint32_t)call, (uint32_t)(call >> 32), (uint32_t)offset,
+                                   (uint32_t)(offset >> 32), (uint32_t)seed, (uint32_t)(seed >> 32));
+  const uint32_t tm = (thr16 - 1u) & 0xFFFFu, tm2 = tm | (tm << 16), ones = 0x00010001u;
+  return u32x4{pk_keep01(r.x, tm2, ones), pk_keep01(r.y, tm2, ones), pk_keep01(r.z, tm2, ones),
+               pk_keep01(r.w, tm2, ones)};
+}
+// bf16 pair x (0 or 1 per halfword): the value itself or +0, bit-exact (asm: one VALU)
+DEV uint32_t pk_mul_u16(uint32_t a, uint32_t b) {
+  uint32_t d;
+  asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
 
 DEV float drop_mask1(uint64_t seed, uint64_t offset, uint64_t e, float p) {
   float m[4];

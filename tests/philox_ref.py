@@ -35,15 +35,33 @@ def drop_mask(seed: int, offset: int, elems, p: float) -> np.ndarray:
     return np.where(r >= thr, 1.0 / (1.0 - np.float64(np.float32(p))), 0.0)
 
 
-def attn_mask(seed: int, offset: int, elems, p: float) -> np.ndarray:
-    """Attention-probability stream (common.h keep_bits8): Philox4x32-7, eight 16-bit draws per call;
-    element e kept iff halfword (e & 7) of philox7(e >> 3, offset; seed) >= uint32(float32(p) * 65536)."""
-    e = np.asarray(elems, dtype=np.uint64)
-    c = e >> np.uint64(3)
+def _keep16(seed: int, offset: int, call, k, p: float) -> np.ndarray:
+    """halfword k (0..7) of philox7(call, offset; seed) >= uint32(float32(p) * 65536): scale or zero."""
+    c = np.asarray(call, dtype=np.uint64)
     w = philox4x32(c & _M32, c >> np.uint64(32), offset & 0xFFFFFFFF, offset >> 32, seed & 0xFFFFFFFF, seed >> 32,
                    rounds=7)
-    k = (e & np.uint64(7)).astype(np.int64)
+    k = np.asarray(k, dtype=np.int64)
     word = np.choose(k >> 1, w)
     half = (word >> (np.uint64(16) * (k & 1).astype(np.uint64))) & np.uint64(0xFFFF)
     thr = np.uint64(min(float(np.float32(p) * np.float32(65536.0)), 65535.0))
     return np.where(half >= thr, 1.0 / (1.0 - np.float64(np.float32(p))), 0.0)
+
+
+def attn_mask(seed: int, offset: int, elems, p: float) -> np.ndarray:
+    """The Philox-7 16-bit stream of the LayerNorm-fused dropout sites (common.h keep_bits8): eight
+    16-bit draws per call; element e kept iff halfword (e & 7) of philox7(e >> 3, offset; seed) >=
+    uint32(float32(p) * 65536)."""
+    e = np.asarray(elems, dtype=np.uint64)
+    return _keep16(seed, offset, e >> np.uint64(3), (e & np.uint64(7)).astype(np.int64), p)
+
+
+def attn_probs_mask(seed: int, offset: int, elems, p: float, L: int) -> np.ndarray:
+    """Attention-probability dropout (csrc/attention.hip attn_call): element e = row * L + key of the
+    [B, H, L, L] probabilities (row = (b * H + h) * L + q), key = 32 c + 16 j + 4 u + r, is kept iff
+    halfword 4 j + r of philox7(row * 4 * ceil(L / 32) + 4 c + u, offset; seed) >= uint32(float32(p) * 65536)."""
+    e = np.asarray(elems, dtype=np.uint64)
+    row, key = e // np.uint64(L), e % np.uint64(L)
+    c, j, u, r = key >> np.uint64(5), (key >> np.uint64(4)) & np.uint64(1), (key >> np.uint64(2)) & np.uint64(3), \
+        key & np.uint64(3)
+    call = row * np.uint64(4 * ((L + 31) // 32)) + np.uint64(4) * c + u
+    return _keep16(seed, offset, call, (np.uint64(4) * j + r).astype(np.int64), p)

@@ -9,7 +9,8 @@ every parameter gradient within 1e-4 relative to that tensor's max |value| (fp32
 Engine element/offset conventions per site (engine.py; R = the forward's rng base):
   emb R+1 | attn_out R+10+3i | ffn_out R+11+3i | attn_probs R+12+3i (attention stream)
   dec_sa R+100+8d | dec_ca R+101+8d | dec_ff R+102+8d | dec_sa_w R+103+8d | dec_ca_probs R+104+8d |
-  dec_ff_inner R+105+8d; element = row-major flat index of the dropped tensor.
+  dec_ff_inner R+105+8d; element = row-major flat index of the dropped tensor (attn_probs: the
+  [B, H, L, L] numbering of philox_ref.attn_probs_mask / attention.hip attn_call).
 """
 import numpy as np
 import pytest
@@ -17,7 +18,7 @@ import torch
 
 from goldens import det_params, load, rel_err
 from oracle import fusion_oracle as O
-from philox_ref import attn_mask, drop_mask
+from philox_ref import attn_mask, attn_probs_mask, drop_mask
 
 pytestmark = pytest.mark.gpu
 
@@ -33,12 +34,13 @@ def replay(seed: int, R: int, p: float):
             # LayerNorm-fused sites (emb, attn_out, ffn_out, dec_sa/ca/ff) draw from the Philox-7
             # 16-bit stream shared with the attention probabilities (layernorm.hip ln_keep)
             "emb": (R + 1, attn_mask), "attn_out": (R + 10 + 3 * i, attn_mask),
-            "ffn_out": (R + 11 + 3 * i, attn_mask), "attn_probs": (R + 12 + 3 * i, attn_mask),
+            "ffn_out": (R + 11 + 3 * i, attn_mask), "attn_probs": (R + 12 + 3 * i, "probs"),
             "dec_sa": (R + 100 + 8 * i, attn_mask), "dec_ca": (R + 101 + 8 * i, attn_mask),
             "dec_ff": (R + 102 + 8 * i, attn_mask), "dec_sa_w": (R + 103 + 8 * i, drop_mask),
             "dec_ca_probs": (R + 104 + 8 * i, drop_mask), "dec_ff_inner": (R + 105 + 8 * i, drop_mask),
         }[kind]
-        m = stream(seed, off, np.arange(x.numel(), dtype=np.uint64), p)
+        e = np.arange(x.numel(), dtype=np.uint64)
+        m = attn_probs_mask(seed, off, e, p, x.shape[-1]) if stream == "probs" else stream(seed, off, e, p)
         return x * torch.from_numpy(m).view(x.shape).to(x.dtype)
     return fn
 

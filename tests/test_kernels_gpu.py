@@ -176,9 +176,9 @@ def _check_bits(bits, z, B, L):
 
 
 def _attn_mask(B, L, p, seed, offset):
-    from philox_ref import attn_mask
+    from philox_ref import attn_probs_mask
     e = torch.arange(B * 12 * L * L, dtype=torch.int64).numpy()
-    return torch.from_numpy(attn_mask(seed, offset, e, p)).view(B, 12, L, L).cuda()
+    return torch.from_numpy(attn_probs_mask(seed, offset, e, p, L)).view(B, 12, L, L).cuda()
 
 
 @pytest.mark.parametrize("dt", DT)

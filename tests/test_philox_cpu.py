@@ -28,3 +28,19 @@ def test_dropout_streams_rates():
     # distinct offsets give independent masks
     a, b = drop_mask(7, 3, e, 0.5) > 0, drop_mask(7, 4, e, 0.5) > 0
     assert abs((a == b).mean() - 0.5) < 0.01
+
+
+def test_attn_probs_numbering_is_a_bijection():
+    """attention.hip attn_call: (row, key) -> (call, halfword) is one-to-one for any L (L % 32 != 0
+    leaves draws unused), and the kept fraction is 1 - p."""
+    import numpy as np
+    from philox_ref import attn_probs_mask
+    for L in (256, 65):
+        rows = 3 * L
+        key = np.arange(L, dtype=np.int64)
+        c, j, u, r = key >> 5, (key >> 4) & 1, (key >> 2) & 3, key & 3
+        call = np.arange(rows, dtype=np.int64)[:, None] * (4 * ((L + 31) // 32)) + 4 * c + u
+        draw = call * 8 + 4 * j + r
+        assert np.unique(draw).size == rows * L
+    m = attn_probs_mask(7, 3, np.arange(64 * 256 * 256, dtype=np.uint64), 0.1, 256)
+    assert abs((m > 0).mean() - 0.9) < 2e-3

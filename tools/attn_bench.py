@@ -40,8 +40,10 @@ def main(B=256, L=256, p=0.1, iters=20, use_bits=True):
 
 
 if __name__ == "__main__":
-    ps = [float(x) for x in sys.argv[1:]] or [0.1]
+    nobits = "--nobits" in sys.argv        # only the regenerated-mask path (the engine's)
+    ps = [float(x) for x in sys.argv[1:] if not x.startswith("--")] or [0.1]
     for p in ps:
-        main(p=p, use_bits=True)
+        if not nobits or p == 0:
+            main(p=p, use_bits=True)
         if p > 0:
             main(p=p, use_bits=False)
