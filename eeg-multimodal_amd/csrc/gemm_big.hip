@@ -952,6 +952,7 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
 // the outputs exist only once the statement completes, so hipcc can neither read nor move them early
 // (a compiler-visible load would instead make hipcc's waitcnt pass, blind to the asm LDS-DMA, wait for
 // the next tile's prefetch at the first use)
+DEV int g_odd(int lane) { return (lane >> 4) & 1; }
 DEV void load_bias8(f32x4 (&b)[8], const float* p) {
   asm volatile(
       "global_load_dwordx4 %0, %8, off\n\tglobal_load_dwordx4 %1, %8, off offset:64\n\t"
@@ -964,14 +965,60 @@ DEV void load_bias8(f32x4 (&b)[8], const float* p) {
       : "memory");
 }
 
-template <bool BKC, int EPI>
+// A bf16 input tile (the beta * C or the aux operand of an input-gradient epilogue) in the widened store
+// layout: lane chunk (i, jp) = 16 B at row mrow + 16 i, column nst + 32 jp (see the store pairing below);
+// all 32 loads in flight at once and retired by the statement's own vmcnt(0), which also covers the
+// next tile's staging issued just before it.  One asm statement: hipcc can neither read nor copy the
+// destination registers before the wait (a compiler-visible load would make its waitcnt pass, blind to
+// the asm LDS-DMA, wait for everything anyway; separate load and wait statements let it move the
+// registers in between)
+DEV void load_tile16(uint4 (&c)[8][4], const bf16* const (&p)[8]) {
+  asm volatile(
+      "global_load_dwordx4 %0, %32, off\n\t"
+      "global_load_dwordx4 %1, %32, off offset:64\n\t"
+      "global_load_dwordx4 %2, %32, off offset:128\n\t"
+      "global_load_dwordx4 %3, %32, off offset:192\n\t"
+      "global_load_dwordx4 %4, %33, off\n\t"
+      "global_load_dwordx4 %5, %33, off offset:64\n\t"
+      "global_load_dwordx4 %6, %33, off offset:128\n\t"
+      "global_load_dwordx4 %7, %33, off offset:192\n\t"
+      "global_load_dwordx4 %8, %34, off\n\t"
+      "global_load_dwordx4 %9, %34, off offset:64\n\t"
+      "global_load_dwordx4 %10, %34, off offset:128\n\t"
+      "global_load_dwordx4 %11, %34, off offset:192\n\t"
+      "global_load_dwordx4 %12, %35, off\n\t"
+      "global_load_dwordx4 %13, %35, off offset:64\n\t"
+      "global_load_dwordx4 %14, %35, off offset:128\n\t"
+      "global_load_dwordx4 %15, %35, off offset:192\n\t"
+      "global_load_dwordx4 %16, %36, off\n\t"
+      "global_load_dwordx4 %17, %36, off offset:64\n\t"
+      "global_load_dwordx4 %18, %36, off offset:128\n\t"
+      "global_load_dwordx4 %19, %36, off offset:192\n\t"
+      "global_load_dwordx4 %20, %37, off\n\t"
+      "global_load_dwordx4 %21, %37, off offset:64\n\t"
+      "global_load_dwordx4 %22, %37, off offset:128\n\t"
+      "global_load_dwordx4 %23, %37, off offset:192\n\t"
+      "global_load_dwordx4 %24, %38, off\n\t"
+      "global_load_dwordx4 %25, %38, off offset:64\n\t"
+      "global_load_dwordx4 %26, %38, off offset:128\n\t"
+      "global_load_dwordx4 %27, %38, off offset:192\n\t"
+      "global_load_dwordx4 %28, %39, off\n\t"
+      "global_load_dwordx4 %29, %39, off offset:64\n\t"
+      "global_load_dwordx4 %30, %39, off offset:128\n\t"
+      "global_load_dwordx4 %31, %39, off offset:192\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=&v"(c[0][0]), "=&v"(c[0][1]), "=&v"(c[0][2]), "=&v"(c[0][3]), "=&v"(c[1][0]), "=&v"(c[1][1]), "=&v"(c[1][2]), "=&v"(c[1][3]), "=&v"(c[2][0]), "=&v"(c[2][1]), "=&v"(c[2][2]), "=&v"(c[2][3]), "=&v"(c[3][0]), "=&v"(c[3][1]), "=&v"(c[3][2]), "=&v"(c[3][3]), "=&v"(c[4][0]), "=&v"(c[4][1]), "=&v"(c[4][2]), "=&v"(c[4][3]), "=&v"(c[5][0]), "=&v"(c[5][1]), "=&v"(c[5][2]), "=&v"(c[5][3]), "=&v"(c[6][0]), "=&v"(c[6][1]), "=&v"(c[6][2]), "=&v"(c[6][3]), "=&v"(c[7][0]), "=&v"(c[7][1]), "=&v"(c[7][2]), "=&v"(c[7][3])
+      : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "v"(p[4]), "v"(p[5]), "v"(p[6]), "v"(p[7])
+      : "memory");
+}
+template <bool BKC, int EPI, bool ACC = false>     // ACC: EPI_NONE with C = alpha A B^T + beta C
 __global__ void __launch_bounds__(NT4, 1) gemm4p_kernel(BigArgs g) {
   constexpr bool AKC = true;
   constexpr int LDS4 = NSLOT4 * SLOT4;
   constexpr bool HAS_BIAS = EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_D;
-  // an aux INPUT tile (EPI_MUL_AUX) or beta * C is not taken: 128 registers of loads would have to be
-  // retired under the prefetch by a counted wait hipcc cannot see (a first version read them through
-  // separate asm loads and got wrong results: hipcc moved the registers before the wait)
+  // an input tile: aux (EPI_MUL_AUX: activation' product) or beta * C (EPI_NONE, beta != 0: residual
+  // accumulate), read by load_tile16 after the next tile's staging is issued
+  constexpr bool IN_EPI = (EPI == EPI_NONE && ACC) || EPI == EPI_MUL_AUX;
   __shared__ __attribute__((aligned(16))) bf16 lds[LDS4];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1133,33 +1180,73 @@ __global__ void __launch_bounds__(NT4, 1) gemm4p_kernel(BigArgs g) {
       stage_first(nA, nB);
     }
     __builtin_amdgcn_sched_barrier(0);
+    // Stores: the epilogue is store-ISSUE-bound (0.25 MB per CU per tile with GELU': ~240 of 490 us per
+    // launch went to 8-B stores, profiles/r3q_exp.log), so column blocks j = 2 jp, 2 jp + 1 are paired:
+    // one v_permlane16_swap per dword gives lanes g even 8 contiguous columns of block 2 jp and lanes g
+    // odd those of block 2 jp + 1 (cdna_hip_programming.md T21, 16-lane form) -> one 16-B store each.
+    // The swap is an involution: applied to an input tile read in that layout it restores the
+    // accumulator layout.
+    const int nst = n0 + wn * 128 + 16 * g_odd(lane) + 8 * (lane >> 5);     // + 32 jp
+    constexpr bool in_tile = IN_EPI;
+    uint4 cin[8][4];
+    if (IN_EPI && in_tile) {
+      const bf16* src = EPI == EPI_MUL_AUX ? g.aux : (const bf16*)g.C;
+      const long ld = EPI == EPI_MUL_AUX ? g.ldaux : g.ldc;
+      const bf16* rows[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) rows[i] = src + (long)(mrow + 16 * i) * ld + nst;
+      load_tile16(cin, rows);
+    }
 
     bf16* Cb = (bf16*)g.C;
+    auto st16 = [&](bf16* base, long ld, long m, int jp, bf16x4 a, bf16x4 b) {
+      uint2 ua = __builtin_bit_cast(uint2, a), ub = __builtin_bit_cast(uint2, b);
+      const auto rx = __builtin_amdgcn_permlane16_swap(ua.x, ub.x, false, false);
+      const auto ry = __builtin_amdgcn_permlane16_swap(ua.y, ub.y, false, false);
+      *(uint4*)(base + m * ld + nst + 32 * jp) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
+    };
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const long m = mrow + 16 * i;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int n = ncol + 16 * j;
-        float v[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = g.alpha * acc[i][j][r] + (HAS_BIAS ? biasv[j][r] : 0.f);
-        bf16x4 o, o2;
-        if (EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_D) {
-          f32x2 gl0, gl1, gd0, gd1;
-          gelu2(f32x2{v[0], v[1]}, gl0, EPI == EPI_BIAS_GELU_D ? &gd0 : nullptr);
-          gelu2(f32x2{v[2], v[3]}, gl1, EPI == EPI_BIAS_GELU_D ? &gd1 : nullptr);
-          if (EPI == EPI_BIAS_GELU_D) {
-            o2[0] = (bf16)gd0.x; o2[1] = (bf16)gd0.y; o2[2] = (bf16)gd1.x; o2[3] = (bf16)gd1.y;
-          } else {
-            o2[0] = (bf16)v[0]; o2[1] = (bf16)v[1]; o2[2] = (bf16)v[2]; o2[3] = (bf16)v[3];   // pre-activation
-          }
-          o[0] = (bf16)gl0.x; o[1] = (bf16)gl0.y; o[2] = (bf16)gl1.x; o[3] = (bf16)gl1.y;
-          if (EPI == EPI_BIAS_GELU_D || g.aux) *(bf16x4*)(g.aux + m * g.ldaux + n) = o2;
-        } else {
-          o[0] = (bf16)v[0]; o[1] = (bf16)v[1]; o[2] = (bf16)v[2]; o[3] = (bf16)v[3];
+      for (int jp = 0; jp < 4; ++jp) {
+        bf16x4 o[2], o2[2], ci[2];
+        if (IN_EPI && in_tile) {     // input chunk back to the accumulator layout (blocks 2 jp, 2 jp + 1)
+          const uint4 c4 = cin[i][jp];
+          const auto rx = __builtin_amdgcn_permlane16_swap(c4.x, c4.z, false, false);
+          const auto ry = __builtin_amdgcn_permlane16_swap(c4.y, c4.w, false, false);
+          ci[0] = __builtin_bit_cast(bf16x4, make_uint2(rx[0], ry[0]));
+          ci[1] = __builtin_bit_cast(bf16x4, make_uint2(rx[1], ry[1]));
         }
-        *(bf16x4*)(Cb + m * g.ldc + n) = o;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int j = 2 * jp + h;
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            v[r] = g.alpha * acc[i][j][r] + (HAS_BIAS ? biasv[j][r] : 0.f);
+            if (IN_EPI && in_tile) {
+              if (EPI == EPI_MUL_AUX) v[r] *= (float)ci[h][r];
+              else v[r] += g.beta * (float)ci[h][r];
+            }
+          }
+          if (EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_D) {
+            f32x2 gl0, gl1, gd0, gd1;
+            gelu2(f32x2{v[0], v[1]}, gl0, EPI == EPI_BIAS_GELU_D ? &gd0 : nullptr);
+            gelu2(f32x2{v[2], v[3]}, gl1, EPI == EPI_BIAS_GELU_D ? &gd1 : nullptr);
+            if (EPI == EPI_BIAS_GELU_D) {
+              o2[h][0] = (bf16)gd0.x; o2[h][1] = (bf16)gd0.y; o2[h][2] = (bf16)gd1.x; o2[h][3] = (bf16)gd1.y;
+            } else {     // pre-activation
+              o2[h][0] = (bf16)v[0]; o2[h][1] = (bf16)v[1]; o2[h][2] = (bf16)v[2]; o2[h][3] = (bf16)v[3];
+            }
+            o[h][0] = (bf16)gl0.x; o[h][1] = (bf16)gl0.y; o[h][2] = (bf16)gl1.x; o[h][3] = (bf16)gl1.y;
+          } else {
+            o[h][0] = (bf16)v[0]; o[h][1] = (bf16)v[1]; o[h][2] = (bf16)v[2]; o[h][3] = (bf16)v[3];
+          }
+        }
+        if ((EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_D) && (EPI == EPI_BIAS_GELU_D || g.aux))
+          st16(g.aux, g.ldaux, m, jp, o2[0], o2[1]);
+        st16(Cb, g.ldc, m, jp, o[0], o[1]);
       }
     }
     if (!more_tiles) break;
@@ -1355,13 +1442,22 @@ template <bool AKC, bool BKC, int EPI, typename TO>
 int launch_big(const BigArgs& a, int splits, hipStream_t s) {
   const int tiles = ((a.M + TM - 1) / TM) * ((a.N + TN - 1) / TN);
   if constexpr (AKC && sizeof(TO) == 2 && (EPI == EPI_NONE || EPI == EPI_BIAS || EPI == EPI_BIAS_GELU ||
-                                           EPI == EPI_BIAS_GELU_D)) {
+                                           EPI == EPI_BIAS_GELU_D || (EPI == EPI_MUL_AUX && !BKC))) {
     const bool won = EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_D || (EPI == EPI_NONE && !BKC && a.K >= 2048);
-    const bool p_ok = g_gemm4p == 1 || (g_gemm4p == 2 && won);
-    if (p_ok && g_gemm8 < 0 && splits == 1 && !a.colsum_part && a.M % TM == 0 && a.N % TN == 0 && a.beta == 0.f &&
+    const bool p_ok = g_gemm4p == 1 || (g_gemm4p >= 2 && won) || (g_gemm4p == 3 && EPI == EPI_MUL_AUX);
+    // beta * C: the EPI_NONE input tile only (the aux epilogue ignores beta, as big_epilogue does)
+    const bool beta_ok = a.beta == 0.f || EPI == EPI_NONE;
+    const bool aux_ok = EPI != EPI_MUL_AUX || (a.aux && a.ldaux % 8 == 0 && (((uintptr_t)a.aux) & 15) == 0);
+    if (p_ok && beta_ok && aux_ok && g_gemm8 < 0 && splits == 1 && !a.colsum_part && a.M % TM == 0 &&
+        a.N % TN == 0 && a.ldc % 8 == 0 && (((uintptr_t)a.C) & 15) == 0 &&
         a.K % BK4 == 0 && (((uintptr_t)a.bias) & 15) == 0) {
-      hipLaunchKernelGGL((gemm4p_kernel<BKC, EPI>), dim3(tiles < cu_count() ? tiles : cu_count()), dim3(NT4), 0, s,
-                         a);
+      const dim3 grid(tiles < cu_count() ? tiles : cu_count());
+      bool acc = false;
+      if constexpr (EPI == EPI_NONE) acc = a.beta != 0.f;
+      if constexpr (EPI == EPI_NONE) {
+        if (acc) hipLaunchKernelGGL((gemm4p_kernel<BKC, EPI, true>), grid, dim3(NT4), 0, s, a);
+      }
+      if (!acc) hipLaunchKernelGGL((gemm4p_kernel<BKC, EPI>), grid, dim3(NT4), 0, s, a);
       return (int)hipGetLastError();
     }
   }
@@ -1594,7 +1690,7 @@ extern "C" int eegf_tune(int key, int value) {
   if (key == 9) { const int o = g_group_m; g_group_m = value; return o; }
   if (key == 7) { const int o = g_ln_bwd_rpb; if (value < 4 || value > 1024 || value % 4) return EEGF_ERR_ARG; g_ln_bwd_rpb = value; return o; }
   if (key == 10) { const int o = g_ln_fwd768; g_ln_fwd768 = value; return o; }
-  if (key == 11) { const int o = g_gemm4p; if (value < 0 || value > 2) return EEGF_ERR_ARG; g_gemm4p = value; return o; }
+  if (key == 11) { const int o = g_gemm4p; if (value < 0 || value > 3) return EEGF_ERR_ARG; g_gemm4p = value; return o; }
   if (key == 6) { const int o = g_ln_rpw; if (value < 1 || value > 64) return EEGF_ERR_ARG; g_ln_rpw = value; return o; }
   return EEGF_ERR_ARG;
 }

@@ -576,24 +576,38 @@ def test_gemm_persistent_fwd(epi, M, N, K):
             assert torch.equal(aux, outs[1][1])
 
 
-@pytest.mark.parametrize("epi", ["none", "mul_aux"])
+@pytest.mark.parametrize("epi", ["none", "mul_aux", "none_beta"])
 @pytest.mark.parametrize("M,N,K", P_SHAPES)
 def test_gemm_persistent_dgrad(epi, M, N, K):
-    """gemm4p_kernel with a k-major B (input gradient); the aux product (mul_aux) is routed to the other
-    kernels under key 11 and must come out the same."""
+    """gemm4p_kernel with a k-major B (input gradient), with the input-tile epilogues (aux product, beta = 1
+    residual accumulate: the tile read in the widened store layout and swapped back), against a float64
+    reference and bit for bit against the default routing (key 11 = 0)."""
     k = _k()
     torch.manual_seed(27)
     dy = torch.randn(M, K, device="cuda").to(torch.bfloat16)
     w = (torch.randn(K, N, device="cuda") * 0.1).to(torch.bfloat16)
-    aux = torch.randn(M, N, device="cuda").to(torch.bfloat16) if epi != "none" else None
-    old = _tune(11, 1)
-    try:
-        out = k.linear_dgrad(dy, w, epi=epi, aux=aux)
-        torch.cuda.synchronize()
-    finally:
-        _tune(11, old)
-    ref, _ = _ref_epi(dy.double() @ w.double(), epi, None, aux, 1.0)
-    _check(out, ref, torch.bfloat16)
+    aux = torch.randn(M, N, device="cuda").to(torch.bfloat16) if epi == "mul_aux" else None
+    c0 = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+    outs = []
+    for key in (1, 0):
+        old = _tune(11, key)
+        try:
+            if epi == "none_beta":
+                out = c0.clone()
+                k.linear_dgrad(dy, w, out=out, beta=1.0)
+            else:
+                out = k.linear_dgrad(dy, w, epi=epi, aux=aux)
+            torch.cuda.synchronize()
+            outs.append(out)
+        finally:
+            _tune(11, old)
+    if epi == "none_beta":
+        ref = c0.double() + dy.double() @ w.double()
+    else:
+        ref, _ = _ref_epi(dy.double() @ w.double(), epi, None, aux, 1.0)
+    _check(outs[0], ref, torch.bfloat16)
+    if K >= 256:
+        assert torch.equal(outs[0], outs[1])
 
 
 def test_gemm_persistent_falls_back_on_ragged_shapes():
