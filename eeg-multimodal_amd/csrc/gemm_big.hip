@@ -1089,15 +1089,32 @@ __global__ void __launch_bounds__(NT4, 1) gemm4p_kernel(BigArgs g) {
   tile_base(L, baseA, baseB, m0, n0);
   stage_first(baseA, baseB);
   f32x4 acc[8][8];
+  // Cross-tile staging (nk >= 8): the K-loop tail of tile t stages tile t + 1's K-tiles 0 .. 4 into the
+  // slots it frees (the ring runs on across tiles: slot0 = where the tile's K-tile 0 sits), those are
+  // retired before the epilogue's first store, and tile t + 1 then skips its prologue wait and the
+  // waits of K-tiles 0 .. 2 (their operands have landed).  The epilogue stores -- counted in vmcnt
+  // with the LDS-DMA, so any wait behind them waits for them too -- drain under those K-tiles' MFMAs
+  // instead of in front of them (the GELU' FFN1 epilogue is store-bound: profiles/r3q_epilogue_anatomy.log)
+  const bool xs = nk >= 8;
+  int slot0 = 0;
+  bool landed = false;          // this tile's K-tiles 0 .. 4 retired (cross-staged and waited for)
   for (;;) {
+    const int Ln = L + G;
+    const bool more_tiles = Ln < ntiles;
+    int m0n = 0, n0n = 0;
+    const bf16* nA = nullptr;
+    const bf16* nB = nullptr;
+    if (more_tiles) tile_base(Ln, nA, nB, m0n, n0n);
+    const bool cross = xs && more_tiles;
     // K-tiles 0 and 1 retired (older epilogue stores still counted only make this wait stricter)
-    vm_wait_tiles(max(0, min(nk, NSLOT4) - 2));
+    if (!landed) vm_wait_tiles(max(0, min(nk, NSLOT4) - 2));
     raw_barrier();
     bf16x8 fa[2][8], fb[2][8];
+    const bf16* img0 = lds + slot0 * SLOT4;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      fa[0][i] = rdA(lds, i);
-      fb[0][i] = rdB(lds, i);
+      fa[0][i] = rdA(img0, i);
+      fb[0][i] = rdB(img0, i);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     raw_barrier();
@@ -1105,10 +1122,12 @@ __global__ void __launch_bounds__(NT4, 1) gemm4p_kernel(BigArgs g) {
     auto ktile = [&](auto Hc, int k, int slot, int nslot, auto Ic, auto Tc) __attribute__((always_inline)) {
       constexpr int H = decltype(Hc)::value;
       constexpr bool INIT = decltype(Ic)::value, TAIL = decltype(Tc)::value;
-      const bool more = !TAIL || k + 1 < nk, st = !TAIL || k + NSLOT4 < nk;
+      const bool more = !TAIL || k + 1 < nk;
+      const bool own = !TAIL || k + NSLOT4 < nk;           // stage this tile's K-tile k + 5
+      const bool st = own || cross;                        // ... or the next tile's K-tile k + 5 - nk
       const bf16* nimg = lds + nslot * SLOT4;
-      const bf16* sA = baseA + (k + NSLOT4) * BK4;
-      const bf16* sB = baseB + (k + NSLOT4) * stepB;
+      const bf16* sA = own ? baseA + (k + NSLOT4) * BK4 : nA + (k + NSLOT4 - nk) * BK4;
+      const bf16* sB = own ? baseB + (k + NSLOT4) * stepB : nB + (k + NSLOT4 - nk) * stepB;
       auto mma = [&](int s, int jj) {
         if (INIT) mma16_acc0(acc[s][jj], fb[H][jj], fa[H][s]);
         else mma16_acc(acc[s][jj], fb[H][jj], fa[H][s]);
@@ -1133,8 +1152,14 @@ __global__ void __launch_bounds__(NT4, 1) gemm4p_kernel(BigArgs g) {
         mma(s, 6);
         mma(s, 7);
       }
-      if (!TAIL) vm_wait_tiles(NSLOT4 - 2);
-      else vm_wait_tiles(max(0, min(nk - 1, k + NSLOT4) - (k + 2)));
+      // K-tile k + 2 retired (its fragments are read in the next K-tile): skipped when it landed before
+      // the tile started (cross-staged, k + 2 <= 4) or when there is no such K-tile of this tile
+      if (!(landed && k < NSLOT4 - 2) && k + 2 < nk) {
+        if (!TAIL || cross) vm_wait_tiles(NSLOT4 - 2);
+        else vm_wait_tiles(max(0, min(nk - 1, k + NSLOT4) - (k + 2)));
+      } else if (!cross && k + 2 >= nk) {
+        vm_wait_tiles(0);
+      }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       raw_barrier();
     };
@@ -1143,7 +1168,7 @@ __global__ void __launch_bounds__(NT4, 1) gemm4p_kernel(BigArgs g) {
     using F = std::false_type;
     using T = std::true_type;
     auto nxt = [](int sl) { return sl == NSLOT4 - 1 ? 0 : sl + 1; };
-    int slot = 0;
+    int slot = slot0;
     if (nk > NSLOT4) ktile(C0{}, 0, slot, nxt(slot), T{}, F{});
     else ktile(C0{}, 0, slot, nxt(slot), T{}, T{});
     slot = nxt(slot);
@@ -1170,15 +1195,10 @@ __global__ void __launch_bounds__(NT4, 1) gemm4p_kernel(BigArgs g) {
     const int ncol = n0 + wn * 128 + 4 * (lane >> 4);
     f32x4 biasv[8];
     if (HAS_BIAS) load_bias8(biasv, g.bias + ncol);
-    const int Ln = L + G;
-    const bool more_tiles = Ln < ntiles;
-    int m0n = 0, n0n = 0;
-    const bf16* nA = nullptr;
-    const bf16* nB = nullptr;
-    if (more_tiles) {
-      tile_base(Ln, nA, nB, m0n, n0n);
-      stage_first(nA, nB);
-    }
+    if (more_tiles && !cross) stage_first(nA, nB);
+    // cross-staged: the next tile's K-tiles 0 .. 4 retired before the first store (load_bias8 /
+    // load_tile16 wait for them too)
+    if (cross) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     // Stores: the epilogue is store-ISSUE-bound (0.25 MB per CU per tile with GELU': ~240 of 490 us per
     // launch went to 8-B stores, profiles/r3q_exp.log), so column blocks j = 2 jp, 2 jp + 1 are paired:
@@ -1255,6 +1275,9 @@ __global__ void __launch_bounds__(NT4, 1) gemm4p_kernel(BigArgs g) {
     n0 = n0n;
     baseA = nA;
     baseB = nB;
+    // cross-staged: the ring runs on (next tile's K-tile 0 sits in the slot after this tile's last)
+    landed = cross;
+    if (cross) slot0 = (slot0 + nk) % NSLOT4;
   }
 }
 
