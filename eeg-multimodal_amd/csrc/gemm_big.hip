@@ -1449,10 +1449,13 @@ __global__ void __launch_bounds__(NT4, 2) gemm4h_kernel(BigArgs g) {
 
 int g_gemm4h = [] { const char* e = getenv("EEGF_GEMM4H"); return e ? atoi(e) : 2; }();   // eegf_tune key 8
 // eegf_tune key 11: the persistent kernel (gemm4p_kernel) for the bf16-output GEMMs it takes: 0 off,
-// 1 every eligible shape, 2 the ones it won in the interleaved A/B (profiles/r3f_p_ab.log): the GELU /
-// GELU' forward GEMMs and the plain (EPI_NONE) input gradients; the bias-only forward GEMMs lost
-// (QKV 265 -> 293 us, out-projection 84 -> 91, FFN2 261 -> 273)
-int g_gemm4p = [] { const char* e = getenv("EEGF_GEMM4P"); return e ? atoi(e) : 2; }();   // step A/B: 67.00 -> 66.39 ms (r3g_step_ab.log)
+// 1 (default) every eligible shape (full 256 x 256 tiles, K-contiguous A: every BERT forward and input
+// gradient of the bench step), 2 the GELU / GELU' forward GEMMs and the plain / residual-accumulating
+// input gradients with K >= 2048, 3 = 2 + the aux-product input gradient.  Whole-step interleaved A/B
+// after the widened stores and the cross-tile staging (profiles/r3y_step_ab.log): 1 < 3 < 2 in every
+// round (median 64.01 / 64.88 / 65.01 ms); before them the bias-only forwards lost on this kernel
+// (QKV 265 -> 293 us, profiles/r3f_p_ab.log)
+int g_gemm4p = [] { const char* e = getenv("EEGF_GEMM4P"); return e ? atoi(e) : 1; }();
 int cu_count() {
   static const int cus = [] {
     int dev = 0, n = 256;

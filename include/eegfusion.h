@@ -76,9 +76,11 @@ int eegf_gemm(int dtype, int out_dtype, int a_kcontig, int b_kcontig, int epi,
  *   key 10: bf16 768-wide rows of eegf_ln_fwd on the 16-B-access kernel (1, default) or the generic
  *          4-columns-per-lane kernel (0);
  *   key 11: the persistent 256x256 bf16 GEMM (one workgroup per CU over the tiles, the next tile's
- *          operands staged under the current epilogue) for full-tile bf16-output GEMMs with epilogue
- *          NONE (beta 0) / BIAS / BIAS_GELU / BIAS_GELU_D: 0 off, 1 every such GEMM, 2 (default) the
- *          GELU / GELU' forward GEMMs and the plain input gradients with K >= 2048.
+ *          operands staged by the current tile's K-loop tail, epilogue stores draining under the next
+ *          tile's first K-tiles) for full-tile bf16-output GEMMs with a K-contiguous A and epilogue
+ *          NONE (any beta) / BIAS / BIAS_GELU / BIAS_GELU_D / MUL_AUX (k-major B): 0 off, 1 (default)
+ *          every such GEMM, 2 the GELU / GELU' forward GEMMs and the input gradients with K >= 2048,
+ *          3 = 2 + the MUL_AUX input gradients.
  * Process-global (see the contract above): test / benchmark state, not for production callers. */
 int eegf_tune(int key, int value);
 /* Diagnostics (no reference counterpart): every following 256-row GEMM launch of the 8-wave / 4-wave
