@@ -31,14 +31,20 @@ N_SIMD = 1024
 
 # bench.py roofline groups -> kernel-name fragments (mangled or demangled) + grid filters
 GROUPS = {     # bf16 instantiations appear mangled in rocprofv3's CSV (DF16b), the others demangled
+    # round 3: every BERT forward / input gradient runs on the persistent kernel gemm4p<BKC, EPI, ACC>;
+    # its grid is one workgroup per CU for every shape, so the three bias-only forwards share a row
     "ffn1_fwd": ("gemm8_kernelILb1ELb1ELi2EDF16bLb0E", "gemm8_kernelILb1ELb1ELi8EDF16bLb0E",
-                 "gemm4p_kernelILb1ELi2E", "gemm4p_kernelILb1ELi8E", "gemm4p_kernel<true, 2>", "gemm4p_kernel<true, 8>"),
+                 "gemm4p_kernel<true, 2, false>", "gemm4p_kernel<true, 8, false>",
+                 "gemm4p_kernelILb1ELi2ELb0E", "gemm4p_kernelILb1ELi8ELb0E"),
+    "fwd_bias_qkv_ao_ffn2": ("gemm4p_kernel<true, 1, false>", "gemm4p_kernelILb1ELi1ELb0E"),
     "qkv_fwd": ("gemm8_kernelILb1ELb1ELi1EDF16bLb0E",),
     "ffn2_fwd": ("gemm4w_kernelILb1ELb1ELi1EDF16bLb0E",),
-    "dgrad_qkv_ffn1": ("gemm4w_kernelILb1ELb0ELi0EDF16bLb0E", "gemm4p_kernelILb0ELi0E", "gemm4p_kernel<false, 0>"),
+    "dgrad_qkv_ffn1": ("gemm4w_kernelILb1ELb0ELi0EDF16bLb0E", "gemm4p_kernel<false, 0, true>",
+                       "gemm4p_kernelILb0ELi0ELb1E"),
     "ao_fwd": ("gemm4h_kernelILb1ELi1E", "gemm4h_kernel<true, 1>"),
-    "dgrad_out": ("gemm4h_kernelILb0ELi0E", "gemm4h_kernel<false, 0>"),
-    "dgrad_ffn2": ("gemm8_kernelILb1ELb0ELi9EDF16bLb0E",),
+    "dgrad_out": ("gemm4h_kernelILb0ELi0E", "gemm4h_kernel<false, 0>", "gemm4p_kernel<false, 0, false>",
+                  "gemm4p_kernelILb0ELi0ELb0E"),
+    "dgrad_ffn2": ("gemm8_kernelILb1ELb0ELi9EDF16bLb0E", "gemm4p_kernel<false, 9, false>", "gemm4p_kernelILb0ELi9ELb0E"),
     "wgrad": ("gemm4w_kernel<false, false, 0, float, true", "gemm4w_kernelILb0ELb0ELi0EfLb1E"),
     "attn_fwd": ("attn_fwd256_kernel",),
     "attn_bwd": ("attn_bwd256_kernel",),
@@ -46,7 +52,9 @@ GROUPS = {     # bf16 instantiations appear mangled in rocprofv3's CSV (DF16b), 
     "ln_bwd": ("ln_bwd_kernel",),
 }
 # bench.py probes the QKV and FFN1 input gradients separately; they share one kernel and grid here
-ALIASES = {"dgrad_qkv": "dgrad_qkv_ffn1", "dgrad_ffn1": "dgrad_qkv_ffn1"}
+# (and, on the persistent kernel, the three bias-only forwards share one)
+ALIASES = {"dgrad_qkv": "dgrad_qkv_ffn1", "dgrad_ffn1": "dgrad_qkv_ffn1", "qkv_fwd": "fwd_bias_qkv_ao_ffn2",
+           "ffn2_fwd": "fwd_bias_qkv_ao_ffn2", "ao_fwd": "fwd_bias_qkv_ao_ffn2"}
 
 
 def short(name):
@@ -164,7 +172,7 @@ def main():
                      "hbm_bytes_per_launch": wavg("hbm_bytes"), "clock_ghz": wavg("clock_ghz"),
                      "lds_conflict_frac": wavg("lds_conflict_frac"), "round": tag}
     for a, g in ALIASES.items():
-        if g in groups:
+        if g in groups and a not in groups:
             groups[a] = dict(groups[g], alias_of=g)
     (ROOT / "profiles" / f"pmc_{tag}.json").write_text(json.dumps(groups, indent=1) + "\n")
     print(json.dumps(groups, indent=1))
