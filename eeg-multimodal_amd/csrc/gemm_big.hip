@@ -39,6 +39,7 @@ struct BigArgs {
   float* rowsum_part;    // gemm4w RS only: [splits][M] sums over this split's K of each row of a k-major A
   long long* ts;         // diagnostics (eegf_gemm_big_timestamps): per-workgroup phase times, null = off
   int group_m;           // tile raster: 0 row-major, G > 0 groups of G row panels walked column by column
+  int store_nt = 0;      // gemm4p: epilogue stores with the non-temporal hint
 };
 // key 9: -1 (default) = groups of 4 row panels when the grid is at least 8 tile columns wide (the
 // K = 768 forward / input-gradient GEMMs with N >= 2304: +2-4 %, profiles/r2r_group.log), row-major
@@ -1223,7 +1224,11 @@ __global__ void __launch_bounds__(NT4, 1) gemm4p_kernel(BigArgs g) {
       uint2 ua = __builtin_bit_cast(uint2, a), ub = __builtin_bit_cast(uint2, b);
       const auto rx = __builtin_amdgcn_permlane16_swap(ua.x, ub.x, false, false);
       const auto ry = __builtin_amdgcn_permlane16_swap(ua.y, ub.y, false, false);
-      *(uint4*)(base + m * ld + nst + 32 * jp) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
+      const u32x4 d = {rx[0], ry[0], rx[1], ry[1]};
+      bf16* pp = base + m * ld + nst + 32 * jp;
+      // non-temporal stores (eegf_tune key 12): 3-4 % off the store-bound epilogues, profiles/r4a_pol.log
+      if (g.store_nt) asm volatile("global_store_dwordx4 %0, %1, off nt" :: "v"(pp), "v"(d) : "memory");
+      else *(u32x4*)pp = d;
     };
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -1455,6 +1460,7 @@ int g_gemm4h = [] { const char* e = getenv("EEGF_GEMM4H"); return e ? atoi(e) : 
 // after the widened stores and the cross-tile staging (profiles/r3y_step_ab.log): 1 < 3 < 2 in every
 // round (median 64.01 / 64.88 / 65.01 ms); before them the bias-only forwards lost on this kernel
 // (QKV 265 -> 293 us, profiles/r3f_p_ab.log)
+int g_store_nt = [] { const char* e = getenv("EEGF_STORE_NT"); return e ? atoi(e) : 0; }();   // eegf_tune key 12
 int g_gemm4p = [] { const char* e = getenv("EEGF_GEMM4P"); return e ? atoi(e) : 1; }();
 int cu_count() {
   static const int cus = [] {
@@ -1478,12 +1484,14 @@ int launch_big(const BigArgs& a, int splits, hipStream_t s) {
         a.N % TN == 0 && a.ldc % 8 == 0 && (((uintptr_t)a.C) & 15) == 0 &&
         a.K % BK4 == 0 && (((uintptr_t)a.bias) & 15) == 0) {
       const dim3 grid(tiles < cu_count() ? tiles : cu_count());
+      BigArgs ap = a;
+      ap.store_nt = g_store_nt;
       bool acc = false;
       if constexpr (EPI == EPI_NONE) acc = a.beta != 0.f;
       if constexpr (EPI == EPI_NONE) {
-        if (acc) hipLaunchKernelGGL((gemm4p_kernel<BKC, EPI, true>), grid, dim3(NT4), 0, s, a);
+        if (acc) hipLaunchKernelGGL((gemm4p_kernel<BKC, EPI, true>), grid, dim3(NT4), 0, s, ap);
       }
-      if (!acc) hipLaunchKernelGGL((gemm4p_kernel<BKC, EPI>), grid, dim3(NT4), 0, s, a);
+      if (!acc) hipLaunchKernelGGL((gemm4p_kernel<BKC, EPI>), grid, dim3(NT4), 0, s, ap);
       return (int)hipGetLastError();
     }
   }
@@ -1716,6 +1724,7 @@ extern "C" int eegf_tune(int key, int value) {
   if (key == 9) { const int o = g_group_m; g_group_m = value; return o; }
   if (key == 7) { const int o = g_ln_bwd_rpb; if (value < 4 || value > 1024 || value % 4) return EEGF_ERR_ARG; g_ln_bwd_rpb = value; return o; }
   if (key == 10) { const int o = g_ln_fwd768; g_ln_fwd768 = value; return o; }
+  if (key == 12) { const int o = g_store_nt; if (value < 0 || value > 1) return EEGF_ERR_ARG; g_store_nt = value; return o; }
   if (key == 11) { const int o = g_gemm4p; if (value < 0 || value > 3) return EEGF_ERR_ARG; g_gemm4p = value; return o; }
   if (key == 6) { const int o = g_ln_rpw; if (value < 1 || value > 64) return EEGF_ERR_ARG; g_ln_rpw = value; return o; }
   return EEGF_ERR_ARG;

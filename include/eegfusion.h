@@ -80,7 +80,9 @@ int eegf_gemm(int dtype, int out_dtype, int a_kcontig, int b_kcontig, int epi,
  *          tile's first K-tiles) for full-tile bf16-output GEMMs with a K-contiguous A and epilogue
  *          NONE (any beta) / BIAS / BIAS_GELU / BIAS_GELU_D / MUL_AUX (k-major B): 0 off, 1 (default)
  *          every such GEMM, 2 the GELU / GELU' forward GEMMs and the input gradients with K >= 2048,
- *          3 = 2 + the MUL_AUX input gradients.
+ *          3 = 2 + the MUL_AUX input gradients;
+ *   key 12: persistent-GEMM epilogue stores with the non-temporal hint: 0 (default) off, 1 on (the
+ *          store-bound GEMMs run 3-4 % faster alone but the step 0.8 % slower, profiles/r4b_*).
  * Process-global (see the contract above): test / benchmark state, not for production callers. */
 int eegf_tune(int key, int value);
 /* Diagnostics (no reference counterpart): every following 256-row GEMM launch of the 8-wave / 4-wave
