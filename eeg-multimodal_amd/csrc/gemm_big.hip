@@ -681,6 +681,9 @@ __global__ void __launch_bounds__(NT, 1) gemm8_kernel(BigArgs g) {
 // LDS image of an operand K-tile: [256 rows][32 k] bf16 = 64-B rows; 16-B chunk c of row r stored at
 // chunk c ^ sw4(r), sw4(r) = 3 * ((r >> 3) & 1): conflict-free for the ds_read_b128 lane groups of a
 // 16-row fragment read (lanes 16q + i read row i, chunk q).
+#ifndef EEGF_W_PROBE
+#define EEGF_W_PROBE 0
+#endif
 constexpr int BK4 = 32, NT4 = 256, SLOT4 = 2 * TM * BK4;   // elements per ring slot (A + B, 32 KB)
 constexpr int NSLOT4 = 5;                                     // ring depth: 5 x 32 KB = the 160 KB of LDS
 static_assert(NSLOT4 * SLOT4 >= TM * LDC, "the epilogue tile reuses the ring");
@@ -773,7 +776,11 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
   // uniform base of K-tile kt: K-contiguous advances 32 elements, k-major 32 rows
   const bf16* baseA = AKC ? g.A + (long)m0 * g.lda + kbeg : g.A + (long)kbeg * g.lda + m0;
   const bf16* baseB = BKC ? g.B + (long)n0 * g.ldb + kbeg : g.B + (long)kbeg * g.ldb + n0;
-  const long stepA = AKC ? BK4 : (long)BK4 * g.lda, stepB = BKC ? BK4 : (long)BK4 * g.ldb;
+  // EEGF_W_PROBE (diagnostic builds only, tools/variant_lib.sh; results are wrong): 1 every K-tile
+  // re-reads K-tile 0's addresses (L2-resident operands), 2 no staging after the prologue, 3 = 2 with no
+  // per-K-tile waits and barrier (the MFMA + LDS-read ceiling of the loop).  profiles/r4c_wgrad_ceilings.log
+  const long stepA = EEGF_W_PROBE == 1 ? 0 : AKC ? BK4 : (long)BK4 * g.lda;
+  const long stepB = EEGF_W_PROBE == 1 ? 0 : BKC ? BK4 : (long)BK4 * g.ldb;
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr_of(lds));
   auto stage_part = [&](const bf16* bA, const bf16* bB, int slot, int j) {   // part j of a K-tile -> ring slot
     const bool kc = j < 4 ? AKC : BKC;
@@ -844,7 +851,7 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
   auto ktile = [&](auto Hc, int k, int slot, int nslot, auto Ic, auto Tc) __attribute__((always_inline)) {
     constexpr int H = decltype(Hc)::value;
     constexpr bool INIT = decltype(Ic)::value, TAIL = decltype(Tc)::value;
-    const bool more = !TAIL || k + 1 < nk, st = !TAIL || k + NSLOT4 < nk;
+    const bool more = !TAIL || k + 1 < nk, st = EEGF_W_PROBE < 2 && (!TAIL || k + NSLOT4 < nk);
     const bf16* nimg = lds + nslot * SLOT4;
     const bf16* sA = baseA + (k + NSLOT4) * stepA;        // uniform K-tile bases of the stage
     const bf16* sB = baseB + (k + NSLOT4) * stepB;
@@ -887,6 +894,10 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
       }
     }
     // K-tile k + 2 retired (its fragments are read in the next K-tile); younger: k + 3 .. k + NSLOT4
+    if constexpr (EEGF_W_PROBE == 3) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      return;
+    }
     if (!TAIL) vm_wait_tiles(NSLOT4 - 2);
     else vm_wait_tiles(max(0, min(nk - 1, k + NSLOT4) - (k + 2)));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads of k + 1 done: its slot may be restaged
