@@ -318,12 +318,32 @@ DEV uint32_t keep_bits8(uint64_t seed, uint64_t offset, uint64_t call, uint32_t 
   const uint32_t bits = (b & 0x55u) | (b >> 15);     // bit k = halfword k
   return thr16 ? bits : 0xFFu;                       // thr16 = 0 (p < 2^-16): every element kept
 }
+// keep_bits8 for a call number known to fit 32 bits (counter word 1 = 0): the same draws; with the
+// high word a constant, the first round's output word 0 and the second round's first product are
+// wave-uniform (scalar), one v_mad_u64_u32 fewer per call
+DEV uint32_t keep_bits8_c32(uint64_t seed, uint64_t offset, uint32_t call, uint32_t thr16) {
+  const u32x4s r = philox4x32_r<7>(call, 0u, (uint32_t)offset, (uint32_t)(offset >> 32), (uint32_t)seed,
+                                   (uint32_t)(seed >> 32));
+  const uint32_t tm = (thr16 - 1u) & 0xFFFFu, tm2 = tm | (tm << 16), ones = 0x00010001u;
+  const uint32_t b = pk_keep01(r.x, tm2, ones) | (pk_keep01(r.y, tm2, ones) << 2) |
+                     (pk_keep01(r.z, tm2, ones) << 4) | (pk_keep01(r.w, tm2, ones) << 6);
+  const uint32_t bits = (b & 0x55u) | (b >> 15);
+  return thr16 ? bits : 0xFFu;
+}
 DEV uint32_t thr16_of(float p) { return (uint32_t)fminf(p * 65536.0f, 65535.0f); }
 // The same eight keep decisions as 0 / 1 halfword multipliers (word j -> halfwords 2j, 2j + 1), for
 // applying a call's draws to eight packed bf16 values at once with v_pk_mul_lo_u16 (thr16 > 0)
 DEV u32x4 keep01x8(uint64_t seed, uint64_t offset, uint64_t call, uint32_t thr16) {
   const u32x4s r = philox4x32_r<7>((uint32_t)call, (uint32_t)(call >> 32), (uint32_t)offset,
                                    (uint32_t)(offset >> 32), (uint32_t)seed, (uint32_t)(seed >> 32));
+  const uint32_t tm = (thr16 - 1u) & 0xFFFFu, tm2 = tm | (tm << 16), ones = 0x00010001u;
+  return u32x4{pk_keep01(r.x, tm2, ones), pk_keep01(r.y, tm2, ones), pk_keep01(r.z, tm2, ones),
+               pk_keep01(r.w, tm2, ones)};
+}
+// keep01x8 for a call number known to fit 32 bits (see keep_bits8_c32)
+DEV u32x4 keep01x8_c32(uint64_t seed, uint64_t offset, uint32_t call, uint32_t thr16) {
+  const u32x4s r = philox4x32_r<7>(call, 0u, (uint32_t)offset, (uint32_t)(offset >> 32), (uint32_t)seed,
+                                   (uint32_t)(seed >> 32));
   const uint32_t tm = (thr16 - 1u) & 0xFFFFu, tm2 = tm | (tm << 16), ones = 0x00010001u;
   return u32x4{pk_keep01(r.x, tm2, ones), pk_keep01(r.y, tm2, ones), pk_keep01(r.z, tm2, ones),
                pk_keep01(r.w, tm2, ones)};
