@@ -43,14 +43,19 @@ DEV void glds16_asm(const void* g, const void* lds_base) {
   const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lv*)lds_base);
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(l) : "memory", "m0");
 }
-// saddr form: wave-uniform 64-bit base + per-lane 32-bit byte offset (no 64-bit address VGPRs)
+// saddr form: wave-uniform 64-bit base + per-lane 32-bit byte offset (no 64-bit address VGPRs).
+// Wait states: the base SGPRs are often written by a VALU just before the statement
+// (v_readfirstlane_b32 below, or v_readlane_b32 restoring a spilled SGPR), and a VMEM instruction
+// reading an SGPR a VALU wrote needs 5 wait states, which hipcc does not insert inside asm.  The
+// s_mov to M0 (1) + s_nop 3 (4) give 5; they also cover the 1 state the LDS-DMA needs after the M0
+// write.  tools/isa_lint.py checks every LDS-DMA of the built library for both hazards.
 DEV void glds16_asm_s(const void* base, uint32_t voff, const void* lds_base) {
   typedef __attribute__((address_space(3))) void lv;
   const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lv*)lds_base);
   const uint64_t b = (uint64_t)(uintptr_t)base;
   const uint64_t bu = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
                       (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
-  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(bu), "s"(l)
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 3\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(bu), "s"(l)
                : "memory", "m0");
 }
 // saddr form with a 32-bit LDS byte address (no generic->LDS pointer cast per call) and a base the
@@ -61,7 +66,7 @@ DEV void glds16_asm_sa(const void* base, uint32_t voff, uint32_t lds_addr) {
   const uint64_t b = (uint64_t)(uintptr_t)base;
   const uint64_t bu = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
                       (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
-  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(bu), "s"(lds_addr)
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 3\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(bu), "s"(lds_addr)
                : "memory", "m0");
 }
 DEV uint32_t lds_addr_of(const void* p) {

@@ -1,0 +1,64 @@
+"""ISA hazard lint of the shipped library (no GPU needed).
+
+The production LDS-DMA statements (``common.h`` ``glds16_asm_s`` / ``glds16_asm_sa``) read a 64-bit
+base from SGPRs that a VALU often writes just before them (``v_readfirstlane_b32``, or a
+``v_readlane_b32`` restoring a spilled SGPR).  A VMEM instruction reading such an SGPR needs 5 wait
+states, which hipcc never inserts inside an asm string; with fewer, some waves of some launches load
+from a stale base with no fault.  ``tools/isa_lint.py`` disassembles every gfx950 code object of
+``libeegfusion.so`` and walks back from each VMEM instruction; this test requires zero findings.
+"""
+from pathlib import Path
+
+import pytest
+
+from tools import isa_lint
+
+LIB = Path(__file__).resolve().parents[1] / "eeg-multimodal_amd" / "eegfusion" / "libeegfusion.so"
+
+
+def _inst(addr, text):
+    mnem, _, rest = text.partition(" ")
+    ops = [o.strip().split()[0] for o in rest.split(",") if o.strip()]
+    return isa_lint.Inst(addr, mnem, ops, text)
+
+
+def _prog(*texts):
+    return [_inst(4 * k, t) for k, t in enumerate(texts)]
+
+
+def test_lint_flags_readfirstlane_two_states_before_dma():
+    """The exact round-3 pattern: 2 wait states between the VALU write and the DMA base read."""
+    f = isa_lint.lint_function("k", _prog(
+        "v_readfirstlane_b32 s1, v7", "v_readfirstlane_b32 s0, v6", "s_mov_b32 m0, s3", "s_nop 0",
+        "global_load_lds_dwordx4 v1, s[0:1]"))
+    assert [(x.kind, x.states) for x in f] == [("valu_sgpr_vmem", 2)]
+
+
+def test_lint_counts_nops_and_accepts_five_states():
+    ok = isa_lint.lint_function("k", _prog(
+        "v_readfirstlane_b32 s0, v6", "s_mov_b32 m0, s3", "s_nop 3", "global_load_lds_dwordx4 v1, s[0:1]"))
+    assert ok == []
+    short = isa_lint.lint_function("k", _prog(
+        "v_readlane_b32 s61, v242, 2", "s_mov_b32 m0, s3", "s_nop 2", "global_load_lds_dwordx4 v1, s[60:61]"))
+    assert [(x.kind, x.states) for x in short] == [("valu_sgpr_vmem", 4)]
+
+
+def test_lint_m0_and_carry_and_branch_predecessors():
+    m0 = isa_lint.lint_function("k", _prog("s_mov_b32 m0, s3", "global_load_lds_dwordx4 v1, off"))
+    assert [x.kind for x in m0] == ["salu_m0_lds_dma"]
+    # a carry-out SGPR of v_mad_u64_u32 read as buffer soffset
+    carry = isa_lint.lint_function("k", _prog(
+        "v_mad_u64_u32 v[4:5], s[8:9], v3, s0, v[0:1]", "buffer_load_dword v1, v2, s[4:7], s8 offen"))
+    assert [x.kind for x in carry] == ["valu_sgpr_vmem"]
+    # the writer sits before a branch that jumps straight to the load (target = function start + 0x10)
+    br = [_inst(0, "v_readfirstlane_b32 s0, v6"), _inst(4, "s_branch 2 <k+0x10>"),
+          _inst(8, "s_nop 7"), _inst(12, "s_nop 7"), _inst(16, "global_load_dword v1, v2, s[0:1]")]
+    assert [(x.kind, x.states) for x in isa_lint.lint_function("k", br)] == [("valu_sgpr_vmem", 1)]
+
+
+@pytest.mark.skipif(not LIB.exists(), reason="libeegfusion.so not built (run __graft_entry__.build())")
+def test_shipped_library_has_no_vmem_sgpr_hazards():
+    findings, counts = isa_lint.lint(LIB)
+    assert counts["lds_dma"] > 1000, counts          # the production GEMM / attention DMA rings are present
+    assert findings == [], "\n".join(
+        f"{f.kind}: {f.func} @0x{f.addr:x} '{f.inst}' {f.states} states after '{f.writer}'" for f in findings[:20])

@@ -1,0 +1,228 @@
+#!/usr/bin/env python3
+"""ISA hazard lint over the gfx950 code objects inside ``libeegfusion.so``.
+
+hipcc pads wait states around its own instructions but nothing inside an ``asm`` string, so a
+hazard between compiler code and an asm statement (or inside one) is invisible until a kernel
+returns wrong values on some waves of some launches (cdna_hip_programming.md "What hipcc does not
+do", item 2).  This lint reads the shipped library, not the sources:
+
+1. the ``.hip_fatbin`` section is split into its clang offload bundles (one per ``csrc/*.hip``
+   translation unit) and every ``gfx950`` code object is disassembled with ``llvm-objdump``;
+2. every vector-memory instruction (``global_*``, ``buffer_*``, ``scratch_*``, ``flat_*``) is walked
+   backwards through straight-line code and branch predecessors, counting wait states (one per
+   instruction, N + 1 for ``s_nop N``), and checked against the two hazards that touch LDS-DMA:
+
+   * ``valu_sgpr_vmem`` — a VALU instruction writes an SGPR (``v_readfirstlane_b32``,
+     ``v_readlane_b32`` restoring a spilled SGPR, a ``v_cmp`` / carry-out destination) that the VMEM
+     instruction reads as address base, descriptor or soffset: 5 wait states required;
+   * ``salu_m0_lds_dma`` — ``s_mov_b32 m0`` ahead of an LDS-DMA load (``*_lds_*`` / ``... lds``),
+     which reads M0 as its LDS destination: 1 wait state required.
+
+usage: python tools/isa_lint.py [path/to/libeegfusion.so] [--all]
+Exit status 1 when any hazard is found.  ``tests/test_isa_lint_cpu.py`` runs it on the built library.
+"""
+from __future__ import annotations
+
+import os
+import re
+import struct
+import subprocess
+import sys
+import tempfile
+from collections import Counter, defaultdict
+from dataclasses import dataclass
+from pathlib import Path
+
+LLVM_BIN = Path(os.environ.get("ROCM_PATH", "/opt/rocm")) / "lib" / "llvm" / "bin"
+BUNDLE_MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+ARCH = "gfx950"
+
+REQUIRED = {"valu_sgpr_vmem": 5, "salu_m0_lds_dma": 1}
+
+# VALU mnemonics whose second operand is an SGPR destination (carry-out / scale flag)
+_SDST1 = re.compile(r"^v_(add_co|sub_co|subrev_co|addc_co|subb_co|subbrev_co)_u32|^v_mad_(u64_u32|i64_i32)|"
+                    r"^v_div_scale_f(32|64)")
+_VMEM = re.compile(r"^(global|buffer|scratch|flat|tbuffer)_")
+_LINE = re.compile(r"^\s+(\S+)(.*?)\s*//\s*([0-9A-Fa-f]+):")
+_FUNC = re.compile(r"^([0-9a-f]+) <(.+)>:$")
+_TARGET = re.compile(r"<(.+)\+0x([0-9a-f]+)>")
+_SREG = re.compile(r"^s\[(\d+):(\d+)\]$|^s(\d+)$")
+_NAMED = {"vcc": ("vcc_lo", "vcc_hi"), "vcc_lo": ("vcc_lo",), "vcc_hi": ("vcc_hi",), "m0": ("m0",),
+          "exec": ("exec_lo", "exec_hi"), "exec_lo": ("exec_lo",), "exec_hi": ("exec_hi",)}
+
+
+@dataclass
+class Inst:
+    addr: int
+    mnem: str
+    ops: list
+    text: str
+
+
+@dataclass
+class Finding:
+    kind: str
+    func: str
+    addr: int
+    inst: str
+    writer: str
+    states: int
+
+
+def bundles(so: Path) -> list[bytes]:
+    """gfx950 code objects of every offload bundle in the library's .hip_fatbin section."""
+    with tempfile.TemporaryDirectory() as td:
+        fb = Path(td) / "fatbin"
+        subprocess.run([str(LLVM_BIN / "llvm-objcopy"), f"--dump-section=.hip_fatbin={fb}", str(so),
+                        str(Path(td) / "stripped")], check=True, capture_output=True)
+        data = fb.read_bytes()
+    out, pos = [], 0
+    while True:
+        start = data.find(BUNDLE_MAGIC, pos)
+        if start < 0:
+            break
+        n = struct.unpack_from("<Q", data, start + 24)[0]
+        p = start + 32
+        end = start + 32
+        for _ in range(n):
+            off, size, tlen = struct.unpack_from("<QQQ", data, p)
+            p += 24
+            triple = data[p:p + tlen].decode()
+            p += tlen
+            end = max(end, start + off + size)
+            if triple.endswith(ARCH) and size:
+                out.append(data[start + off:start + off + size])
+        pos = max(end, start + len(BUNDLE_MAGIC))
+    return out
+
+
+def disassemble(code: bytes) -> dict[str, list[Inst]]:
+    with tempfile.NamedTemporaryFile(suffix=".o") as f:
+        f.write(code)
+        f.flush()
+        txt = subprocess.run([str(LLVM_BIN / "llvm-objdump"), "-d", "--no-show-raw-insn", f"--mcpu={ARCH}",
+                              f.name], check=True, capture_output=True, text=True).stdout
+    funcs: dict[str, list[Inst]] = {}
+    cur = None
+    for line in txt.splitlines():
+        m = _FUNC.match(line)
+        if m:
+            cur = funcs.setdefault(m.group(2), [])
+            continue
+        m = _LINE.match(line)
+        if m and cur is not None:
+            mnem, rest, addr = m.group(1), m.group(2).strip(), int(m.group(3), 16)
+            ops = [o.strip().split()[0] for o in rest.split(",") if o.strip()] if rest else []
+            cur.append(Inst(addr, mnem, ops, f"{mnem} {rest}".strip()))
+    return funcs
+
+
+def sregs(op: str) -> tuple:
+    m = _SREG.match(op)
+    if m:
+        if m.group(3) is not None:
+            return (f"s{m.group(3)}",)
+        return tuple(f"s{i}" for i in range(int(m.group(1)), int(m.group(2)) + 1))
+    return _NAMED.get(op, ())
+
+
+def valu_sgpr_writes(ins: Inst) -> set:
+    if not ins.mnem.startswith("v_") or not ins.ops:
+        return set()
+    w = set(sregs(ins.ops[0]))
+    if len(ins.ops) > 1 and _SDST1.match(ins.mnem):
+        w |= set(sregs(ins.ops[1]))
+    if ins.mnem.startswith("v_cmpx"):
+        w |= {"exec_lo", "exec_hi"}
+    return w
+
+
+def is_lds_dma(ins: Inst) -> bool:
+    return bool(_VMEM.match(ins.mnem)) and ("_lds_" in ins.mnem or re.search(r"\blds\b", ins.text) is not None)
+
+
+def vmem_sgpr_reads(ins: Inst) -> set:
+    r = set()
+    for op in ins.ops[1:] if not ins.mnem.startswith(("global_store", "buffer_store", "scratch_store", "flat_store",
+                                                       "global_atomic", "buffer_atomic")) else ins.ops:
+        r |= set(sregs(op))
+    if is_lds_dma(ins):
+        r.add("m0")
+    return r
+
+
+def states(ins: Inst) -> int:
+    if ins.mnem == "s_nop":
+        return int(ins.ops[0], 0) + 1 if ins.ops else 1
+    return 1
+
+
+def lint_function(name: str, insts: list[Inst]) -> list[Finding]:
+    by_addr = {ins.addr: k for k, ins in enumerate(insts)}
+    preds = defaultdict(list)               # index of a branch target -> indices of branches to it
+    for k, ins in enumerate(insts):
+        if ins.mnem.startswith(("s_branch", "s_cbranch")):
+            m = _TARGET.search(ins.text)
+            if m and insts:
+                tgt = insts[0].addr + int(m.group(2), 16)
+                if tgt in by_addr:
+                    preds[by_addr[tgt]].append(k)
+    out: list[Finding] = []
+    for k, ins in enumerate(insts):
+        if not _VMEM.match(ins.mnem):
+            continue
+        reads = vmem_sgpr_reads(ins)
+        if not reads:
+            continue
+        found = {}
+
+        def walk(j: int, acc: int, seen: frozenset):
+            # j: index of the instruction just before the point reached; acc: wait states between
+            while j >= 0 and acc < REQUIRED["valu_sgpr_vmem"]:
+                for b in preds.get(j + 1, ()):   # insts[j + 1] is a branch target: its branches too
+                    if b != j and b not in seen:
+                        walk(b - 1, acc + 1, seen | {b})
+                p = insts[j]
+                if p.mnem in ("s_branch", "s_endpgm", "s_setpc_b64"):
+                    return                       # no fall-through from above an unconditional branch
+                if valu_sgpr_writes(p) & reads:
+                    found.setdefault("valu_sgpr_vmem", (acc, p.text))
+                    return
+                if is_lds_dma(ins) and p.mnem.startswith("s_") and p.ops and p.ops[0] == "m0" and \
+                        acc < REQUIRED["salu_m0_lds_dma"]:
+                    found.setdefault("salu_m0_lds_dma", (acc, p.text))
+                acc += states(p)
+                j -= 1
+
+        walk(k - 1, 0, frozenset())
+        for kind, (acc, wtext) in found.items():
+            out.append(Finding(kind, name, ins.addr, ins.text, wtext, acc))
+    return out
+
+
+def lint(so: Path) -> tuple[list[Finding], Counter]:
+    findings, vmem = [], Counter()
+    for code in bundles(so):
+        for name, insts in disassemble(code).items():
+            findings += lint_function(name, insts)
+            vmem["lds_dma"] += sum(is_lds_dma(i) for i in insts)
+            vmem["vmem"] += sum(bool(_VMEM.match(i.mnem)) for i in insts)
+    return findings, vmem
+
+
+def main(argv: list[str]) -> int:
+    args = [a for a in argv if not a.startswith("--")]
+    so = Path(args[0]) if args else Path(__file__).resolve().parents[1] / "eeg-multimodal_amd" / "eegfusion" / \
+        "libeegfusion.so"
+    findings, vmem = lint(so)
+    print(f"{so}: {vmem['vmem']} VMEM instructions ({vmem['lds_dma']} LDS-DMA), {len(findings)} hazards")
+    per = Counter((f.kind, f.func) for f in findings)
+    for (kind, func), n in per.most_common():
+        print(f"  {n:5d}  {kind:16s} {func}")
+    for f in findings if "--all" in argv else findings[:10]:
+        print(f"  {f.kind}: {f.func} @0x{f.addr:x}: '{f.inst}' {f.states} state(s) after '{f.writer}'")
+    return 1 if findings else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main(sys.argv[1:]))
