@@ -113,21 +113,38 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline(variant: str, batch: int, iters: int) -> dict:
-    def progress(msg):
-        print(f"[bench cpu_baseline] {msg}", file=sys.stderr, flush=True)
+def cpu_share() -> dict:
+    """Host CPUs this process may use: the affinity mask, the cgroup CPU quota (cpu.max; a GPU box shows
+    the whole machine in its affinity mask but grants one GPU's share) and OMP_NUM_THREADS."""
+    avail = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or None
+    threads = min(x for x in (avail, quota, omp) if x)
+    return {"threads": threads, "affinity": avail, "cgroup_quota": quota, "omp_num_threads": omp}
 
+
+def cpu_baseline(variant: str, batch: int, iters: int) -> dict:
     """The CPU oracle (torch fp32 restatement, oracle/fusion_oracle.py; pinned against the reference's
     own outputs by tests/test_oracle_golden.py) timed on the host cores on a bounded sample of the
     same iteration: the bench's batch (256), dropout 0.1 at every reference site as on the GPU leg,
     PriConcat with the honoured feature_all_lap mechanism, one warm-up iteration then `iters` timed.
-    Threads = the CPUs this process may run on (sched_getaffinity), capped by OMP_NUM_THREADS (the
-    GPU box's CPU share)."""
+    Threads = the CPUs this process may run on (sched_getaffinity), capped by the cgroup quota and
+    OMP_NUM_THREADS (the GPU box's CPU share): cpu_share()."""
     import torch
     import torch.nn.functional as F
     from oracle import fusion_oracle as O
-    avail = len(os.sched_getaffinity(0))
-    threads = min(avail, int(os.environ.get("OMP_NUM_THREADS", avail)) or avail)
+
+    def progress(msg):
+        print(f"[bench cpu_baseline] {msg}", file=sys.stderr, flush=True)
+
+    share = cpu_share()
+    avail, threads = share["affinity"], share["threads"]
     torch.set_num_threads(threads)
     g = torch.Generator().manual_seed(0)
     O.set_dropout_replay(lambda site, x: F.dropout(x, 0.1, training=True))
@@ -190,7 +207,8 @@ def cpu_baseline(variant: str, batch: int, iters: int) -> dict:
     finally:
         O.set_dropout_replay(None)
     return {"value": round(batch * iters / dt, 4), "unit": "samples/s", "cores": threads, "kind": "port",
-            "cpu_model": cpu_model(), "cpus_available": avail, "seconds_per_iteration": round(dt / iters, 2),
+            "cpu_model": cpu_model(), "cpus_available": avail, "cpu_share": share,
+            "seconds_per_iteration": round(dt / iters, 2),
             "warmup_seconds": round(warm, 2),
             "sample": f"oracle/fusion_oracle.py {variant} iteration (torch CPU fp32, dropout 0.1"
                       f"{', feature_all_lap honoured' if variant != 'prigumbel' else ''}), batch {batch}, "
@@ -380,10 +398,11 @@ def main():
                     "bound": "mfma", "achieved": round(dom["tflops"], 1) if dom else None, "peak": PEAK_BF16,
                     "unit": "TFLOP/s", "frac": round(dom["tflops"] / PEAK_BF16, 4) if dom else None,
                     "traffic": pmc.get("hbm_bytes_per_launch"), "mfma_busy": pmc.get("mfma_busy"),
+                    "pmc_round": pmc.get("round"),
                     "avg_ms": round(dom["avg_ms"], 4) if dom else None,
                     "flops_per_launch": dom["flops_per_launch"] if dom else None}
         f1 = ks.get("ffn1_fwd")
-        ffn1 = load_profile_json("traffic.json", "ffn1_fwd") or {}
+        ffn1 = load_profile_json(PMC_FILE, "ffn1_fwd") or {}      # both FFN1 forms (pass 1 GELU, pass 2 + GELU')
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "samples/s", "n_gpus": world, "steps": steps,
             "warmup": args.warmup, "ms_per_step": round(total_dt / steps * 1e3, 3), "higher_is_better": True,
@@ -399,7 +418,8 @@ def main():
             "roofline_ffn1": ({"kernel": "ffn1_fwd (BertIntermediate GEMM + bias + GELU)", "bound": "mfma",
                                "achieved": round(f1["tflops"], 1), "peak": PEAK_BF16, "unit": "TFLOP/s",
                                "frac": round(f1["tflops"] / PEAK_BF16, 4), "avg_ms": round(f1["avg_ms"], 4),
-                               "traffic": ffn1.get("hbm_bytes_per_launch")} if f1 else None),
+                               "traffic": ffn1.get("hbm_bytes_per_launch"), "mfma_busy": ffn1.get("mfma_busy"),
+                               "pmc_round": ffn1.get("round")} if f1 else None),
             "step_roofline": {"achieved": round(step_tf, 1), "unit": "TFLOP/s", "frac": round(step_tf / PEAK_BF16, 4),
                               "flops_per_sample": flops_per_sample(args.variant)},
             "kernels": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}

@@ -53,7 +53,10 @@ def _bert(model, cfg, batch, training):
         ids, mask = batch["title_input"], batch["text_mask"]
         lens = mask.sum(1)
         right_padded = bool((mask == (torch.arange(mask.shape[1]) < lens[:, None]).long()).all())
-        if right_padded and int(lens.min()) > 0:
+        # cut to the longest real sequence only where no dropout is drawn: F.dropout / SDPA dropout over
+        # the cut tensors would consume torch's global RNG differently from the reference's padded run,
+        # so every later draw (noise, gate, DataLoader order) would stop being seed-for-seed comparable
+        if right_padded and int(lens.min()) > 0 and p_h == 0.0 and p_a == 0.0:
             keep = int(lens.max())
             ids, mask = ids[:, :keep], mask[:, :keep]
         B, L = ids.shape

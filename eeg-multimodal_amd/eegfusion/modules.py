@@ -253,6 +253,12 @@ class FusionModel(nn.Module):
         if any(t is not None and t.is_cuda for t in ts):
             raise RuntimeError("eegfusion: the model is in host memory but the inputs are device tensors; "
                                "call model.cuda()")
+        # the host path serves machines without a GPU (BASELINE configs[0]); on a GPU machine a model
+        # left in host memory is almost always a forgotten .cuda() and would run orders of magnitude
+        # slower without a word, so it is refused unless asked for explicitly
+        if torch.cuda.is_available() and os.environ.get("EEGF_HOST_PATH") != "1":
+            raise RuntimeError("eegfusion: the model is in host memory while a GPU is present; call model.cuda() "
+                               "(or set EEGF_HOST_PATH=1 to run the torch-op host path on purpose)")
         return True
 
     def _run(self, batch: dict, hard: bool) -> torch.Tensor:

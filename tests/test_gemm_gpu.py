@@ -539,7 +539,11 @@ def test_gemm_4h_dgrad(epi, M, N, K):
 
 # the persistent kernel (eegf_tune key 11): full tiles only; production-sized grids loop several rounds,
 # K below the ring depth (3 and 1 K-tiles) prefetches fewer K-tiles, a 24-tile grid runs one round
-P_SHAPES = [(65536, 2304, 768), (4096, 768, 768), (8192, 3072, 96), (2048, 1024, 32), (16384, 768, 3072)]
+# nk = K / 32 K-tiles: 24, 24, 3, 1, 96, and the ring-edge cases 5..7 (a full 5-slot ring, no cross-tile
+# staging) and 8 (the first cross-staged shape: the next tile's K-tiles 0..4 landed before it starts),
+# each with three rounds per CU on a 256-CU grid (768 tiles)
+P_SHAPES = [(65536, 2304, 768), (4096, 768, 768), (8192, 3072, 96), (2048, 1024, 32), (16384, 768, 3072),
+            (16384, 3072, 160), (16384, 3072, 192), (16384, 3072, 224), (16384, 3072, 256)]
 
 
 @pytest.mark.parametrize("epi", ["bias", "bias_gelu", "bias_gelu_d", "gelu_noaux", "none"])

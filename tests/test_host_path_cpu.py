@@ -107,3 +107,44 @@ def test_host_model_refuses_device_inputs():
     fake = torch.empty(0)
     with pytest.raises(RuntimeError):
         m._host(type("T", (), {"is_cuda": True})(), fake)
+
+
+def test_host_model_refused_when_a_gpu_is_present(monkeypatch):
+    """A model left in host memory on a GPU machine is a forgotten .cuda(): refused with a pointer to it,
+    unless EEGF_HOST_PATH=1 asks for the host path explicitly."""
+    from eegfusion.modules import ConcatModel
+    m = ConcatModel(contract="W", dropout=0.0)
+    x = torch.empty(0)
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    monkeypatch.delenv("EEGF_HOST_PATH", raising=False)
+    with pytest.raises(RuntimeError, match="model.cuda"):
+        m._host(x)
+    monkeypatch.setenv("EEGF_HOST_PATH", "1")
+    assert m._host(x)
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: False)
+    monkeypatch.delenv("EEGF_HOST_PATH")
+    assert m._host(x)
+
+
+def test_host_tokens_cut_only_without_dropout(monkeypatch):
+    """Right-padded token batches are cut to their longest real sequence only when no dropout is drawn
+    (eval, or p = 0): in training with dropout the padded tensors keep the reference's RNG consumption."""
+    from eegfusion import cpu_path
+    import model as drop_in
+    m = drop_in.ConcatModel()
+    B, Lp = 2, 512
+    ids = torch.zeros(B, Lp, dtype=torch.long)
+    mask = torch.zeros(B, Lp, dtype=torch.long)
+    mask[:, :40] = 1
+    seen = []
+    real_embedding = torch.nn.functional.embedding
+
+    def spy(i, w, *a, **k):
+        seen.append(i.shape[1])
+        return real_embedding(i, w, *a, **k)
+    monkeypatch.setattr(cpu_path.F, "embedding", spy)
+    batch = {"title_input": ids, "text_mask": mask}
+    with torch.no_grad():
+        cpu_path._bert(m, m.engine.cfg, batch, training=False)
+        cpu_path._bert(m, m.engine.cfg, batch, training=True)
+    assert seen == [40, Lp]
