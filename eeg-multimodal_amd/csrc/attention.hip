@@ -432,13 +432,14 @@ __global__ void dq_convert_kernel(const float* dq_acc, void* dqkv, int is_bf16, 
 
 #include "attention256.inc"
 
+}  // namespace
+
+int persistent_cus();    // gemm_big.hip: CU count minus the eegf_tune key 13 reserve
+
+namespace {
 // persistent L = 256 kernels: one workgroup per CU (capped by the item count)
 int l256_grid(int items) {
-  static const int cus = [] {
-    int dev = 0, n = 256;
-    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-    return n > 0 ? n : 256;
-  }();
+  const int cus = persistent_cus();
   return items < cus ? items : cus;
 }
 }  // namespace

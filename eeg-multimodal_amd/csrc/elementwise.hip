@@ -113,3 +113,29 @@ extern "C" int eegf_seq_mean_bwd(int dtype, int B, int L, int width, const float
   else return EEGF_ERR_ARG;
   return (int)hipGetLastError();
 }
+
+// Diagnostics (no reference counterpart): a stand-in for an RCCL all-reduce kernel's use of the CUs,
+// for measuring on one GPU whether the gradient all-reduces issued during the backward (trainer.py
+// GradReducer) can make progress while the backward's kernels hold the chip.  A fixed grid
+// of `wgs` workgroups (RCCL runs one block per channel) walks x[0, n) with a grid-stride loop `passes`
+// times, reading and rewriting every element unchanged (x * 1 + 0: the values stay bit-identical).
+namespace {
+__global__ void __launch_bounds__(256) ring_proxy_kernel(long n4, int passes, float* __restrict__ x) {
+  const long stride = (long)gridDim.x * 256;
+  for (int p = 0; p < passes; ++p) {
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
+      f32x4 v = ((f32x4*)x)[i];
+      // an opaque identity: the compiler may not drop the read-modify-write
+      asm volatile("" : "+v"(v));
+      ((f32x4*)x)[i] = v;
+    }
+    __syncthreads();
+  }
+}
+}  // namespace
+
+extern "C" int eegf_ring_proxy(long n, int passes, int wgs, float* x, hipStream_t stream) {
+  if (n <= 0 || n % 4 || passes <= 0 || wgs <= 0 || wgs > 4096 || !x || (((uintptr_t)x) & 15)) return EEGF_ERR_ARG;
+  hipLaunchKernelGGL(ring_proxy_kernel, dim3(wgs), dim3(256), 0, stream, n / 4, passes, x);
+  return (int)hipGetLastError();
+}

@@ -684,6 +684,9 @@ __global__ void __launch_bounds__(NT, 1) gemm8_kernel(BigArgs g) {
 #ifndef EEGF_W_PROBE
 #define EEGF_W_PROBE 0
 #endif
+#ifndef EEGF_W_READS
+#define EEGF_W_READS 0
+#endif
 constexpr int BK4 = 32, NT4 = 256, SLOT4 = 2 * TM * BK4;   // elements per ring slot (A + B, 32 KB)
 constexpr int NSLOT4 = 5;                                     // ring depth: 5 x 32 KB = the 160 KB of LDS
 static_assert(NSLOT4 * SLOT4 >= TM * LDC, "the epilogue tile reuses the ring");
@@ -859,19 +862,36 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
       if (INIT) mma16_acc0(acc[s][jj], fb[H][jj], fa[H][s]);
       else mma16_acc(acc[s][jj], fb[H][jj], fa[H][s]);
     };
+    // next K-tile's fragment reads: EEGF_W_READS 1 issues them in groups 0..5 (as gemm4p's
+    // EEGF_P_READS), 0 one fa + one fb per group
+    auto rd_next = [&](int s, int jj) __attribute__((always_inline)) {
+      if (!more) return;
+      if (EEGF_W_READS == 0) {
+        if (jj == 0) fa[H ^ 1][s] = rdA(nimg, s);
+        if (jj == 1) fb[H ^ 1][s] = rdB(nimg, s);
+      } else if (s < 4) {
+        if (jj == 0) fa[H ^ 1][s] = rdA(nimg, s);
+        if (jj == 1) fb[H ^ 1][2 * s] = rdB(nimg, 2 * s);
+        if (jj == 3) fb[H ^ 1][2 * s + 1] = rdB(nimg, 2 * s + 1);
+      } else if (s < 6) {
+        if (jj == 0) fa[H ^ 1][2 * s - 4] = rdA(nimg, 2 * s - 4);
+        if (jj == 1) fa[H ^ 1][2 * s - 3] = rdA(nimg, 2 * s - 3);
+      }
+    };
     // group s: the non-MFMA work sits in the shadows of the group's first MFMAs
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       mma(s, 0);
-      if (more) fa[H ^ 1][s] = rdA(nimg, s);
+      rd_next(s, 0);
       __builtin_amdgcn_sched_barrier(0);
       mma(s, 1);
-      if (more) fb[H ^ 1][s] = rdB(nimg, s);
+      rd_next(s, 1);
       __builtin_amdgcn_sched_barrier(0);
       mma(s, 2);
       if (st) stage_part(sA, sB, slot, s);
       __builtin_amdgcn_sched_barrier(0);
       mma(s, 3);
+      rd_next(s, 3);
       __builtin_amdgcn_sched_barrier(0);
       mma(s, 4);
       __builtin_amdgcn_sched_barrier(0);
@@ -1023,6 +1043,12 @@ DEV void load_tile16(uint4 (&c)[8][4], const bf16* const (&p)[8]) {
       : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "v"(p[4]), "v"(p[5]), "v"(p[6]), "v"(p[7])
       : "memory");
 }
+#ifndef EEGF_P_READS
+#define EEGF_P_READS 0
+#endif
+#ifndef EEGF_P_PROBE
+#define EEGF_P_PROBE 0
+#endif
 template <bool BKC, int EPI, bool ACC = false>     // ACC: EPI_NONE with C = alpha A B^T + beta C
 __global__ void __launch_bounds__(NT4, 1) gemm4p_kernel(BigArgs g) {
   constexpr bool AKC = true;
@@ -1144,18 +1170,39 @@ __global__ void __launch_bounds__(NT4, 1) gemm4p_kernel(BigArgs g) {
         if (INIT) mma16_acc0(acc[s][jj], fb[H][jj], fa[H][s]);
         else mma16_acc(acc[s][jj], fb[H][jj], fa[H][s]);
       };
+      // EEGF_P_READS 1: the next K-tile's 16 fragment reads issued in groups 0..5 (fb in 0..3 two per
+      // group beside that group's fa, fa 4..7 in 4..5), so the last two groups carry no LDS read and the
+      // lgkmcnt(0) ahead of the barrier finds them landed; 0: one fa + one fb per group (fb[7] read in
+      // group 7, ~6 MFMAs before the wait)
+      // EEGF_P_PROBE (diagnostic builds only, results wrong): 1 no staging after the first K-tiles,
+      // 2 = 1 + no per-K-tile waits or barrier
+      auto rd_next = [&](int s, int jj) __attribute__((always_inline)) {
+        if (!more) return;
+        if (EEGF_P_READS == 0) {
+          if (jj == 0) fa[H ^ 1][s] = rdA(nimg, s);
+          if (jj == 1) fb[H ^ 1][s] = rdB(nimg, s);
+        } else if (s < 4) {
+          if (jj == 0) fa[H ^ 1][s] = rdA(nimg, s);
+          if (jj == 1) fb[H ^ 1][2 * s] = rdB(nimg, 2 * s);
+          if (jj == 3) fb[H ^ 1][2 * s + 1] = rdB(nimg, 2 * s + 1);
+        } else if (s < 6) {
+          if (jj == 0) fa[H ^ 1][2 * s - 4] = rdA(nimg, 2 * s - 4);
+          if (jj == 1) fa[H ^ 1][2 * s - 3] = rdA(nimg, 2 * s - 3);
+        }
+      };
 #pragma unroll
       for (int s = 0; s < 8; ++s) {
         mma(s, 0);
-        if (more) fa[H ^ 1][s] = rdA(nimg, s);
+        rd_next(s, 0);
         __builtin_amdgcn_sched_barrier(0);
         mma(s, 1);
-        if (more) fb[H ^ 1][s] = rdB(nimg, s);
+        rd_next(s, 1);
         __builtin_amdgcn_sched_barrier(0);
         mma(s, 2);
-        if (st) stage_part(sA, sB, slot, s);
+        if (st && EEGF_P_PROBE == 0) stage_part(sA, sB, slot, s);
         __builtin_amdgcn_sched_barrier(0);
         mma(s, 3);
+        rd_next(s, 3);
         __builtin_amdgcn_sched_barrier(0);
         mma(s, 4);
         __builtin_amdgcn_sched_barrier(0);
@@ -1163,6 +1210,10 @@ __global__ void __launch_bounds__(NT4, 1) gemm4p_kernel(BigArgs g) {
         __builtin_amdgcn_sched_barrier(0);
         mma(s, 6);
         mma(s, 7);
+      }
+      if constexpr (EEGF_P_PROBE == 2) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        return;
       }
       // K-tile k + 2 retired (its fragments are read in the next K-tile): skipped when it landed before
       // the tile started (cross-staged, k + 2 <= 4) or when there is no such K-tile of this tile
@@ -1481,6 +1532,14 @@ int cu_count() {
   }();
   return cus;
 }
+int g_cu_reserve = 0;      // eegf_tune key 13
+}  // namespace
+// workgroups of a persistent grid: every CU but the reserved ones (room for RCCL kernels, key 13)
+int persistent_cus() {
+  const int n = cu_count() - g_cu_reserve;
+  return n > 0 ? n : 1;
+}
+namespace {
 template <bool AKC, bool BKC, int EPI, typename TO>
 int launch_big(const BigArgs& a, int splits, hipStream_t s) {
   const int tiles = ((a.M + TM - 1) / TM) * ((a.N + TN - 1) / TN);
@@ -1494,7 +1553,7 @@ int launch_big(const BigArgs& a, int splits, hipStream_t s) {
     if (p_ok && beta_ok && aux_ok && g_gemm8 < 0 && splits == 1 && !a.colsum_part && a.M % TM == 0 &&
         a.N % TN == 0 && a.ldc % 8 == 0 && (((uintptr_t)a.C) & 15) == 0 &&
         a.K % BK4 == 0 && (((uintptr_t)a.bias) & 15) == 0) {
-      const dim3 grid(tiles < cu_count() ? tiles : cu_count());
+      const dim3 grid(tiles < persistent_cus() ? tiles : persistent_cus());
       BigArgs ap = a;
       ap.store_nt = g_store_nt;
       bool acc = false;
@@ -1737,6 +1796,7 @@ extern "C" int eegf_tune(int key, int value) {
   if (key == 10) { const int o = g_ln_fwd768; g_ln_fwd768 = value; return o; }
   if (key == 12) { const int o = g_store_nt; if (value < 0 || value > 1) return EEGF_ERR_ARG; g_store_nt = value; return o; }
   if (key == 11) { const int o = g_gemm4p; if (value < 0 || value > 3) return EEGF_ERR_ARG; g_gemm4p = value; return o; }
+  if (key == 13) { const int o = g_cu_reserve; if (value < 0 || value >= cu_count()) return EEGF_ERR_ARG; g_cu_reserve = value; return o; }
   if (key == 6) { const int o = g_ln_rpw; if (value < 1 || value > 64) return EEGF_ERR_ARG; g_ln_rpw = value; return o; }
   return EEGF_ERR_ARG;
 }

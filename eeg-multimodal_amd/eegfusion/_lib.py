@@ -44,6 +44,7 @@ SIGNATURES: dict[str, list] = {
                       vp, vp],
     "eegf_tune": [i32, i32],
     "eegf_gemm_big_timestamps": [vp],
+    "eegf_ring_proxy": [i64, i32, i32, vp, vp],
     "eegf_ln_fwd": [i32, i64, i32, vp, vp, vp, i32, vp, vp, vp, f32, f32, i32, u64, u64, vp, vp, vp, vp, vp],
     "eegf_ln_bwd_partial_rows": [i64],
     "eegf_ln_bwd": [i32, i64, i32, vp, vp, vp, vp, vp, f32, i32, u64, u64, vp, vp, vp, vp, vp],

@@ -85,10 +85,17 @@ int eegf_gemm(int dtype, int out_dtype, int a_kcontig, int b_kcontig, int epi,
  *          store-bound GEMMs run 3-4 % faster alone but the step 0.8 % slower, profiles/r4b_*).
  * Process-global (see the contract above): test / benchmark state, not for production callers. */
 int eegf_tune(int key, int value);
+/*   key 13: CUs left free by the persistent kernels (the 256x256 GEMM and the L = 256 attention grids
+ *          launch cu_count - value workgroups; 0 = default): room for RCCL's kernels during the
+ *          backward when world > 1 (tools/overlap_proxy.py prices it). */
 /* Diagnostics (no reference counterpart): every following 256-row GEMM launch of the 8-wave / 4-wave
  * kernels writes 4 s_memrealtime stamps per workgroup (start, prologue done, K-loop done, epilogue
  * issued, slot 4 the CU id) into buf = int64 [grid.y][grid.x][8]; nullptr switches it off.  tools/gemm_phases.py. */
 int eegf_gemm_big_timestamps(long long* buf);
+/* Diagnostics (no reference counterpart): a stand-in for the CU use of an RCCL all-reduce kernel, for
+ * the one-GPU overlap proxy of the gradient all-reduces (tools/overlap_proxy.py): `wgs`
+ * workgroups read and rewrite x[0, n) unchanged `passes` times (n % 4 == 0, x 16-B aligned). */
+int eegf_ring_proxy(long n, int passes, int wgs, float* x, hipStream_t stream);
 /* Rows of the a_colsum partial buffer eegf_gemm_acs writes for this shape (ceil(M/256)), or 0 when
  * the fused column sums are unavailable (needs bf16 in/out, K-contiguous A, M >= 2048, N >= 256,
  * K % 64 == 0, 8-aligned dims). */

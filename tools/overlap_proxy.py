@@ -1,0 +1,138 @@
+"""One-GPU proxy for the gradient all-reduce / backward overlap of DESIGN §8.
+
+With world > 1 the trainer issues one RCCL all-reduce per BERT layer (28 MB) as soon as that layer's
+weight gradients are final, and RCCL's kernels then need CUs while the remaining layers' backward
+kernels run.  The persistent GEMM / attention kernels launch one workgroup per CU and hold its whole
+register file, so nothing can co-reside with them.  This tool measures what that means on one GPU:
+at each `grad_ready` point the reducer launches `eegf_ring_proxy` (a fixed grid of `wgs` workgroups
+reading and rewriting the layer's gradient range `passes` times, the CU footprint of a ring
+all-reduce kernel) on a side stream, and reports
+
+  * the step time with and without the proxy (interleaved rounds, one process);
+  * for every proxied range: the delay from its issue to the proxy kernel's start, its duration, and
+    whether it finished before the backward's last kernel (how much of the "all-reduce" overlapped);
+  * the same with the persistent grids capped at cu_count - k (eegf_tune key 13) for k in --reserve.
+
+Usage: python tools/overlap_proxy.py [--rounds 5] [--steps 6] [--wgs 32] [--passes 2] [--reserve 0,8,16]
+"""
+import argparse
+import json
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT / "eeg-multimodal_amd"), str(ROOT)]
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=6)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--wgs", type=int, default=32)
+    ap.add_argument("--passes", type=int, default=2)
+    ap.add_argument("--reserve", default="0,8,16")
+    args = ap.parse_args()
+    from eegfusion import _lib
+    from eegfusion._lib import call
+    from eegfusion.modules import PriGumbelModel
+    from eegfusion.trainer import GradReducer, PriGumbelTrainer
+
+    class ProxyReducer(GradReducer):
+        """GradReducer whose 'all-reduce' is the ring proxy on a side stream (timed per range)."""
+
+        def __init__(self, on):
+            super().__init__(scale_in_optimizer=True)
+            self.on = on
+            self.side = torch.cuda.Stream()
+            self.recs, self.bwd_end = [], None
+
+        def _launch(self, rngs):
+            g = self.arena.grad
+            for lo, hi in rngs:
+                for i in range(lo, hi, self.bucket):
+                    j = min(hi, i + self.bucket)
+                    self.log.append((i, j))
+                    n = (j - i) // 4 * 4
+                    if not self.on or n <= 0 or (g[i:].data_ptr() & 15):
+                        continue
+                    issue = torch.cuda.Event(enable_timing=True)
+                    issue.record()                                  # compute stream reached grad_ready
+                    self.side.wait_event(issue)
+                    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    s.record(self.side)
+                    call("eegf_ring_proxy", n, args.passes, args.wgs, g[i:].data_ptr(), self.side.cuda_stream)
+                    e.record(self.side)
+                    self.recs.append((issue, s, e, n * 4))
+
+        def finish(self, lo, hi):
+            if self.todo:
+                self._launch(self.ranges(self.arena, self.todo))
+                self.todo = set()
+            self.bwd_end = torch.cuda.Event(enable_timing=True)
+            self.bwd_end.record()                                   # the backward's last kernel is done here
+            torch.cuda.current_stream().wait_stream(self.side)
+
+    lib = _lib.lib()
+    dev = torch.device("cuda")
+    torch.manual_seed(980616)
+    m = PriGumbelModel(1.0, contract="W", dropout=0.1).to(dev).set_compute_dtype(torch.bfloat16)
+    B = args.batch
+    gen = torch.Generator(device=dev).manual_seed(7)
+    batch = {"eeg": torch.randn(B, 64, 256, generator=gen, device=dev),
+             "act": torch.randn(B, 32, generator=gen, device=dev) * 0.5}
+    labels = (torch.rand(B, generator=gen, device=dev) < 0.66).long()
+    reserves = [int(x) for x in args.reserve.split(",")]
+    modes = [(r, on) for r in reserves for on in (False, True)]
+    trainers = {mode: PriGumbelTrainer(m.engine, lr=1e-6, reducer=ProxyReducer(mode[1])) for mode in modes}
+    times = {mode: [] for mode in modes}
+    stats = {mode: [] for mode in modes}
+    old = lib.eegf_tune(13, 0)
+    try:
+        for _ in range(args.rounds):
+            for mode in modes:
+                lib.eegf_tune(13, mode[0])
+                tr = trainers[mode]
+                for _ in range(2):
+                    tr.step(batch, labels)
+                torch.cuda.synchronize()
+                tr.reduce.recs = []
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                per_step = []
+                for _ in range(args.steps):
+                    tr.reduce.recs = []
+                    tr.step(batch, labels)
+                    per_step.append((tr.reduce.recs, tr.reduce.bwd_end))
+                e.record()
+                torch.cuda.synchronize()
+                times[mode].append(s.elapsed_time(e) / args.steps)
+                for recs, end in per_step:
+                    for issue, ps, pe, nbytes in recs:
+                        stats[mode].append({"delay_ms": issue.elapsed_time(ps), "dur_ms": ps.elapsed_time(pe),
+                                            "slack_ms": pe.elapsed_time(end), "bytes": nbytes})
+    finally:
+        lib.eegf_tune(13, old)
+    out = {"workload": f"PriGumbel B={B} bf16 step", "wgs": args.wgs, "passes": args.passes, "modes": []}
+    for mode in modes:
+        t = sorted(times[mode])
+        med = t[len(t) // 2]
+        row = {"cu_reserve": mode[0], "proxy": mode[1], "ms_per_step": round(med, 3),
+               "samples_per_s": round(B / med * 1e3, 1), "all_ms": [round(x, 3) for x in times[mode]]}
+        st = stats[mode]
+        if st:
+            tot = sum(x["bytes"] for x in st)
+            before = sum(x["bytes"] for x in st if x["slack_ms"] >= 0)
+            row.update({"ranges_per_step": len(st) // (args.rounds * args.steps),
+                        "bytes_done_before_bwd_end": round(before / tot, 3),
+                        "median_delay_ms": round(sorted(x["delay_ms"] for x in st)[len(st) // 2], 3),
+                        "median_dur_ms": round(sorted(x["dur_ms"] for x in st)[len(st) // 2], 3),
+                        "max_overhang_ms": round(max(-x["slack_ms"] for x in st), 3)})
+        out["modes"].append(row)
+        print(json.dumps(row), flush=True)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,60 @@
+"""Issue cost of single VALU instructions on gfx950 (tools/ubench.hip; build: bash tools/ubench_build.sh).
+Prints cycles per instruction (s_memtime delta / instructions, median over waves) at 1 and 2 waves
+per SIMD.  Usage: python tools/ubench.py"""
+import ctypes
+import sys
+from pathlib import Path
+
+import torch
+
+OPS = ["v_add_u32", "v_mul_lo_u32", "v_mul_hi_u32", "v_fma_f32", "v_xor_b32", "v_mad_u64_u32", "v_exp_f32",
+       "v_pk_fma_f32", "v_mul_u32_u24", "v_rcp_f32"]
+
+
+def main():
+    lib = ctypes.CDLL(str(Path(__file__).resolve().parent / "libubench.so"))
+    blocks, iters = 256, 2000
+    torch.zeros(1, device="cuda")
+    for threads in (256,):
+        for op, name in enumerate(OPS):
+            cyc = torch.zeros(blocks * threads // 64, dtype=torch.int64, device="cuda")
+            sink = torch.zeros(blocks * threads, dtype=torch.int32, device="cuda")
+            for _ in range(2):
+                rc = lib.ubench(op, blocks, threads, iters, ctypes.c_void_p(cyc.data_ptr()),
+                                ctypes.c_void_p(sink.data_ptr()))
+                assert rc == 0, rc
+            torch.cuda.synchronize()
+            c = cyc.double().sort().values
+            print(f"{name:16s} waves/SIMD {threads // 256}: {float(c[len(c) // 2]) / (iters * 8):6.2f} cyc/inst",
+                  flush=True)
+
+
+def dma():
+    """LDS-DMA source pattern (ubench.hip dma_kernel): 16 rows x 64 B vs 8 rows x 128 B per wave-instruction"""
+    lib = ctypes.CDLL(str(Path(__file__).resolve().parent / "libubench.so"))
+    K = 768
+    for blocks in (256,):
+        A = torch.randn(blocks * 256, K, device="cuda").to(torch.bfloat16)
+        for rounds in (1, 4):
+            for pat in (0, 1, 0, 1):
+                cyc = torch.zeros(blocks, dtype=torch.int64, device="cuda")
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                lib.ubench_dma(pat, blocks, ctypes.c_void_p(A.data_ptr()), K, rounds, ctypes.c_void_p(cyc.data_ptr()))
+                torch.cuda.synchronize()
+                s.record()
+                rc = lib.ubench_dma(pat, blocks, ctypes.c_void_p(A.data_ptr()), K, rounds, ctypes.c_void_p(cyc.data_ptr()))
+                e.record()
+                torch.cuda.synchronize()
+                assert rc == 0, rc
+                ms = s.elapsed_time(e)
+                nbytes = A.numel() * 2 * rounds
+                c = cyc.double().sort().values
+                print(f"dma pat {pat} ({'16 rows x 64 B' if pat == 0 else '8 rows x 128 B'}) rounds {rounds}: "
+                      f"{ms * 1e3:8.1f} us  {nbytes / ms / 1e6:7.1f} GB/s  median {float(c[len(c) // 2]) / (nbytes / blocks):.3f} "
+                      f"cyc/B per CU", flush=True)
+
+
+if __name__ == "__main__":
+    if "--dma" in sys.argv:
+        sys.exit(dma())
+    sys.exit(main())
