@@ -68,8 +68,9 @@ def _overlap_worker(rank, world, port, q):
     r.begin(a, ["l1.w", "l1.b", "l0.w", "l0.b"])
     r.ready(["l1.w"])                    # issued early (async), 4 buckets of <= 100
     r.ready(["l0.w", "l1.w"])            # l1.w already issued: ignored
-    r.finish(lo, hi)                     # l1.b, l0.b, then wait + 1/N
+    r.finish(lo, hi)                     # l1.b + l0.b staged into one collective, then wait + 1/N
     out = {n: a.gview(n).flatten().tolist() for n, _ in specs}
+    assert r.n_coalesced == 1
     q.put((rank, out, r.log))
     dist.barrier()
     dist.destroy_process_group()
