@@ -76,6 +76,8 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-baseline-only", action="store_true",
                     help="time only the CPU baseline (e.g. --cpu-batch 256 --cpu-iters 3, BASELINE.md §3) and print "
                          "its JSON; profiles/" + "cpu_baseline_b256.json holds that run for the bench line")
+    ap.add_argument("--cpu-baseline-out", default="",
+                    help="with --cpu-baseline-only: also merge the result into this JSON file under the variant's key")
     ap.add_argument("--master-port", type=int, default=29531)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N > 1: nccl (= RCCL, one GPU per rank) or gloo (device "
@@ -251,7 +253,13 @@ def main():
     sys.path.insert(0, str(ROOT / "eeg-multimodal_amd"))
     sys.path.insert(0, str(ROOT))
     if args.cpu_baseline_only:
-        print(json.dumps(cpu_baseline(args.variant, args.cpu_batch, args.cpu_iters)), flush=True)
+        cb = cpu_baseline(args.variant, args.cpu_batch, args.cpu_iters)
+        print(json.dumps(cb), flush=True)
+        if args.cpu_baseline_out:
+            f = Path(args.cpu_baseline_out)
+            d = json.loads(f.read_text()) if f.exists() else {}
+            d[args.variant] = cb
+            f.write_text(json.dumps(d, indent=1) + "\n")
         return
     import torch
     import torch.distributed as dist

@@ -687,6 +687,9 @@ __global__ void __launch_bounds__(NT, 1) gemm8_kernel(BigArgs g) {
 #ifndef EEGF_W_READS
 #define EEGF_W_READS 0
 #endif
+#ifndef EEGF_W_STAGGER
+#define EEGF_W_STAGGER 0
+#endif
 constexpr int BK4 = 32, NT4 = 256, SLOT4 = 2 * TM * BK4;   // elements per ring slot (A + B, 32 KB)
 constexpr int NSLOT4 = 5;                                     // ring depth: 5 x 32 KB = the 160 KB of LDS
 static_assert(NSLOT4 * SLOT4 >= TM * LDC, "the epilogue tile reuses the ring");
@@ -879,25 +882,31 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
       }
     };
     // group s: the non-MFMA work sits in the shadows of the group's first MFMAs
+    // EEGF_W_STAGGER 1: wave w issues its LDS-DMA of group s after the group's MFMA 2 w (as gemm4p's
+    // EEGF_P_STAGGER)
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       mma(s, 0);
       rd_next(s, 0);
+      if (EEGF_W_STAGGER && st && wave == 0) stage_part(sA, sB, slot, s);
       __builtin_amdgcn_sched_barrier(0);
       mma(s, 1);
       rd_next(s, 1);
       __builtin_amdgcn_sched_barrier(0);
       mma(s, 2);
-      if (st) stage_part(sA, sB, slot, s);
+      if (EEGF_W_STAGGER ? st && wave == 1 : st) stage_part(sA, sB, slot, s);
       __builtin_amdgcn_sched_barrier(0);
       mma(s, 3);
       rd_next(s, 3);
       __builtin_amdgcn_sched_barrier(0);
       mma(s, 4);
+      if (EEGF_W_STAGGER && st && wave == 2) stage_part(sA, sB, slot, s);
       __builtin_amdgcn_sched_barrier(0);
       mma(s, 5);
       __builtin_amdgcn_sched_barrier(0);
       mma(s, 6);
+      if (EEGF_W_STAGGER && st && wave == 3) stage_part(sA, sB, slot, s);
+      __builtin_amdgcn_sched_barrier(0);
       mma(s, 7);
       // RS: row sums of this K-tile's A rows 16 s .. (lane & 15 -> row, every D column the same sum);
       // compiler-visible MFMA (hazards against the VALU reads at the end are the compiler's)
@@ -1043,11 +1052,97 @@ DEV void load_tile16(uint4 (&c)[8][4], const bf16* const (&p)[8]) {
       : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "v"(p[4]), "v"(p[5]), "v"(p[6]), "v"(p[7])
       : "memory");
 }
+// Epilogue of the persistent 256x256 kernels (gemm4p / gemm4q): bias / GELU / GELU' / aux product /
+// beta C from the AGPR accumulators straight to global memory in the widened 16-B store layout.
+// biasv: the lane's bias quads (HAS_BIAS); mrow = m0 + wm 128 + (lane & 15).
+template <int EPI, bool ACC>
+DEV void p_store_tile(const BigArgs& g, f32x4 (&acc)[8][8], const f32x4 (&biasv)[8], int mrow, int n0, int wn,
+                      int lane) {
+  constexpr bool HAS_BIAS = EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_D;
+  constexpr bool IN_EPI = (EPI == EPI_NONE && ACC) || EPI == EPI_MUL_AUX;
+  // Stores: the epilogue is store-ISSUE-bound (0.25 MB per CU per tile with GELU': ~240 of 490 us per
+  // launch went to 8-B stores, profiles/r3q_exp.log), so column blocks j = 2 jp, 2 jp + 1 are paired:
+  // one v_permlane16_swap per dword gives lanes g even 8 contiguous columns of block 2 jp and lanes g
+  // odd those of block 2 jp + 1 (cdna_hip_programming.md T21, 16-lane form) -> one 16-B store each.
+  // The swap is an involution: applied to an input tile read in that layout it restores the
+  // accumulator layout.
+  const int nst = n0 + wn * 128 + 16 * g_odd(lane) + 8 * (lane >> 5);     // + 32 jp
+  constexpr bool in_tile = IN_EPI;
+  uint4 cin[8][4];
+  if (IN_EPI && in_tile) {
+    const bf16* src = EPI == EPI_MUL_AUX ? g.aux : (const bf16*)g.C;
+    const long ld = EPI == EPI_MUL_AUX ? g.ldaux : g.ldc;
+    const bf16* rows[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) rows[i] = src + (long)(mrow + 16 * i) * ld + nst;
+    load_tile16(cin, rows);
+  }
+
+  bf16* Cb = (bf16*)g.C;
+  auto st16 = [&](bf16* base, long ld, long m, int jp, bf16x4 a, bf16x4 b) {
+    uint2 ua = __builtin_bit_cast(uint2, a), ub = __builtin_bit_cast(uint2, b);
+    const auto rx = __builtin_amdgcn_permlane16_swap(ua.x, ub.x, false, false);
+    const auto ry = __builtin_amdgcn_permlane16_swap(ua.y, ub.y, false, false);
+    const u32x4 d = {rx[0], ry[0], rx[1], ry[1]};
+    bf16* pp = base + m * ld + nst + 32 * jp;
+    // non-temporal stores (eegf_tune key 12): 3-4 % off the store-bound epilogues, profiles/r4a_pol.log
+    if (g.store_nt) asm volatile("global_store_dwordx4 %0, %1, off nt" :: "v"(pp), "v"(d) : "memory");
+    else *(u32x4*)pp = d;
+  };
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const long m = mrow + 16 * i;
+#pragma unroll
+    for (int jp = 0; jp < 4; ++jp) {
+      bf16x4 o[2], o2[2], ci[2];
+      if (IN_EPI && in_tile) {     // input chunk back to the accumulator layout (blocks 2 jp, 2 jp + 1)
+        const uint4 c4 = cin[i][jp];
+        const auto rx = __builtin_amdgcn_permlane16_swap(c4.x, c4.z, false, false);
+        const auto ry = __builtin_amdgcn_permlane16_swap(c4.y, c4.w, false, false);
+        ci[0] = __builtin_bit_cast(bf16x4, make_uint2(rx[0], ry[0]));
+        ci[1] = __builtin_bit_cast(bf16x4, make_uint2(rx[1], ry[1]));
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int j = 2 * jp + h;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = g.alpha * acc[i][j][r] + (HAS_BIAS ? biasv[j][r] : 0.f);
+          if (IN_EPI && in_tile) {
+            if (EPI == EPI_MUL_AUX) v[r] *= (float)ci[h][r];
+            else v[r] += g.beta * (float)ci[h][r];
+          }
+        }
+        if (EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_D) {
+          f32x2 gl0, gl1, gd0, gd1;
+          gelu2(f32x2{v[0], v[1]}, gl0, EPI == EPI_BIAS_GELU_D ? &gd0 : nullptr);
+          gelu2(f32x2{v[2], v[3]}, gl1, EPI == EPI_BIAS_GELU_D ? &gd1 : nullptr);
+          if (EPI == EPI_BIAS_GELU_D) {
+            o2[h][0] = (bf16)gd0.x; o2[h][1] = (bf16)gd0.y; o2[h][2] = (bf16)gd1.x; o2[h][3] = (bf16)gd1.y;
+          } else {     // pre-activation
+            o2[h][0] = (bf16)v[0]; o2[h][1] = (bf16)v[1]; o2[h][2] = (bf16)v[2]; o2[h][3] = (bf16)v[3];
+          }
+          o[h][0] = (bf16)gl0.x; o[h][1] = (bf16)gl0.y; o[h][2] = (bf16)gl1.x; o[h][3] = (bf16)gl1.y;
+        } else {
+          o[h][0] = (bf16)v[0]; o[h][1] = (bf16)v[1]; o[h][2] = (bf16)v[2]; o[h][3] = (bf16)v[3];
+        }
+      }
+      if ((EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_D) && (EPI == EPI_BIAS_GELU_D || g.aux))
+        st16(g.aux, g.ldaux, m, jp, o2[0], o2[1]);
+      st16(Cb, g.ldc, m, jp, o[0], o[1]);
+    }
+  }
+}
+
 #ifndef EEGF_P_READS
 #define EEGF_P_READS 0
 #endif
 #ifndef EEGF_P_PROBE
 #define EEGF_P_PROBE 0
+#endif
+#ifndef EEGF_P_STAGGER
+#define EEGF_P_STAGGER 0
 #endif
 template <bool BKC, int EPI, bool ACC = false>     // ACC: EPI_NONE with C = alpha A B^T + beta C
 __global__ void __launch_bounds__(NT4, 1) gemm4p_kernel(BigArgs g) {
@@ -1175,7 +1270,7 @@ __global__ void __launch_bounds__(NT4, 1) gemm4p_kernel(BigArgs g) {
       // lgkmcnt(0) ahead of the barrier finds them landed; 0: one fa + one fb per group (fb[7] read in
       // group 7, ~6 MFMAs before the wait)
       // EEGF_P_PROBE (diagnostic builds only, results wrong): 1 no staging after the first K-tiles,
-      // 2 = 1 + no per-K-tile waits or barrier
+      // 2 = 1 + no per-K-tile waits or barrier, 3 staging as built with no per-K-tile vmcnt waits
       auto rd_next = [&](int s, int jj) __attribute__((always_inline)) {
         if (!more) return;
         if (EEGF_P_READS == 0) {
@@ -1190,25 +1285,33 @@ __global__ void __launch_bounds__(NT4, 1) gemm4p_kernel(BigArgs g) {
           if (jj == 1) fa[H ^ 1][2 * s - 3] = rdA(nimg, 2 * s - 3);
         }
       };
+      // EEGF_P_STAGGER 1: wave w issues its LDS-DMA of group s after the group's MFMA 2 w, so at any moment
+      // one wave of the CU is issuing one (the waves run the K-tile in lockstep: with the DMA at the same
+      // place in every wave, four queue for the CU's address unit at once and stall their MFMA streams)
+      const bool stw = st && EEGF_P_PROBE != 1 && EEGF_P_PROBE != 2;
 #pragma unroll
       for (int s = 0; s < 8; ++s) {
         mma(s, 0);
         rd_next(s, 0);
+        if (EEGF_P_STAGGER && stw && wave == 0) stage_part(sA, sB, slot, s);
         __builtin_amdgcn_sched_barrier(0);
         mma(s, 1);
         rd_next(s, 1);
         __builtin_amdgcn_sched_barrier(0);
         mma(s, 2);
-        if (st && EEGF_P_PROBE == 0) stage_part(sA, sB, slot, s);
+        if (EEGF_P_STAGGER ? stw && wave == 1 : stw) stage_part(sA, sB, slot, s);
         __builtin_amdgcn_sched_barrier(0);
         mma(s, 3);
         rd_next(s, 3);
         __builtin_amdgcn_sched_barrier(0);
         mma(s, 4);
+        if (EEGF_P_STAGGER && stw && wave == 2) stage_part(sA, sB, slot, s);
         __builtin_amdgcn_sched_barrier(0);
         mma(s, 5);
         __builtin_amdgcn_sched_barrier(0);
         mma(s, 6);
+        if (EEGF_P_STAGGER && stw && wave == 3) stage_part(sA, sB, slot, s);
+        __builtin_amdgcn_sched_barrier(0);
         mma(s, 7);
       }
       if constexpr (EEGF_P_PROBE == 2) {
@@ -1217,7 +1320,9 @@ __global__ void __launch_bounds__(NT4, 1) gemm4p_kernel(BigArgs g) {
       }
       // K-tile k + 2 retired (its fragments are read in the next K-tile): skipped when it landed before
       // the tile started (cross-staged, k + 2 <= 4) or when there is no such K-tile of this tile
-      if (!(landed && k < NSLOT4 - 2) && k + 2 < nk) {
+      if (EEGF_P_PROBE == 3) {
+        // probe 3: LDS-DMA issued as built, never waited for (results wrong): the DMA issue cost alone
+      } else if (!(landed && k < NSLOT4 - 2) && k + 2 < nk) {
         if (!TAIL || cross) vm_wait_tiles(NSLOT4 - 2);
         else vm_wait_tiles(max(0, min(nk - 1, k + NSLOT4) - (k + 2)));
       } else if (!cross && k + 2 >= nk) {
@@ -1263,79 +1368,7 @@ __global__ void __launch_bounds__(NT4, 1) gemm4p_kernel(BigArgs g) {
     // load_tile16 wait for them too)
     if (cross) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    // Stores: the epilogue is store-ISSUE-bound (0.25 MB per CU per tile with GELU': ~240 of 490 us per
-    // launch went to 8-B stores, profiles/r3q_exp.log), so column blocks j = 2 jp, 2 jp + 1 are paired:
-    // one v_permlane16_swap per dword gives lanes g even 8 contiguous columns of block 2 jp and lanes g
-    // odd those of block 2 jp + 1 (cdna_hip_programming.md T21, 16-lane form) -> one 16-B store each.
-    // The swap is an involution: applied to an input tile read in that layout it restores the
-    // accumulator layout.
-    const int nst = n0 + wn * 128 + 16 * g_odd(lane) + 8 * (lane >> 5);     // + 32 jp
-    constexpr bool in_tile = IN_EPI;
-    uint4 cin[8][4];
-    if (IN_EPI && in_tile) {
-      const bf16* src = EPI == EPI_MUL_AUX ? g.aux : (const bf16*)g.C;
-      const long ld = EPI == EPI_MUL_AUX ? g.ldaux : g.ldc;
-      const bf16* rows[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) rows[i] = src + (long)(mrow + 16 * i) * ld + nst;
-      load_tile16(cin, rows);
-    }
-
-    bf16* Cb = (bf16*)g.C;
-    auto st16 = [&](bf16* base, long ld, long m, int jp, bf16x4 a, bf16x4 b) {
-      uint2 ua = __builtin_bit_cast(uint2, a), ub = __builtin_bit_cast(uint2, b);
-      const auto rx = __builtin_amdgcn_permlane16_swap(ua.x, ub.x, false, false);
-      const auto ry = __builtin_amdgcn_permlane16_swap(ua.y, ub.y, false, false);
-      const u32x4 d = {rx[0], ry[0], rx[1], ry[1]};
-      bf16* pp = base + m * ld + nst + 32 * jp;
-      // non-temporal stores (eegf_tune key 12): 3-4 % off the store-bound epilogues, profiles/r4a_pol.log
-      if (g.store_nt) asm volatile("global_store_dwordx4 %0, %1, off nt" :: "v"(pp), "v"(d) : "memory");
-      else *(u32x4*)pp = d;
-    };
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const long m = mrow + 16 * i;
-#pragma unroll
-      for (int jp = 0; jp < 4; ++jp) {
-        bf16x4 o[2], o2[2], ci[2];
-        if (IN_EPI && in_tile) {     // input chunk back to the accumulator layout (blocks 2 jp, 2 jp + 1)
-          const uint4 c4 = cin[i][jp];
-          const auto rx = __builtin_amdgcn_permlane16_swap(c4.x, c4.z, false, false);
-          const auto ry = __builtin_amdgcn_permlane16_swap(c4.y, c4.w, false, false);
-          ci[0] = __builtin_bit_cast(bf16x4, make_uint2(rx[0], ry[0]));
-          ci[1] = __builtin_bit_cast(bf16x4, make_uint2(rx[1], ry[1]));
-        }
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int j = 2 * jp + h;
-          float v[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            v[r] = g.alpha * acc[i][j][r] + (HAS_BIAS ? biasv[j][r] : 0.f);
-            if (IN_EPI && in_tile) {
-              if (EPI == EPI_MUL_AUX) v[r] *= (float)ci[h][r];
-              else v[r] += g.beta * (float)ci[h][r];
-            }
-          }
-          if (EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_D) {
-            f32x2 gl0, gl1, gd0, gd1;
-            gelu2(f32x2{v[0], v[1]}, gl0, EPI == EPI_BIAS_GELU_D ? &gd0 : nullptr);
-            gelu2(f32x2{v[2], v[3]}, gl1, EPI == EPI_BIAS_GELU_D ? &gd1 : nullptr);
-            if (EPI == EPI_BIAS_GELU_D) {
-              o2[h][0] = (bf16)gd0.x; o2[h][1] = (bf16)gd0.y; o2[h][2] = (bf16)gd1.x; o2[h][3] = (bf16)gd1.y;
-            } else {     // pre-activation
-              o2[h][0] = (bf16)v[0]; o2[h][1] = (bf16)v[1]; o2[h][2] = (bf16)v[2]; o2[h][3] = (bf16)v[3];
-            }
-            o[h][0] = (bf16)gl0.x; o[h][1] = (bf16)gl0.y; o[h][2] = (bf16)gl1.x; o[h][3] = (bf16)gl1.y;
-          } else {
-            o[h][0] = (bf16)v[0]; o[h][1] = (bf16)v[1]; o[h][2] = (bf16)v[2]; o[h][3] = (bf16)v[3];
-          }
-        }
-        if ((EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_D) && (EPI == EPI_BIAS_GELU_D || g.aux))
-          st16(g.aux, g.ldaux, m, jp, o2[0], o2[1]);
-        st16(Cb, g.ldc, m, jp, o[0], o[1]);
-      }
-    }
+    p_store_tile<EPI, ACC>(g, acc, biasv, mrow, n0, wn, lane);
     if (!more_tiles) break;
     L = Ln;
     m0 = m0n;
@@ -1345,6 +1378,234 @@ __global__ void __launch_bounds__(NT4, 1) gemm4p_kernel(BigArgs g) {
     // cross-staged: the ring runs on (next tile's K-tile 0 sits in the slot after this tile's last)
     landed = cross;
     if (cross) slot0 = (slot0 + nk) % NSLOT4;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// gemm4q: gemm4p with every K-contiguous operand staged in WHOLE 128-B lines.  gemm4p's LDS-DMA
+// instruction covers 16 rows x 64 B of a K-contiguous operand (one 32-deep K-tile of each row: half
+// of every 128-B line it touches); from L2-resident sources the CU's LDS-DMA path moves 31 B/cycle in
+// that pattern and 46 B/cycle in 8 rows x 128 B (profiles/r4e_dma_line_pattern.log), while a 256x256
+// K-tile needs 32 KB per 1,024 MFMA cycles, so gemm4p's forward K-loop ran at the DMA ceiling (its
+// no-staging probe: FFN2 forward 283 -> 207 us, profiles/r4c_gemm_probe_ab.log).  Here:
+//   * the ring holds K-tile PAIRS (64 deep): 2 pair slots of 64 KB, each [256 rows][64 k] per
+//     K-contiguous operand (16-B chunk c of row r stored at c ^ (r & 7): conflict-free ds_read_b128),
+//     [64 k][256 cols] per k-major operand (gemm4p's swz_k image, two K-tiles stacked);
+//   * pair t + 2 is staged during the odd (second) K-tile of pair t into pair t's slot (free since
+//     the barrier that ended pair t's even K-tile) and waited for at the end of the next even K-tile:
+//     one vmcnt + one barrier per pair, none at odd K-tiles;
+//   * the same MFMA K order as gemm4p (bitwise identical results), the same epilogue (p_store_tile) and
+//     cross-tile staging (the last two odd K-tiles stage the next tile's pairs 0 and 1).
+// Needs K % 64 == 0 and K >= 128 (launch_big routes other shapes to gemm4p).
+constexpr int BKP = 64, PSLOT = 2 * TM * BKP;          // K per pair, elements per pair slot (64 KB)
+template <bool BKC, int EPI, bool ACC = false>
+__global__ void __launch_bounds__(NT4, 1) gemm4q_kernel(BigArgs g) {
+  constexpr bool HAS_BIAS = EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_D;
+  __shared__ __attribute__((aligned(16))) bf16 lds[2 * PSLOT];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int tiles_n = g.N / TN, tiles_m = g.M / TM, ntiles = tiles_m * tiles_n;
+  const int G = gridDim.x;
+  const int np = g.K / BKP;                            // pairs per tile (>= 2)
+  int L = xcd_remap(blockIdx.x, G);
+  if (L >= ntiles) return;
+
+  // Staging, 16 parts per pair and wave (8 A, 8 B), each one wave-instruction of 1 KB.
+  // K-contiguous part j: rows (8 wave + j) 8 + lane / 8, 16-B chunk lane & 7 of the row's 128 B, read from
+  // source chunk (lane & 7) ^ (row & 7); row & 7 = lane / 8 for every part, so one per-lane offset serves
+  // all parts (a part's first row is a uniform offset of the SGPR base).
+  // k-major part j: k-rows (8 wave + j) 2 + lane / 32 (512 B each), 16-B column chunk (lane & 31) ^
+  // swz_k(k); swz_k reads k bits 0, 1, 3 = lane / 32, j & 1, j >> 2: four per-lane offsets.
+  const int kr = lane >> 3;
+  const uint32_t voffA = (uint32_t)(((long)kr * g.lda + ((lane & 7) ^ kr) * 8) * 2);
+  uint32_t voffB[4];
+  if (BKC) {
+    voffB[0] = (uint32_t)(((long)kr * g.ldb + ((lane & 7) ^ kr) * 8) * 2);
+  } else {
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int j = (v & 1) | ((v >> 1) << 2);
+      const int k = (wave * 8 + j) * 2 + (lane >> 5);
+      voffB[v] = (uint32_t)(((long)(lane >> 5) * g.ldb + ((lane & 31) ^ swz_k(k)) * 8) * 2);
+    }
+  }
+  const long pstepB = BKC ? BKP : (long)BKP * g.ldb;
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr_of(lds));
+  auto stage_part = [&](const bf16* bA, const bf16* bB, int ps, int j) __attribute__((always_inline)) {
+    const int jj = j & 7, pr = wave * 8 + jj;
+    if (j < 8) {
+      glds16_asm_sa(bA + (long)pr * 8 * g.lda, voffA, lds0 + 2u * (ps * PSLOT + pr * 8 * BKP));
+    } else if (BKC) {
+      glds16_asm_sa(bB + (long)pr * 8 * g.ldb, voffB[0], lds0 + 2u * (ps * PSLOT + TM * BKP + pr * 8 * BKP));
+    } else {
+      glds16_asm_sa(bB + (long)pr * 2 * g.ldb, voffB[(jj & 1) | ((jj >> 2) << 1)],
+                    lds0 + 2u * (ps * PSLOT + TM * BKP + pr * 2 * TN));
+    }
+  };
+  auto tile_base = [&](int l, const bf16*& bA, const bf16*& bB, int& m0, int& n0) {
+    int tm, tn;
+    tile_coords(g, l, tiles_m, tiles_n, tm, tn);
+    m0 = __builtin_amdgcn_readfirstlane(tm * TM);
+    n0 = __builtin_amdgcn_readfirstlane(tn * TN);
+    bA = g.A + (long)m0 * g.lda;
+    bB = BKC ? g.B + (long)n0 * g.ldb : g.B + n0;
+  };
+  // fragments.  K-contiguous [256][64] image: half h of a pair (K-tile 2t + h) is chunk 4 h + fq of rows
+  // r0 + fr (r0 % 16 == 0, so the swizzle is fr & 7); k-major: gemm4p's rd_col offsets, half 1 32 k-rows on
+  const int fr = lane & 15, fq = lane >> 4;
+  const int offA0 = (wm * 128 + fr) * BKP + ((fq ^ (fr & 7)) << 3);
+  const int offA1 = (wm * 128 + fr) * BKP + (((4 + fq) ^ (fr & 7)) << 3);
+  const int offB0 = TM * BKP + (wn * 128 + fr) * BKP + ((fq ^ (fr & 7)) << 3);
+  const int offB1 = TM * BKP + (wn * 128 + fr) * BKP + (((4 + fq) ^ (fr & 7)) << 3);
+  int tB0[8], tB1[8];
+  if (!BKC) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int q = fr >> 2, p4 = fr & 3;
+      const int col = wn * 128 + 16 * i + 4 * p4, ch = col >> 3, off = col & 7;
+      const int ka = 8 * fq + q, kb = ka + 4;
+      tB0[i] = TM * BKP + ka * TN + (((ch ^ swz_k(ka)) << 3) | off);
+      tB1[i] = TM * BKP + kb * TN + (((ch ^ swz_k(kb)) << 3) | off);
+    }
+  }
+  auto rdA = [&](const bf16* img, auto Hc, int i) {
+    return *(const bf16x8*)(img + (decltype(Hc)::value ? offA1 : offA0) + i * 16 * BKP);
+  };
+  auto rdB = [&](const bf16* img, auto Hc, int i) {
+    constexpr int h = decltype(Hc)::value;
+    return BKC ? *(const bf16x8*)(img + (h ? offB1 : offB0) + i * 16 * BKP)
+               : rd_col_off(img + h * 32 * TN, tB0[i], tB1[i]);
+  };
+  using C0 = std::integral_constant<int, 0>;
+  using C1 = std::integral_constant<int, 1>;
+
+  const bf16* baseA;
+  const bf16* baseB;
+  int m0, n0;
+  tile_base(L, baseA, baseB, m0, n0);
+#pragma unroll 1
+  for (int j = 0; j < 16; ++j) stage_part(baseA, baseB, 0, j);                 // pair 0 -> slot 0
+#pragma unroll 1
+  for (int j = 0; j < 16; ++j) stage_part(baseA + BKP, baseB + pstepB, 1, j);  // pair 1 -> slot 1
+  f32x4 acc[8][8];
+  int ps0 = 0;                  // pair slot of the tile's pair 0
+  bool landed = false;          // the tile's pairs 0 and 1 retired (cross-staged and waited for)
+  for (;;) {
+    const int Ln = L + G;
+    const bool more_tiles = Ln < ntiles;
+    int m0n = 0, n0n = 0;
+    const bf16* nA = nullptr;
+    const bf16* nB = nullptr;
+    if (more_tiles) tile_base(Ln, nA, nB, m0n, n0n);
+    if (!landed) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");      // pair 0 (pair 1 younger)
+    raw_barrier();
+    bf16x8 fa[2][8], fb[2][8];
+    {
+      const bf16* img0 = lds + ps0 * PSLOT;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        fa[0][i] = rdA(img0, C0{}, i);
+        fb[0][i] = rdB(img0, C0{}, i);
+      }
+    }
+    // K-tile s = 2 t + H of pair t (slot ps = (ps0 + t) & 1): its fragments are in fa / fb[H]; the next
+    // K-tile's are read into [H ^ 1] (H = 0: the same slot's half 1; H = 1: pair t + 1's half 0); the odd
+    // K-tile stages pair t + 2 (or the next tile's pair t + 2 - np) into slot ps
+    // TAIL (the last two pairs): whether there is a next K-tile to read and what to stage are decided at
+    // run time; in the steady state (t + 2 < np) both are compile-time true, so the K-tile body carries no
+    // branch and hipcc's waitcnt pass sees straight-line LDS reads
+    auto ktile = [&](auto Hc, int t, auto Ic, auto Tc) __attribute__((always_inline)) {
+      constexpr int H = decltype(Hc)::value;
+      constexpr bool INIT = decltype(Ic)::value, TAIL = decltype(Tc)::value;
+      const int ps = (ps0 + t) & 1;
+      const bool more = !TAIL || H == 0 || t + 1 < np;
+      const bf16* nimg = lds + (H == 0 ? ps : ps ^ 1) * PSLOT;
+      const bool own = !TAIL || t + 2 < np;
+      const bool st = H == 1 && (own || more_tiles);
+      const bf16* sA = own ? baseA + (t + 2) * BKP : nA + (t + 2 - np) * BKP;
+      const bf16* sB = own ? baseB + (t + 2) * pstepB : nB + (t + 2 - np) * pstepB;
+      auto mma = [&](int s8, int jj) {
+        if (INIT) mma16_acc0(acc[s8][jj], fb[H][jj], fa[H][s8]);
+        else mma16_acc(acc[s8][jj], fb[H][jj], fa[H][s8]);
+      };
+      using HN = std::integral_constant<int, H ^ 1>;
+#pragma unroll
+      for (int s8 = 0; s8 < 8; ++s8) {
+        mma(s8, 0);
+        if (more) fa[H ^ 1][s8] = rdA(nimg, HN{}, s8);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(s8, 1);
+        if (more) fb[H ^ 1][s8] = rdB(nimg, HN{}, s8);
+        __builtin_amdgcn_sched_barrier(0);
+        if (EEGF_P_STAGGER) {     // wave w: its two parts after MFMAs 2 w and 2 w + 1 of the group
+          if (H == 1 && st && wave == 0) stage_part(sA, sB, ps, 2 * s8);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        mma(s8, 2);
+        if (EEGF_P_STAGGER ? H == 1 && st && wave == 1 : H == 1 && st) stage_part(sA, sB, ps, 2 * s8);
+        if (EEGF_P_STAGGER && H == 1 && st && wave == 0) stage_part(sA, sB, ps, 2 * s8 + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(s8, 3);
+        if (EEGF_P_STAGGER && H == 1 && st && wave == 1) stage_part(sA, sB, ps, 2 * s8 + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(s8, 4);
+        if (EEGF_P_STAGGER ? H == 1 && st && wave == 2 : H == 1 && st) stage_part(sA, sB, ps, 2 * s8 + (EEGF_P_STAGGER ? 0 : 1));
+        __builtin_amdgcn_sched_barrier(0);
+        mma(s8, 5);
+        if (EEGF_P_STAGGER && H == 1 && st && wave == 2) stage_part(sA, sB, ps, 2 * s8 + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(s8, 6);
+        if (EEGF_P_STAGGER && H == 1 && st && wave == 3) stage_part(sA, sB, ps, 2 * s8);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(s8, 7);
+        if (EEGF_P_STAGGER && H == 1 && st && wave == 3) stage_part(sA, sB, ps, 2 * s8 + 1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (H == 0) {
+        // pair t + 1 (staged during pair t - 1's odd K-tile, the only DMAs in flight) must have landed
+        // before the next K-tile reads its fragments; the barrier also frees pair t's slot for pair t + 2
+        if ((!TAIL || t + 1 < np) && !(landed && t == 0)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        raw_barrier();
+      }
+    };
+    using F = std::false_type;
+    using T = std::true_type;
+    if (np > 2) {
+      ktile(C0{}, 0, T{}, F{});
+      ktile(C1{}, 0, F{}, F{});
+    } else {
+      ktile(C0{}, 0, T{}, T{});
+      ktile(C1{}, 0, F{}, T{});
+    }
+#pragma unroll 1
+    for (int t = 1; t + 2 < np; ++t) {
+      ktile(C0{}, t, F{}, F{});
+      ktile(C1{}, t, F{}, F{});
+    }
+#pragma unroll 1
+    for (int t = max(1, np - 2); t < np; ++t) {
+      ktile(C0{}, t, F{}, T{});
+      ktile(C1{}, t, F{}, T{});
+    }
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+    const int mrow = m0 + wm * 128 + (lane & 15);
+    const int ncol = n0 + wn * 128 + 4 * (lane >> 4);
+    f32x4 biasv[8];
+    if (HAS_BIAS) load_bias8(biasv, g.bias + ncol);
+    // the next tile's pairs 0 and 1 (cross-staged) retired before the first store
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    p_store_tile<EPI, ACC>(g, acc, biasv, mrow, n0, wn, lane);
+    if (!more_tiles) break;
+    L = Ln;
+    m0 = m0n;
+    n0 = n0n;
+    baseA = nA;
+    baseB = nB;
+    landed = true;
+    ps0 = (ps0 + np) & 1;
   }
 }
 
@@ -1524,6 +1785,9 @@ int g_gemm4h = [] { const char* e = getenv("EEGF_GEMM4H"); return e ? atoi(e) : 
 // (QKV 265 -> 293 us, profiles/r3f_p_ab.log)
 int g_store_nt = [] { const char* e = getenv("EEGF_STORE_NT"); return e ? atoi(e) : 0; }();   // eegf_tune key 12
 int g_gemm4p = [] { const char* e = getenv("EEGF_GEMM4P"); return e ? atoi(e) : 1; }();
+// key 14: the persistent GEMM's staging: 1 (default) whole 128-B lines (gemm4q) where K % 64 == 0 and
+// K >= 128, 0 gemm4p's 64-B half lines everywhere
+int g_gemm4q = [] { const char* e = getenv("EEGF_GEMM4Q"); return e ? atoi(e) : 1; }();
 int cu_count() {
   static const int cus = [] {
     int dev = 0, n = 256;
@@ -1558,10 +1822,16 @@ int launch_big(const BigArgs& a, int splits, hipStream_t s) {
       ap.store_nt = g_store_nt;
       bool acc = false;
       if constexpr (EPI == EPI_NONE) acc = a.beta != 0.f;
+      // whole-line staging (gemm4q) for the forward layout (both operands K-contiguous) where K splits
+      // into >= 2 pairs of K-tiles: 3-4 % faster there; with a k-major B (input gradients, already whole
+      // lines) its shallower 2-pair ring lost 1-6 % (profiles/r4i_gemm_ab.log), so those stay on gemm4p
+      const bool q = g_gemm4q == 1 && BKC && a.K % BKP == 0 && a.K >= 2 * BKP;
       if constexpr (EPI == EPI_NONE) {
-        if (acc) hipLaunchKernelGGL((gemm4p_kernel<BKC, EPI, true>), grid, dim3(NT4), 0, s, ap);
+        if (acc && q) hipLaunchKernelGGL((gemm4q_kernel<BKC, EPI, true>), grid, dim3(NT4), 0, s, ap);
+        if (acc && !q) hipLaunchKernelGGL((gemm4p_kernel<BKC, EPI, true>), grid, dim3(NT4), 0, s, ap);
       }
-      if (!acc) hipLaunchKernelGGL((gemm4p_kernel<BKC, EPI>), grid, dim3(NT4), 0, s, ap);
+      if (!acc && q) hipLaunchKernelGGL((gemm4q_kernel<BKC, EPI>), grid, dim3(NT4), 0, s, ap);
+      if (!acc && !q) hipLaunchKernelGGL((gemm4p_kernel<BKC, EPI>), grid, dim3(NT4), 0, s, ap);
       return (int)hipGetLastError();
     }
   }
@@ -1796,6 +2066,7 @@ extern "C" int eegf_tune(int key, int value) {
   if (key == 10) { const int o = g_ln_fwd768; g_ln_fwd768 = value; return o; }
   if (key == 12) { const int o = g_store_nt; if (value < 0 || value > 1) return EEGF_ERR_ARG; g_store_nt = value; return o; }
   if (key == 11) { const int o = g_gemm4p; if (value < 0 || value > 3) return EEGF_ERR_ARG; g_gemm4p = value; return o; }
+  if (key == 14) { const int o = g_gemm4q; if (value < 0 || value > 1) return EEGF_ERR_ARG; g_gemm4q = value; return o; }
   if (key == 13) { const int o = g_cu_reserve; if (value < 0 || value >= cu_count()) return EEGF_ERR_ARG; g_cu_reserve = value; return o; }
   if (key == 6) { const int o = g_ln_rpw; if (value < 1 || value > 64) return EEGF_ERR_ARG; g_ln_rpw = value; return o; }
   return EEGF_ERR_ARG;

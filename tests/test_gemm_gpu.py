@@ -559,8 +559,9 @@ def test_gemm_persistent_fwd(epi, M, N, K):
     b = torch.randn(N, device="cuda")
     e = "bias_gelu" if epi == "gelu_noaux" else epi
     outs = []
-    for key in (1, 0):
-        old = _tune(11, key)
+    # (key 11, key 14): persistent with whole-line staging (gemm4q, default), persistent gemm4p, non-persistent
+    for k11, k14 in ((1, 1), (0, 1), (1, 0)):
+        old, old14 = _tune(11, k11), _tune(14, k14)
         try:
             aux = torch.full((M, N), float("nan"), device="cuda", dtype=torch.bfloat16) \
                 if epi in ("bias_gelu", "bias_gelu_d") else None
@@ -569,6 +570,11 @@ def test_gemm_persistent_fwd(epi, M, N, K):
             outs.append((out, aux))
         finally:
             _tune(11, old)
+            _tune(14, old14)
+    # gemm4q and gemm4p: the same MFMA K order and epilogue, bit for bit
+    assert torch.equal(outs[0][0], outs[2][0])
+    if outs[0][1] is not None:
+        assert torch.equal(outs[0][1], outs[2][1])
     out, aux = outs[0]
     ref, pre = _ref_epi(x.double() @ w.double().t(), e, None if epi == "none" else b, None, 1.0)
     _check(out, ref, torch.bfloat16)
@@ -593,8 +599,8 @@ def test_gemm_persistent_dgrad(epi, M, N, K):
     aux = torch.randn(M, N, device="cuda").to(torch.bfloat16) if epi == "mul_aux" else None
     c0 = torch.randn(M, N, device="cuda").to(torch.bfloat16)
     outs = []
-    for key in (1, 0):
-        old = _tune(11, key)
+    for k11, k14 in ((1, 1), (0, 1), (1, 0)):
+        old, old14 = _tune(11, k11), _tune(14, k14)
         try:
             if epi == "none_beta":
                 out = c0.clone()
@@ -605,6 +611,8 @@ def test_gemm_persistent_dgrad(epi, M, N, K):
             outs.append(out)
         finally:
             _tune(11, old)
+            _tune(14, old14)
+    assert torch.equal(outs[0], outs[2])          # gemm4q == gemm4p bit for bit
     if epi == "none_beta":
         ref = c0.double() + dy.double() @ w.double()
     else:

@@ -7,9 +7,12 @@ TAG=$1 ROUNDS=$2 LIBS=$3; shift 3
 O=gpurun_out; mkdir -p $O; export PYTHONUNBUFFERED=1
 for r in $(seq 1 $ROUNDS); do
   for v in $LIBS; do
-    lib=""; [ $v != cur ] && lib=ab/lib$v.so
+    # cur = the in-tree library; NAME=VALUE = the in-tree library under that environment variable; else ab/lib<v>.so
+    # <lib>@NAME=VALUE: ab/lib<lib>.so under that environment variable
+    lib=""; envs=""
+    case $v in cur) ;; *@*) lib=ab/lib${v%%@*}.so; envs=${v#*@} ;; *=*) envs=$v ;; *) lib=ab/lib$v.so ;; esac
     echo "== $v $r" >> $O/${TAG}_gemm_ab.log
-    EEGF_LIB=$lib timeout -k 10 200 python -u tools/gemm_bench.py "$@" >> $O/${TAG}_gemm_ab.log 2>&1 || exit 1
+    env EEGF_LIB=$lib $envs timeout -k 10 200 python -u tools/gemm_bench.py "$@" >> $O/${TAG}_gemm_ab.log 2>&1 || exit 1
   done
 done
 python3 - "$O/${TAG}_gemm_ab.log" <<'PY'

@@ -86,12 +86,22 @@ extern "C" int ubench(int op, int blocks, int threads, int iters, long long* cyc
 //          K-tile pair every second K-tile
 // Same bytes, same instruction count; `rounds` passes over the same panel (L2-warm after the first).
 template <int PAT>
-__global__ void __launch_bounds__(256, 1) dma_kernel(const uint16_t* __restrict__ A, int K, int rounds, long long* cyc) {
+__global__ void __launch_bounds__(256, 1) dma_kernel(const uint16_t* __restrict__ A, int K, int rounds, int panels,
+                                                     long long* cyc) {
   __shared__ __attribute__((aligned(16))) uint16_t lds[5 * 256 * 32];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint16_t* panel = A + (long)blockIdx.x * 256 * K;
+  const uint16_t* panel = A + (long)(blockIdx.x % panels) * 256 * K;   // panels < grid: L2-shared sources
   typedef __attribute__((address_space(3))) void lv;
   const uint32_t l0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lv*)lds);
+  // raw buffer resource over the panel (gfx9 dword3 0x00020000), built from uniform values
+  typedef __attribute__((ext_vector_type(4))) uint32_t u32x4_t;
+  const uint64_t pb = (uint64_t)(uintptr_t)panel;
+  u32x4_t rsrc;
+  rsrc[0] = __builtin_amdgcn_readfirstlane((uint32_t)pb);
+  rsrc[1] = __builtin_amdgcn_readfirstlane((uint32_t)(pb >> 32) & 0xFFFFu);
+  rsrc[2] = 0xFFFFFFFFu;
+  rsrc[3] = 0x00020000u;
+  asm volatile("s_nop 4" ::: "memory");
   const long long t0 = __builtin_amdgcn_s_memtime();
   const int nk = K / 32;
   for (int r = 0; r < rounds; ++r) {
@@ -104,6 +114,26 @@ __global__ void __launch_bounds__(256, 1) dma_kernel(const uint16_t* __restrict_
           const uint16_t* src = panel + (long)row * K + kt * 32 + (lane & 3) * 8;
           const uint32_t dst = l0 + 2u * (slot * 256 * 32 + (wave * 4 + j) * 16 * 32);
           asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(dst) : "memory");
+        }
+      } else if (PAT == 2) {      // PAT 0's rows through the buffer path (MUBUF ... lds)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int row = (wave * 4 + j) * 16 + (lane >> 2);
+          const uint32_t voff = (uint32_t)(((long)row * K + kt * 32 + (lane & 3) * 8) * 2);
+          const uint32_t dst = l0 + 2u * (slot * 256 * 32 + (wave * 4 + j) * 16 * 32);
+          asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rsrc),
+                       "s"(dst) : "memory");
+        }
+      } else if (PAT == 3) {      // PAT 1's rows through the buffer path
+        if ((kt & 1) == 0) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int row = (wave * 8 + j) * 8 + (lane >> 3);
+            const uint32_t voff = (uint32_t)(((long)row * K + kt * 32 + (lane & 7) * 8) * 2);
+            const uint32_t dst = l0 + 2u * ((slot % 4) * 256 * 32 + (wave * 8 + j) * 8 * 64 % (256 * 32));
+            asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff),
+                         "s"(rsrc), "s"(dst) : "memory");
+          }
         }
       } else if ((kt & 1) == 0) {
 #pragma unroll
@@ -122,8 +152,11 @@ __global__ void __launch_bounds__(256, 1) dma_kernel(const uint16_t* __restrict_
   if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
 }
 
-extern "C" int ubench_dma(int pat, int blocks, const void* A, int K, int rounds, long long* cyc) {
-  if (pat == 0) hipLaunchKernelGGL(dma_kernel<0>, dim3(blocks), dim3(256), 0, 0, (const uint16_t*)A, K, rounds, cyc);
-  else hipLaunchKernelGGL(dma_kernel<1>, dim3(blocks), dim3(256), 0, 0, (const uint16_t*)A, K, rounds, cyc);
+extern "C" int ubench_dma(int pat, int blocks, const void* A, int K, int rounds, int panels, long long* cyc) {
+  const uint16_t* a = (const uint16_t*)A;
+  if (pat == 0) hipLaunchKernelGGL(dma_kernel<0>, dim3(blocks), dim3(256), 0, 0, a, K, rounds, panels, cyc);
+  else if (pat == 1) hipLaunchKernelGGL(dma_kernel<1>, dim3(blocks), dim3(256), 0, 0, a, K, rounds, panels, cyc);
+  else if (pat == 2) hipLaunchKernelGGL(dma_kernel<2>, dim3(blocks), dim3(256), 0, 0, a, K, rounds, panels, cyc);
+  else hipLaunchKernelGGL(dma_kernel<3>, dim3(blocks), dim3(256), 0, 0, a, K, rounds, panels, cyc);
   return (int)hipGetLastError();
 }

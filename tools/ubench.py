@@ -33,25 +33,27 @@ def dma():
     """LDS-DMA source pattern (ubench.hip dma_kernel): 16 rows x 64 B vs 8 rows x 128 B per wave-instruction"""
     lib = ctypes.CDLL(str(Path(__file__).resolve().parent / "libubench.so"))
     K = 768
-    for blocks in (256,):
-        A = torch.randn(blocks * 256, K, device="cuda").to(torch.bfloat16)
-        for rounds in (1, 4):
-            for pat in (0, 1, 0, 1):
+    blocks = 256
+    A = torch.randn(blocks * 256, K, device="cuda").to(torch.bfloat16)
+    for panels in (256, 8, 1):
+        for rounds in (4,):
+            for pat in (0, 1, 2, 3, 0, 1, 2, 3):
                 cyc = torch.zeros(blocks, dtype=torch.int64, device="cuda")
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                lib.ubench_dma(pat, blocks, ctypes.c_void_p(A.data_ptr()), K, rounds, ctypes.c_void_p(cyc.data_ptr()))
+                args = (pat, blocks, ctypes.c_void_p(A.data_ptr()), K, rounds, panels, ctypes.c_void_p(cyc.data_ptr()))
+                lib.ubench_dma(*args)
                 torch.cuda.synchronize()
                 s.record()
-                rc = lib.ubench_dma(pat, blocks, ctypes.c_void_p(A.data_ptr()), K, rounds, ctypes.c_void_p(cyc.data_ptr()))
+                rc = lib.ubench_dma(*args)
                 e.record()
                 torch.cuda.synchronize()
                 assert rc == 0, rc
                 ms = s.elapsed_time(e)
-                nbytes = A.numel() * 2 * rounds
+                per_cu = 256 * K * 2 * rounds
                 c = cyc.double().sort().values
-                print(f"dma pat {pat} ({'16 rows x 64 B' if pat == 0 else '8 rows x 128 B'}) rounds {rounds}: "
-                      f"{ms * 1e3:8.1f} us  {nbytes / ms / 1e6:7.1f} GB/s  median {float(c[len(c) // 2]) / (nbytes / blocks):.3f} "
-                      f"cyc/B per CU", flush=True)
+                print(f"dma pat {pat} ({['16 rows x 64 B global', '8 rows x 128 B global', '16 rows x 64 B buffer', '8 rows x 128 B buffer'][pat]}) panels {panels:3d} rounds "
+                      f"{rounds}: {ms * 1e3:8.1f} us  {per_cu * blocks / ms / 1e6:7.1f} GB/s  per CU "
+                      f"{per_cu / float(c[len(c) // 2]):.1f} B/cyc (s_memtime)", flush=True)
 
 
 if __name__ == "__main__":
