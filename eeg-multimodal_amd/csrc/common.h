@@ -60,14 +60,21 @@ DEV void glds16_asm_s(const void* base, uint32_t voff, const void* lds_base) {
 }
 // saddr form with a 32-bit LDS byte address (no generic->LDS pointer cast per call) and a base the
 // caller knows to be wave-uniform
+// EEGF_DMA_POL: cache-policy bits of the saddr LDS-DMA (diagnostic A/B builds; default none)
+#ifndef EEGF_DMA_POL
+#define EEGF_DMA_POL ""
+#endif
+#ifndef EEGF_DMA_NOP
+#define EEGF_DMA_NOP "3"      // diagnostic builds only: fewer is unsafe wherever the lint finds a VALU-written base
+#endif
 DEV void glds16_asm_sa(const void* base, uint32_t voff, uint32_t lds_addr) {
   // readfirstlane: a no-op on a base the compiler already keeps in SGPRs, and it keeps the "s"
   // constraint satisfiable when control flow elsewhere in the kernel makes it place the base in VGPRs
   const uint64_t b = (uint64_t)(uintptr_t)base;
   const uint64_t bu = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
                       (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
-  asm volatile("s_mov_b32 m0, %2\n\ts_nop 3\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(bu), "s"(lds_addr)
-               : "memory", "m0");
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop " EEGF_DMA_NOP "\n\tglobal_load_lds_dwordx4 %0, %1" EEGF_DMA_POL ::"v"(voff), "s"(bu),
+               "s"(lds_addr) : "memory", "m0");
 }
 DEV uint32_t lds_addr_of(const void* p) {
   typedef __attribute__((address_space(3))) void lv;

@@ -14,7 +14,14 @@ compared, on the SAME bf16 inputs and the replayed Philox dropout mask (tests/ph
 
 The kernel must match the emulation to within fp32 accumulation-order noise (the kernel implements
 exactly those roundings), and the emulation's distance to the exact result is the bf16 floor that any
-bf16-operand attention kernel has on these inputs.  The printed numbers are recorded in DESIGN.md §6.
+bf16-operand attention kernel has on these inputs.
+
+Measured (profiles/r4m_layer11_attention_localisation.log): cos(kernel, emulation) 1.000000 for O, dQ, dK,
+dV (relative error <= 9.3e-5), cos(kernel, exact) >= 0.999981 (dQ) and >= 0.999998 (O, dK, dV), and the
+query / key weight-gradient contributions of the checked samples 0.999999 / 0.999998 against float64.  The
+0.9952 worst Q/K weight-gradient cosine of test_production_gpu (bf16 engine vs fp32 engine) therefore does
+not come from the attention kernels: at layer 11 they are exact to bf16 rounding on their own inputs; it
+is the drift of those inputs (bf16 vs fp32 activations through 12 layers) that the engine comparison sees.
 """
 import numpy as np
 import pytest
@@ -138,6 +145,10 @@ def test_layer11_attention_within_bf16_rounding():
               f"cos(emulation, exact) {_cos(d['em'], d['ex']):.6f}  cos(kernel, exact) {_cos(d['k'], d['ex']):.6f}")
     for n, r in res.items():
         # the kernel is the emulation up to fp32 summation order and bf16 output rounding ties
-        assert min(r["k_vs_em"]) >= 0.99995, (n, r["k_vs_em"])
-        # ... and no further from the exact result than the bf16-operand floor allows
-        assert min(r["k_vs_ex"]) >= min(r["em_vs_ex"]) - 2e-4, (n, r["k_vs_ex"], r["em_vs_ex"])
+        assert min(r["k_vs_em"]) >= 0.99999, (n, r["k_vs_em"])
+        assert max(r["k_rel_em"]) <= 5e-4, (n, r["k_rel_em"])
+        # ... no further from the exact result than the bf16-operand floor allows, and close to it
+        assert min(r["k_vs_ex"]) >= min(r["em_vs_ex"]) - 1e-5, (n, r["k_vs_ex"], r["em_vs_ex"])
+        assert min(r["k_vs_ex"]) >= 0.9999, (n, r["k_vs_ex"])
+    for w, d in wsum.items():
+        assert _cos(d["k"], d["ex"]) >= 0.99999, (w, _cos(d["k"], d["ex"]))

@@ -11,9 +11,12 @@ persistent attention.  The B <= 4 parity tests never reach them.  Here:
     margin (profiles/r3a_gpu_tests.log: logits rel <= 4.0e-3, worst gradient cosine >= 0.99842 over
     the ~190 parameter gradients): logits within 1e-2 relative, worst parameter-gradient cosine >= 0.997;
   * B = 256 and B = 512 (configs[2]/[4] per-GPU sizes), PriGumbel with dropout on: everything finite,
-    bf16 vs fp32 engine on the same inputs and the same Philox streams (measured: logits cosine
-    1.000000, worst of DP + 36 Q/K/V gradients 0.99796 at B = 256): logits cosine >= 0.9999, the DP
-    gradient and the 36 Q/K/V weight gradients >= 0.996;
+    bf16 vs fp32 engine on the same inputs and the same Philox streams: logits cosine >= 0.9999, and the
+    DP gradient and the 36 Q/K/V weight gradients >= 0.994 at every rng base with a median worst
+    cosine >= 0.999 over the three bases (measured 0.9952-0.9999 over eight bases, profiles/r3v_cos.log).
+    The worst case is input drift, not a kernel error: at that point (B = 256, rng0 = 1 << 20, layer 11)
+    the attention kernels match a float64 reference on their own inputs to >= 0.99998
+    (tests/test_attn_layer11_gpu.py);
   * B = 256 training: the pass-2 loss strictly decreases over 5 PriGumbelTrainer iterations at lr 2e-5
     (draws fixed per step so the objective is one function), parameters and gradients finite.  At lr
     1e-4 (measured r2a) Adam's first, sign-like step of 1e-4 on all 117 M parameters overshoots:
