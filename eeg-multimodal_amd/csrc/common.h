@@ -64,17 +64,18 @@ DEV void glds16_asm_s(const void* base, uint32_t voff, const void* lds_base) {
 #ifndef EEGF_DMA_POL
 #define EEGF_DMA_POL ""
 #endif
-#ifndef EEGF_DMA_NOP
-#define EEGF_DMA_NOP "3"      // diagnostic builds only: fewer is unsafe wherever the lint finds a VALU-written base
-#endif
+// NOP: wait states after the M0 write (s_nop NOP).  3 (default) covers a base a VALU wrote just before
+// the statement; callers whose bases are SALU-computed may pass 0 (the 1 state the DMA needs after the M0
+// write) -- tools/isa_lint.py / tests/test_isa_lint_cpu.py check every site of the built library.
+template <int NOP = 3>
 DEV void glds16_asm_sa(const void* base, uint32_t voff, uint32_t lds_addr) {
   // readfirstlane: a no-op on a base the compiler already keeps in SGPRs, and it keeps the "s"
   // constraint satisfiable when control flow elsewhere in the kernel makes it place the base in VGPRs
   const uint64_t b = (uint64_t)(uintptr_t)base;
   const uint64_t bu = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
                       (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
-  asm volatile("s_mov_b32 m0, %2\n\ts_nop " EEGF_DMA_NOP "\n\tglobal_load_lds_dwordx4 %0, %1" EEGF_DMA_POL ::"v"(voff), "s"(bu),
-               "s"(lds_addr) : "memory", "m0");
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop %3\n\tglobal_load_lds_dwordx4 %0, %1" EEGF_DMA_POL ::"v"(voff), "s"(bu),
+               "s"(lds_addr), "i"(NOP) : "memory", "m0");
 }
 DEV uint32_t lds_addr_of(const void* p) {
   typedef __attribute__((address_space(3))) void lv;

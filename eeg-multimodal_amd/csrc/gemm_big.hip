@@ -690,6 +690,9 @@ __global__ void __launch_bounds__(NT, 1) gemm8_kernel(BigArgs g) {
 #ifndef EEGF_W_STAGGER
 #define EEGF_W_STAGGER 0
 #endif
+#ifndef EEGF_W_NOP
+#define EEGF_W_NOP 0
+#endif
 constexpr int BK4 = 32, NT4 = 256, SLOT4 = 2 * TM * BK4;   // elements per ring slot (A + B, 32 KB)
 constexpr int NSLOT4 = 5;                                     // ring depth: 5 x 32 KB = the 160 KB of LDS
 static_assert(NSLOT4 * SLOT4 >= TM * LDC, "the epilogue tile reuses the ring");
@@ -788,13 +791,18 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
   const long stepA = EEGF_W_PROBE == 1 ? 0 : AKC ? BK4 : (long)BK4 * g.lda;
   const long stepB = EEGF_W_PROBE == 1 ? 0 : BKC ? BK4 : (long)BK4 * g.ldb;
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr_of(lds));
-  auto stage_part = [&](const bf16* bA, const bf16* bB, int slot, int j) {   // part j of a K-tile -> ring slot
+  // part j of a K-tile -> ring slot; NOP as gemm4p's (0 in the K-loop, whose bases are pinned to SGPRs
+  // at the top of each K-tile, 3 in the prologue)
+  auto stage_part = [&](const bf16* bA, const bf16* bB, int slot, int j, auto Nc) __attribute__((always_inline)) {
+    constexpr int NOP = decltype(Nc)::value;
     const bool kc = j < 4 ? AKC : BKC;
     const uint32_t dst = lds0 + 2u * (slot * SLOT4 + (j < 4 ? 0 : TM * BK4) +
                                       (wave * 4 + (j & 3)) * (kc ? 16 * BK4 : 2 * TN));
-    if (j < 4) glds16_asm_sa(bA, voffA[j & 3], dst);
-    else glds16_asm_sa(bB, voffB[j & 3], dst);
+    if (j < 4) glds16_asm_sa<NOP>(bA, voffA[j & 3], dst);
+    else glds16_asm_sa<NOP>(bB, voffB[j & 3], dst);
   };
+  using WNOP = std::integral_constant<int, EEGF_W_NOP>;
+  using NOP3 = std::integral_constant<int, 3>;
   // fragment reads.  K-contiguous: rows r0 + (lane & 15) of a [256][32] image, chunk lane >> 4; the
   // swizzle of row r0 + 16s + i equals that of row i (r0 % 16 == 0): one per-lane offset +
   // immediates.  k-major: rd_col of k-rows 8 (lane >> 4) + .., columns r0 + 16s + (lane & 15), at
@@ -838,7 +846,7 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
   ts_mark(g, 0);
   for (int kt = 0; kt < NSLOT4; ++kt)
     if (kt < nk)
-      for (int j = 0; j < 8; ++j) stage_part(baseA + kt * stepA, baseB + kt * stepB, kt, j);
+      for (int j = 0; j < 8; ++j) stage_part(baseA + kt * stepA, baseB + kt * stepB, kt, j, NOP3{});
   vm_wait_tiles(max(0, min(nk, NSLOT4) - 2));
   raw_barrier();
   bf16x8 fa[2][8], fb[2][8];
@@ -859,8 +867,19 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
     constexpr bool INIT = decltype(Ic)::value, TAIL = decltype(Tc)::value;
     const bool more = !TAIL || k + 1 < nk, st = EEGF_W_PROBE < 2 && (!TAIL || k + NSLOT4 < nk);
     const bf16* nimg = lds + nslot * SLOT4;
-    const bf16* sA = baseA + (k + NSLOT4) * stepA;        // uniform K-tile bases of the stage
-    const bf16* sB = baseB + (k + NSLOT4) * stepB;
+    // uniform K-tile bases of the stage, moved to SGPRs here, 50+ instructions ahead of the first DMA
+    // (left to hipcc they stay in VGPRs and each DMA is preceded by a v_readfirstlane pair)
+    uint64_t sAu = (uint64_t)(uintptr_t)(baseA + (k + NSLOT4) * stepA);
+    uint64_t sBu = (uint64_t)(uintptr_t)(baseB + (k + NSLOT4) * stepB);
+    // (readfirstlane returns int: the low word is cast back to uint32_t, else it sign-extends into the
+    // high word and bit 31 of an address corrupts bits 32..63 -- an illegal address, measured r4o)
+    sAu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(sAu >> 32)) << 32) |
+          (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)sAu);
+    sBu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(sBu >> 32)) << 32) |
+          (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)sBu);
+    asm volatile("" : "+s"(sAu), "+s"(sBu));
+    const bf16* sA = (const bf16*)(uintptr_t)sAu;
+    const bf16* sB = (const bf16*)(uintptr_t)sBu;
     auto mma = [&](int s, int jj) {
       if (INIT) mma16_acc0(acc[s][jj], fb[H][jj], fa[H][s]);
       else mma16_acc(acc[s][jj], fb[H][jj], fa[H][s]);
@@ -888,24 +907,24 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
     for (int s = 0; s < 8; ++s) {
       mma(s, 0);
       rd_next(s, 0);
-      if (EEGF_W_STAGGER && st && wave == 0) stage_part(sA, sB, slot, s);
+      if (EEGF_W_STAGGER && st && wave == 0) stage_part(sA, sB, slot, s, WNOP{});
       __builtin_amdgcn_sched_barrier(0);
       mma(s, 1);
       rd_next(s, 1);
       __builtin_amdgcn_sched_barrier(0);
       mma(s, 2);
-      if (EEGF_W_STAGGER ? st && wave == 1 : st) stage_part(sA, sB, slot, s);
+      if (EEGF_W_STAGGER ? st && wave == 1 : st) stage_part(sA, sB, slot, s, WNOP{});
       __builtin_amdgcn_sched_barrier(0);
       mma(s, 3);
       rd_next(s, 3);
       __builtin_amdgcn_sched_barrier(0);
       mma(s, 4);
-      if (EEGF_W_STAGGER && st && wave == 2) stage_part(sA, sB, slot, s);
+      if (EEGF_W_STAGGER && st && wave == 2) stage_part(sA, sB, slot, s, WNOP{});
       __builtin_amdgcn_sched_barrier(0);
       mma(s, 5);
       __builtin_amdgcn_sched_barrier(0);
       mma(s, 6);
-      if (EEGF_W_STAGGER && st && wave == 3) stage_part(sA, sB, slot, s);
+      if (EEGF_W_STAGGER && st && wave == 3) stage_part(sA, sB, slot, s, WNOP{});
       __builtin_amdgcn_sched_barrier(0);
       mma(s, 7);
       // RS: row sums of this K-tile's A rows 16 s .. (lane & 15 -> row, every D column the same sum);
@@ -1144,6 +1163,9 @@ DEV void p_store_tile(const BigArgs& g, f32x4 (&acc)[8][8], const f32x4 (&biasv)
 #ifndef EEGF_P_STAGGER
 #define EEGF_P_STAGGER 0
 #endif
+#ifndef EEGF_P_NOP
+#define EEGF_P_NOP 0
+#endif
 template <bool BKC, int EPI, bool ACC = false>     // ACC: EPI_NONE with C = alpha A B^T + beta C
 __global__ void __launch_bounds__(NT4, 1) gemm4p_kernel(BigArgs g) {
   constexpr bool AKC = true;
@@ -1177,13 +1199,18 @@ __global__ void __launch_bounds__(NT4, 1) gemm4p_kernel(BigArgs g) {
   }
   const long stepB = BKC ? BK4 : (long)BK4 * g.ldb;
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr_of(lds));
-  auto stage_part = [&](const bf16* bA, const bf16* bB, int slot, int j) {
+  // NOP: the K-loop's DMAs take SALU-computed bases (s_nop 0 after the M0 write, isa_lint-checked); the
+  // prologue's come straight from tile_base's v_readfirstlane (s_nop 3)
+  auto stage_part = [&](const bf16* bA, const bf16* bB, int slot, int j, auto Nc) __attribute__((always_inline)) {
+    constexpr int NOP = decltype(Nc)::value;
     const bool kc = j < 4 ? AKC : BKC;
     const uint32_t dst = lds0 + 2u * (slot * SLOT4 + (j < 4 ? 0 : TM * BK4) +
                                       (wave * 4 + (j & 3)) * (kc ? 16 * BK4 : 2 * TN));
-    if (j < 4) glds16_asm_sa(bA, voffA[j & 3], dst);
-    else glds16_asm_sa(bB, voffB[j & 3], dst);
+    if (j < 4) glds16_asm_sa<NOP>(bA, voffA[j & 3], dst);
+    else glds16_asm_sa<NOP>(bB, voffB[j & 3], dst);
   };
+  using NOP0 = std::integral_constant<int, EEGF_P_NOP>;
+  using NOP3 = std::integral_constant<int, 3>;
   auto tile_base = [&](int l, const bf16*& bA, const bf16*& bB, int& m0, int& n0) {
     int tm, tn;
     tile_coords(g, l, tiles_m, tiles_n, tm, tn);
@@ -1195,7 +1222,7 @@ __global__ void __launch_bounds__(NT4, 1) gemm4p_kernel(BigArgs g) {
   auto stage_first = [&](const bf16* bA, const bf16* bB) {   // K-tiles 0 .. NSLOT4-1 -> slots 0 .. 4
     for (int kt = 0; kt < NSLOT4; ++kt)
       if (kt < nk)
-        for (int j = 0; j < 8; ++j) stage_part(bA + kt * BK4, bB + kt * stepB, kt, j);
+        for (int j = 0; j < 8; ++j) stage_part(bA + kt * BK4, bB + kt * stepB, kt, j, NOP3{});
   };
   const int fr = lane & 15, fq = lane >> 4;
   const int offA = (wm * 128 + fr) * BK4 + ((fq ^ sw4(fr)) << 3);
@@ -1293,24 +1320,24 @@ __global__ void __launch_bounds__(NT4, 1) gemm4p_kernel(BigArgs g) {
       for (int s = 0; s < 8; ++s) {
         mma(s, 0);
         rd_next(s, 0);
-        if (EEGF_P_STAGGER && stw && wave == 0) stage_part(sA, sB, slot, s);
+        if (EEGF_P_STAGGER && stw && wave == 0) stage_part(sA, sB, slot, s, NOP0{});
         __builtin_amdgcn_sched_barrier(0);
         mma(s, 1);
         rd_next(s, 1);
         __builtin_amdgcn_sched_barrier(0);
         mma(s, 2);
-        if (EEGF_P_STAGGER ? stw && wave == 1 : stw) stage_part(sA, sB, slot, s);
+        if (EEGF_P_STAGGER ? stw && wave == 1 : stw) stage_part(sA, sB, slot, s, NOP0{});
         __builtin_amdgcn_sched_barrier(0);
         mma(s, 3);
         rd_next(s, 3);
         __builtin_amdgcn_sched_barrier(0);
         mma(s, 4);
-        if (EEGF_P_STAGGER && stw && wave == 2) stage_part(sA, sB, slot, s);
+        if (EEGF_P_STAGGER && stw && wave == 2) stage_part(sA, sB, slot, s, NOP0{});
         __builtin_amdgcn_sched_barrier(0);
         mma(s, 5);
         __builtin_amdgcn_sched_barrier(0);
         mma(s, 6);
-        if (EEGF_P_STAGGER && stw && wave == 3) stage_part(sA, sB, slot, s);
+        if (EEGF_P_STAGGER && stw && wave == 3) stage_part(sA, sB, slot, s, NOP0{});
         __builtin_amdgcn_sched_barrier(0);
         mma(s, 7);
       }
@@ -1398,6 +1425,9 @@ __global__ void __launch_bounds__(NT4, 1) gemm4p_kernel(BigArgs g) {
 //     cross-tile staging (the last two odd K-tiles stage the next tile's pairs 0 and 1).
 // Needs K % 64 == 0 and K >= 128 (launch_big routes other shapes to gemm4p).
 constexpr int BKP = 64, PSLOT = 2 * TM * BKP;          // K per pair, elements per pair slot (64 KB)
+#ifndef EEGF_Q_NOP
+#define EEGF_Q_NOP 0
+#endif
 template <bool BKC, int EPI, bool ACC = false>
 __global__ void __launch_bounds__(NT4, 1) gemm4q_kernel(BigArgs g) {
   constexpr bool HAS_BIAS = EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_D;
@@ -1434,13 +1464,16 @@ __global__ void __launch_bounds__(NT4, 1) gemm4q_kernel(BigArgs g) {
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr_of(lds));
   auto stage_part = [&](const bf16* bA, const bf16* bB, int ps, int j) __attribute__((always_inline)) {
     const int jj = j & 7, pr = wave * 8 + jj;
+    // bases SALU-computed in this kernel (isa_lint: no VALU-written base within 5 states of any of its
+    // DMAs), so the DMA needs only the 1 state after its M0 write
+    constexpr int NOP = EEGF_Q_NOP;
     if (j < 8) {
-      glds16_asm_sa(bA + (long)pr * 8 * g.lda, voffA, lds0 + 2u * (ps * PSLOT + pr * 8 * BKP));
+      glds16_asm_sa<NOP>(bA + (long)pr * 8 * g.lda, voffA, lds0 + 2u * (ps * PSLOT + pr * 8 * BKP));
     } else if (BKC) {
-      glds16_asm_sa(bB + (long)pr * 8 * g.ldb, voffB[0], lds0 + 2u * (ps * PSLOT + TM * BKP + pr * 8 * BKP));
+      glds16_asm_sa<NOP>(bB + (long)pr * 8 * g.ldb, voffB[0], lds0 + 2u * (ps * PSLOT + TM * BKP + pr * 8 * BKP));
     } else {
-      glds16_asm_sa(bB + (long)pr * 2 * g.ldb, voffB[(jj & 1) | ((jj >> 2) << 1)],
-                    lds0 + 2u * (ps * PSLOT + TM * BKP + pr * 2 * TN));
+      glds16_asm_sa<NOP>(bB + (long)pr * 2 * g.ldb, voffB[(jj & 1) | ((jj >> 2) << 1)],
+                         lds0 + 2u * (ps * PSLOT + TM * BKP + pr * 2 * TN));
     }
   };
   auto tile_base = [&](int l, const bf16*& bA, const bf16*& bB, int& m0, int& n0) {

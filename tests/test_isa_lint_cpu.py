@@ -56,6 +56,18 @@ def test_lint_m0_and_carry_and_branch_predecessors():
     assert [(x.kind, x.states) for x in isa_lint.lint_function("k", br)] == [("valu_sgpr_vmem", 1)]
 
 
+def test_lint_flags_sign_extended_low_word_of_an_address():
+    """r4o: ``hi << 32 | readfirstlane(lo)`` (an ``int``) compiled to a sign-extend + OR; bit 31 of the
+    address set the whole high word and the weight-gradient GEMM faulted the GPU."""
+    bad = isa_lint.lint_function("k", _prog(
+        "s_add_u32 s54, s52, s70", "s_bfe_i64 s[54:55], s[54:55], 0x200000", "s_or_b64 s[56:57], s[54:55], s[44:45]"))
+    assert [x.kind for x in bad] == ["sext_low_word"]
+    # the same extract feeding something else (a sign-extended int64 index) is not the pattern
+    ok = isa_lint.lint_function("k", _prog(
+        "s_bfe_i64 s[4:5], s[4:5], 0x200000", "s_lshl_b64 s[4:5], s[4:5], 1", "s_add_u32 s0, s0, s4"))
+    assert ok == []
+
+
 @pytest.mark.skipif(not LIB.exists(), reason="libeegfusion.so not built (run __graft_entry__.build())")
 def test_shipped_library_has_no_vmem_sgpr_hazards():
     findings, counts = isa_lint.lint(LIB)

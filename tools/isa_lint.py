@@ -18,6 +18,12 @@ do", item 2).  This lint reads the shipped library, not the sources:
    * ``salu_m0_lds_dma`` — ``s_mov_b32 m0`` ahead of an LDS-DMA load (``*_lds_*`` / ``... lds``),
      which reads M0 as its LDS destination: 1 wait state required.
 
+3. one source-level bug class that shows in the ISA: ``sext_low_word`` — ``s_bfe_i64 d, s, 0x200000``
+   (sign-extend bits 0..31) whose result is ``s_or_b64``-ed within the next two instructions, i.e. a
+   64-bit address rebuilt as ``hi << 32 | lo`` from a signed low word (``__builtin_amdgcn_readfirstlane``
+   returns ``int``): bit 31 of the address then sets bits 32..63, an illegal address on roughly half
+   of all buffers (r4o: a GPU memory-access fault in the weight-gradient GEMM).
+
 usage: python tools/isa_lint.py [path/to/libeegfusion.so] [--all]
 Exit status 1 when any hazard is found.  ``tests/test_isa_lint_cpu.py`` runs it on the built library.
 """
@@ -38,6 +44,7 @@ BUNDLE_MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
 ARCH = "gfx950"
 
 REQUIRED = {"valu_sgpr_vmem": 5, "salu_m0_lds_dma": 1}
+SEXT32 = "0x200000"          # s_bfe_i64 operand: offset 0, width 32
 
 # VALU mnemonics whose second operand is an SGPR destination (carry-out / scale flag)
 _SDST1 = re.compile(r"^v_(add_co|sub_co|subrev_co|addc_co|subb_co|subbrev_co)_u32|^v_mad_(u64_u32|i64_i32)|"
@@ -169,6 +176,12 @@ def lint_function(name: str, insts: list[Inst]) -> list[Finding]:
                     preds[by_addr[tgt]].append(k)
     out: list[Finding] = []
     for k, ins in enumerate(insts):
+        if ins.mnem == "s_bfe_i64" and len(ins.ops) == 3 and ins.ops[2] == SEXT32:
+            dst = set(sregs(ins.ops[0]))
+            for p in insts[k + 1:k + 3]:
+                if p.mnem == "s_or_b64" and dst & set().union(*(sregs(o) for o in p.ops[1:])):
+                    out.append(Finding("sext_low_word", name, ins.addr, ins.text, p.text, 0))
+                    break
         if not _VMEM.match(ins.mnem):
             continue
         reads = vmem_sgpr_reads(ins)
