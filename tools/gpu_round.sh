@@ -6,7 +6,7 @@ TAG=${1:-r1}
 O=gpurun_out
 mkdir -p $O
 export PYTHONUNBUFFERED=1
-step() { local name=$1; shift; echo "[gpu_round] $name" ; "$@"; local rc=$?; echo "[gpu_round] $name rc=$rc"; return $rc; }
+step() { local name=$1; shift; echo "[gpu_round] $name" >&2; "$@"; local rc=$?; echo "[gpu_round] $name rc=$rc" >&2; return $rc; }
 # pytest exit 1 = some test failed (no fault): keep going; anything else (timeout 124/137, abort 134,
 # segfault 139, interrupted 2) ends the session
 tstep() { step "$@"; local rc=$?; [ $rc -eq 0 ] || [ $rc -eq 1 ]; }

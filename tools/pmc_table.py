@@ -35,8 +35,11 @@ GROUPS = {     # bf16 instantiations appear mangled in rocprofv3's CSV (DF16b), 
     # its grid is one workgroup per CU for every shape, so the three bias-only forwards share a row
     "ffn1_fwd": ("gemm8_kernelILb1ELb1ELi2EDF16bLb0E", "gemm8_kernelILb1ELb1ELi8EDF16bLb0E",
                  "gemm4p_kernel<true, 2, false>", "gemm4p_kernel<true, 8, false>",
-                 "gemm4p_kernelILb1ELi2ELb0E", "gemm4p_kernelILb1ELi8ELb0E"),
-    "fwd_bias_qkv_ao_ffn2": ("gemm4p_kernel<true, 1, false>", "gemm4p_kernelILb1ELi1ELb0E"),
+                 "gemm4p_kernelILb1ELi2ELb0E", "gemm4p_kernelILb1ELi8ELb0E",
+                 # round 4: the K-contiguous forwards run on gemm4q (K-tile pairs in whole lines)
+                 "gemm4q_kernel<true, 2, false>", "gemm4q_kernel<true, 8, false>"),
+    "fwd_bias_qkv_ao_ffn2": ("gemm4p_kernel<true, 1, false>", "gemm4p_kernelILb1ELi1ELb0E",
+                             "gemm4q_kernel<true, 1, false>"),
     "qkv_fwd": ("gemm8_kernelILb1ELb1ELi1EDF16bLb0E",),
     "ffn2_fwd": ("gemm4w_kernelILb1ELb1ELi1EDF16bLb0E",),
     "dgrad_qkv_ffn1": ("gemm4w_kernelILb1ELb0ELi0EDF16bLb0E", "gemm4p_kernel<false, 0, true>",
