@@ -73,6 +73,9 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-batch", type=int, default=16,
                     help="CPU-baseline batch of the live sample (bounded: ~10-30 s of CPU work)")
     ap.add_argument("--cpu-iters", type=int, default=2, help="CPU-baseline timed iterations after one warm-up")
+    ap.add_argument("--cpu-warm-batch", type=int, default=0,
+                    help="batch of the CPU-baseline warm-up iteration (0 = --cpu-batch; the batch-256 sample "
+                         "warms up at 16: thread pool and allocator, not another 2-4 minutes of page faults)")
     ap.add_argument("--cpu-baseline-only", action="store_true",
                     help="time only the CPU baseline (e.g. --cpu-batch 256 --cpu-iters 3, BASELINE.md §3) and print "
                          "its JSON; profiles/" + "cpu_baseline_b256.json holds that run for the bench line")
@@ -131,7 +134,7 @@ def cpu_share() -> dict:
     return {"threads": threads, "affinity": avail, "cgroup_quota": quota, "omp_num_threads": omp}
 
 
-def cpu_baseline(variant: str, batch: int, iters: int) -> dict:
+def cpu_baseline(variant: str, batch: int, iters: int, warm_batch: int = 0) -> dict:
     """The CPU oracle (torch fp32 restatement, oracle/fusion_oracle.py; pinned against the reference's
     own outputs by tests/test_oracle_golden.py) timed on the host cores on a bounded sample of the
     same iteration: the bench's batch (256), dropout 0.1 at every reference site as on the GPU leg,
@@ -160,53 +163,69 @@ def cpu_baseline(variant: str, batch: int, iters: int) -> dict:
         else:
             t = torch.zeros(s)
         p[k] = t.requires_grad_()
-    eeg = torch.randn(batch, C, L, generator=g)
-    act = torch.randn(batch, A, generator=g) * 0.5
-    labels = (torch.rand(batch, generator=g) < 0.66).long()
-    batch_d = dict(eeg=eeg, act=act)
+    def make_batch(n):
+        eeg = torch.randn(n, C, L, generator=g)
+        act = torch.randn(n, A, generator=g) * 0.5
+        return dict(eeg=eeg, act=act), (torch.rand(n, generator=g) < 0.66).long()
+
     model_p = [v for k, v in p.items() if k != "DP"]
     mopt = torch.optim.Adam(model_p, lr=1e-6)
     dopt = torch.optim.Adam([p["DP"]], lr=1e-6) if "DP" in p else None
     lap = torch.distributions.laplace.Laplace(torch.tensor([0.0]), torch.tensor([1.0]))
 
-    def draws():
-        n = lap.sample((batch, 3 * HID)).view(batch, 3 * HID)
-        gm = -torch.empty(2, batch, 3 * HID).exponential_().log()
-        return n, gm
+    def draws(n):
+        noise = lap.sample((n, 3 * HID)).view(n, 3 * HID)
+        gm = -torch.empty(2, n, 3 * HID).exponential_().log()
+        return noise, gm
 
-    def iteration():
+    def iteration(batch_d, labels):
+        nb = labels.shape[0]
         if variant == "prigumbel":
             dopt.zero_grad()
             with torch.no_grad():
                 pooled, img, cross = O.encoders(p, batch_d, O.PathConfig(contract="W"))
-            n, gm = draws()
+            n, gm = draws(nb)
             f = O.minmax(torch.cat((pooled, img, cross), 1))
             logits = O.head(p, O.prigumbel_gate(f, p["DP"], n, gm, 1.0, "newfrac", False))
             O.cal_loss(logits, labels)[0].backward()
             dopt.step()
             mopt.zero_grad()
-            n, gm = draws()
+            n, gm = draws(nb)
             pc = O.PathConfig(contract="W", variant="prigumbel", hard=True)
             O.cal_loss(O.forward(p, batch_d, pc, noise=n, gumbels=gm), labels)[0].backward()
             mopt.step()
         else:
             mopt.zero_grad()
             pc = O.PathConfig(contract="W", variant="priconcat", honor_dp_mode=True)
-            row = lap.sample((batch,)).view(batch)
+            row = lap.sample((nb,)).view(nb)
             torch.nn.functional.cross_entropy(O.forward(p, batch_d, pc, row_noise=row), labels).backward()
             mopt.step()
 
+    # a heartbeat line every 30 s: one batch-256 iteration runs for minutes with nothing else to say
+    import threading
+    t_start, done = time.perf_counter(), threading.Event()
+
+    def heartbeat():
+        while not done.wait(30.0):
+            progress(f"... {time.perf_counter() - t_start:.0f} s")
+
+    threading.Thread(target=heartbeat, daemon=True).start()
+    warm_batch = warm_batch or batch
+    warm_d, warm_l = make_batch(warm_batch)
+    batch_d, labels = make_batch(batch)
     try:
-        progress(f"{variant} batch {batch}, {threads} threads: warm-up")
+        progress(f"{variant} batch {batch}, {threads} threads: warm-up at batch {warm_batch}")
         t0 = time.perf_counter()
-        iteration()                                    # warm-up (allocations, thread pool)
+        iteration(warm_d, warm_l)                      # warm-up (allocations, thread pool)
         warm = time.perf_counter() - t0
+        del warm_d, warm_l
         t0 = time.perf_counter()
         for i in range(iters):
-            iteration()
+            iteration(batch_d, labels)
             progress(f"iteration {i + 1}/{iters}: {time.perf_counter() - t0:.1f} s")
         dt = time.perf_counter() - t0
     finally:
+        done.set()
         O.set_dropout_replay(None)
     return {"value": round(batch * iters / dt, 4), "unit": "samples/s", "cores": threads, "kind": "port",
             "cpu_model": cpu_model(), "cpus_available": avail, "cpu_share": share,
@@ -214,7 +233,8 @@ def cpu_baseline(variant: str, batch: int, iters: int) -> dict:
             "warmup_seconds": round(warm, 2),
             "sample": f"oracle/fusion_oracle.py {variant} iteration (torch CPU fp32, dropout 0.1"
                       f"{', feature_all_lap honoured' if variant != 'prigumbel' else ''}), batch {batch}, "
-                      f"64x256 EEG + 32-d action, {iters} timed iteration(s) after 1 warm-up, {dt:.1f} s timed"}
+                      f"64x256 EEG + 32-d action, {iters} timed iteration(s) after 1 warm-up"
+                      f"{f' at batch {warm_batch}' if warm_batch != batch else ''}, {dt:.1f} s timed"}
 
 
 def load_profile_json(name: str, tag: str):
@@ -253,7 +273,7 @@ def main():
     sys.path.insert(0, str(ROOT / "eeg-multimodal_amd"))
     sys.path.insert(0, str(ROOT))
     if args.cpu_baseline_only:
-        cb = cpu_baseline(args.variant, args.cpu_batch, args.cpu_iters)
+        cb = cpu_baseline(args.variant, args.cpu_batch, args.cpu_iters, args.cpu_warm_batch)
         print(json.dumps(cb), flush=True)
         if args.cpu_baseline_out:
             f = Path(args.cpu_baseline_out)
@@ -440,7 +460,7 @@ def main():
         if replicas is not None:
             out["replicas"] = replicas
         if world == 1 and not args.no_cpu_baseline:
-            cb = cpu_baseline(args.variant, args.cpu_batch, args.cpu_iters)
+            cb = cpu_baseline(args.variant, args.cpu_batch, args.cpu_iters, args.cpu_warm_batch)
             # the BASELINE.md §3 sample (batch 256, 1 warm-up + 3 timed) measured on a GPU box's host by
             # `bench.py --cpu-baseline-only --cpu-batch 256 --cpu-iters 3`: too long for the default run
             ref = load_profile_json("cpu_baseline_b256.json", args.variant)

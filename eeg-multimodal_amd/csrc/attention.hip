@@ -474,9 +474,10 @@ extern "C" int eegf_attn_fwd(int dtype, int B, int H, int L, const void* qkv, lo
   if (B > 65535 || drop_p < 0.f || drop_p >= 1.f) return EEGF_ERR_ARG;
   AttnArgs a{qkv, out, lse, key_bias, nullptr, nullptr, nullptr, nullptr, B, H, L, ld_qkv, ld_out, scale,
              drop_p, seed, offset, drop_p > 0.f ? drop_bits : nullptr};
-  if (l256_path(dtype, B, H, L, key_bias, false) && !a.bits) {
+  if (l256_path(dtype, B, H, L, key_bias, false)) {
     const dim3 g1(l256_grid(B * H));
-    if (drop_p > 0.f) hipLaunchKernelGGL(attn_fwd256_kernel<true>, g1, dim3(512), 0, stream, a);
+    if (a.bits) hipLaunchKernelGGL((attn_fwd256_kernel<true, true>), g1, dim3(512), 0, stream, a);
+    else if (drop_p > 0.f) hipLaunchKernelGGL(attn_fwd256_kernel<true>, g1, dim3(512), 0, stream, a);
     else hipLaunchKernelGGL(attn_fwd256_kernel<false>, g1, dim3(512), 0, stream, a);
     return (int)hipGetLastError();
   }

@@ -22,6 +22,7 @@ derivatives, LN backward with deterministic partial sums and column reductions f
 from __future__ import annotations
 
 import math
+import os
 import struct
 from dataclasses import dataclass, field
 
@@ -64,6 +65,10 @@ class EngineConfig:
     tau: float = 1.0               # PriGumbel-v1 gumbel_softmax temperature (train_val.py:95)
     varlen: bool = True            # contract T: BERT over the packed real tokens (pad skipping, 8(f)#2)
     modal: str = "ti"              # custom_models/models.py variant: ti | it | ii | tt | tisc (MODALS)
+    # attention dropout mask exported by the forward and read by the backward (default False: the
+    # backward regenerates it; exporting costs the forward 30 us and the reading backward is 18 us
+    # slower than the regenerating one per layer at B = 256, profiles/r4s_attn_bits_ab.log)
+    attn_bits: bool = field(default_factory=lambda: os.environ.get("EEGF_ATTN_BITS", "0") == "1")
 
 
 @dataclass
@@ -749,9 +754,10 @@ class FusionEngine:
                         self.a.span(pre + "attention.self.query.bias", 3), qkv, R, tag="qkv_fwd")
             ctx = self.empty(R, HID)
             lse = torch.empty(B, NH, L, dtype=torch.float32, device=self.a.device)
-            # the backward regenerates the dropout mask from the Philox stream (measured faster than
-            # storing the keep bits in the forward and reading them back)
-            bits = None
+            # dropout keep bits (1 bit per probability, 25 MB per layer at B = 256) only with
+            # cfg.attn_bits: by default the backward regenerates the Philox stream
+            bits = (torch.empty(B * NH * L * L // 32, dtype=torch.int32, device=self.a.device)
+                    if save and adrop > 0 and vl is None and self.cfg.attn_bits else None)
             ev = self._ev_start("attn_fwd")
             if vl is None:
                 call("eegf_attn_fwd", self.code, B, NH, L, P(qkv), 3 * HID, P(kbias), scale, float(adrop),

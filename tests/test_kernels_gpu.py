@@ -228,6 +228,39 @@ def test_attention_fwd_bwd(dt, L, masked, pdrop, use_bits):
         assert e < _tol(dt) * 3, (name, e)
 
 
+@pytest.mark.parametrize("pdrop", [1e-6, 0.1])
+def test_attention256_exports_keep_bits(pdrop):
+    """The L = 256 forward with a drop_bits buffer (the engine's path since round 4): identical output
+    bits to the forward without it, the exported mask equals the Philox replay (p = 1e-6 < 2^-16: every
+    probability kept, all-ones words), and the backward reading the bits equals the one regenerating."""
+    lib = _lib()
+    torch.manual_seed(3)
+    B, L = 3, 256
+    qkv = torch.randn(B, L, 2304, device="cuda").to(torch.bfloat16)
+    dout = torch.randn(B, L, 768, device="cuda").to(torch.bfloat16)
+    ws = torch.empty(max(lib.lib().eegf_attn_bwd_workspace(B, L), 1), device="cuda")
+    res = {}
+    for use_bits in (False, True):
+        out = torch.empty(B, L, 768, device="cuda", dtype=torch.bfloat16)
+        lse = torch.empty(B, 12, L, device="cuda")
+        bits = torch.zeros(B * 12 * L * L // 32, device="cuda", dtype=torch.int32)
+        dqkv = torch.empty_like(qkv)
+        bp = bits.data_ptr() if use_bits else None
+        lib.call("eegf_attn_fwd", _code(torch.bfloat16), B, 12, L, qkv.data_ptr(), 2304, None, 0.125, pdrop, 11, 4,
+                 out.data_ptr(), 768, lse.data_ptr(), bp, _s())
+        lib.call("eegf_attn_bwd", _code(torch.bfloat16), B, 12, L, qkv.data_ptr(), 2304, None, 0.125, pdrop, 11, 4,
+                 out.data_ptr(), dout.data_ptr(), 768, lse.data_ptr(), bp, dqkv.data_ptr(), ws.data_ptr(), _s())
+        torch.cuda.synchronize()
+        res[use_bits] = (out, lse, dqkv, bits)
+    assert torch.equal(res[False][0], res[True][0]) and torch.equal(res[False][1], res[True][1])
+    assert torch.equal(res[False][2], res[True][2])
+    bits = res[True][3]
+    if pdrop < 2.0 ** -16:
+        assert bool((bits == -1).all())
+    else:
+        _check_bits(bits, _attn_mask(B, L, pdrop, 11, 4), B, L)
+
+
 @pytest.mark.parametrize("dt", DT)
 def test_xattn_mixed_dtypes(dt):
     """bf16 memory with fp32 query/context (mixed-precision engine)."""

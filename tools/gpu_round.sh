@@ -26,7 +26,7 @@ for s in "${@:2}"; do
     priconcat) step priconcat timeout -k 10 300 python -u bench.py --variant priconcat --no-cpu-baseline > $O/${TAG}_priconcat.json 2> $O/${TAG}_priconcat.err || exit 1 ;;
     b512) step b512 timeout -k 10 300 python -u bench.py --batch 512 --no-cpu-baseline > $O/${TAG}_b512.json 2> $O/${TAG}_b512.err || exit 1 ;;
     pmc) step pmc bash tools/pmc_round.sh $TAG || exit 1 ;;
-    cpub256) step cpub256 timeout -k 10 900 python -u bench.py --cpu-baseline-only --cpu-batch 256 --cpu-iters 3 --cpu-baseline-out $O/cpu_baseline_b256.json > $O/${TAG}_cpub256.json 2> $O/${TAG}_cpub256.err || exit 1 ;;
+    cpub256) step cpub256 timeout -k 10 1080 python -u bench.py --cpu-baseline-only --cpu-batch 256 --cpu-iters 3 --cpu-warm-batch 16 --cpu-baseline-out $O/cpu_baseline_b256.json > $O/${TAG}_cpub256.json 2> $O/${TAG}_cpub256.err || exit 1 ;;
     layer11) tstep layer11 timeout -k 10 300 python -u -m pytest tests/test_attn_layer11_gpu.py -x -v -s --timeout 240 --timeout-method thread > $O/${TAG}_layer11.log 2>&1 || exit 1 ;;
     smoke) step smoke timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/${TAG}_smoke.log 2>&1 || exit 1 ;;
   esac
