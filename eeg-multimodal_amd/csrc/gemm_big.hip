@@ -1425,13 +1425,24 @@ __global__ void __launch_bounds__(NT4, 1) gemm4p_kernel(BigArgs g) {
 //     cross-tile staging (the last two odd K-tiles stage the next tile's pairs 0 and 1).
 // Needs K % 64 == 0 and K >= 128 (launch_big routes other shapes to gemm4p).
 constexpr int BKP = 64, PSLOT = 2 * TM * BKP;          // K per pair, elements per pair slot (64 KB)
+constexpr int HSLOT = TM * BKP;                        // one operand of a pair (32 KB)
 #ifndef EEGF_Q_NOP
 #define EEGF_Q_NOP 0
+#endif
+// EEGF_Q_RING5 1: the 160 KB of LDS as a ring of five 32-KB operand slots (A of pair u in slot 2u mod 5, B
+// in 2u + 1 mod 5) instead of two 64-KB pair slots, so pair t + 2's A is staged during pair t's EVEN
+// K-tile (into pair t - 1's B slot) and its B during the odd one (into pair t's A slot): 32 KB of LDS-DMA
+// per K-tile at an even rate instead of 64 KB in every odd K-tile (above the 46 B/cycle the CU's DMA
+// path moves in whole lines, profiles/r4e_dma_line_pattern.log); same waits and barriers, same MFMA order
+#ifndef EEGF_Q_RING5
+#define EEGF_Q_RING5 1
 #endif
 template <bool BKC, int EPI, bool ACC = false>
 __global__ void __launch_bounds__(NT4, 1) gemm4q_kernel(BigArgs g) {
   constexpr bool HAS_BIAS = EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_D;
-  __shared__ __attribute__((aligned(16))) bf16 lds[2 * PSLOT];
+  constexpr bool R5 = EEGF_Q_RING5 != 0;
+  static_assert(!(R5 && EEGF_P_STAGGER), "the staggered DMA placement is a two-slot-ring probe");
+  __shared__ __attribute__((aligned(16))) bf16 lds[R5 ? 5 * HSLOT : 2 * PSLOT];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
@@ -1462,18 +1473,20 @@ __global__ void __launch_bounds__(NT4, 1) gemm4q_kernel(BigArgs g) {
   }
   const long pstepB = BKC ? BKP : (long)BKP * g.ldb;
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr_of(lds));
+  // ps: pair slot (its A image at 0, B at TM * BKP) or, R5, the operand slot of the part (A parts j < 8,
+  // B parts j >= 8)
   auto stage_part = [&](const bf16* bA, const bf16* bB, int ps, int j) __attribute__((always_inline)) {
     const int jj = j & 7, pr = wave * 8 + jj;
     // bases SALU-computed in this kernel (isa_lint: no VALU-written base within 5 states of any of its
     // DMAs), so the DMA needs only the 1 state after its M0 write
     constexpr int NOP = EEGF_Q_NOP;
+    const int b0 = R5 ? ps * HSLOT : ps * PSLOT + TM * BKP;    // element offset of the B image
     if (j < 8) {
-      glds16_asm_sa<NOP>(bA + (long)pr * 8 * g.lda, voffA, lds0 + 2u * (ps * PSLOT + pr * 8 * BKP));
+      glds16_asm_sa<NOP>(bA + (long)pr * 8 * g.lda, voffA, lds0 + 2u * ((R5 ? ps * HSLOT : ps * PSLOT) + pr * 8 * BKP));
     } else if (BKC) {
-      glds16_asm_sa<NOP>(bB + (long)pr * 8 * g.ldb, voffB[0], lds0 + 2u * (ps * PSLOT + TM * BKP + pr * 8 * BKP));
+      glds16_asm_sa<NOP>(bB + (long)pr * 8 * g.ldb, voffB[0], lds0 + 2u * (b0 + pr * 8 * BKP));
     } else {
-      glds16_asm_sa<NOP>(bB + (long)pr * 2 * g.ldb, voffB[(jj & 1) | ((jj >> 2) << 1)],
-                         lds0 + 2u * (ps * PSLOT + TM * BKP + pr * 2 * TN));
+      glds16_asm_sa<NOP>(bB + (long)pr * 2 * g.ldb, voffB[(jj & 1) | ((jj >> 2) << 1)], lds0 + 2u * (b0 + pr * 2 * TN));
     }
   };
   auto tile_base = [&](int l, const bf16*& bA, const bf16*& bB, int& m0, int& n0) {
@@ -1489,8 +1502,9 @@ __global__ void __launch_bounds__(NT4, 1) gemm4q_kernel(BigArgs g) {
   const int fr = lane & 15, fq = lane >> 4;
   const int offA0 = (wm * 128 + fr) * BKP + ((fq ^ (fr & 7)) << 3);
   const int offA1 = (wm * 128 + fr) * BKP + (((4 + fq) ^ (fr & 7)) << 3);
-  const int offB0 = TM * BKP + (wn * 128 + fr) * BKP + ((fq ^ (fr & 7)) << 3);
-  const int offB1 = TM * BKP + (wn * 128 + fr) * BKP + (((4 + fq) ^ (fr & 7)) << 3);
+  constexpr int BIMG = R5 ? 0 : TM * BKP;     // B image offset from the image base rdB is given
+  const int offB0 = BIMG + (wn * 128 + fr) * BKP + ((fq ^ (fr & 7)) << 3);
+  const int offB1 = BIMG + (wn * 128 + fr) * BKP + (((4 + fq) ^ (fr & 7)) << 3);
   int tB0[8], tB1[8];
   if (!BKC) {
 #pragma unroll
@@ -1498,8 +1512,8 @@ __global__ void __launch_bounds__(NT4, 1) gemm4q_kernel(BigArgs g) {
       const int q = fr >> 2, p4 = fr & 3;
       const int col = wn * 128 + 16 * i + 4 * p4, ch = col >> 3, off = col & 7;
       const int ka = 8 * fq + q, kb = ka + 4;
-      tB0[i] = TM * BKP + ka * TN + (((ch ^ swz_k(ka)) << 3) | off);
-      tB1[i] = TM * BKP + kb * TN + (((ch ^ swz_k(kb)) << 3) | off);
+      tB0[i] = BIMG + ka * TN + (((ch ^ swz_k(ka)) << 3) | off);
+      tB1[i] = BIMG + kb * TN + (((ch ^ swz_k(kb)) << 3) | off);
     }
   }
   auto rdA = [&](const bf16* img, auto Hc, int i) {
@@ -1518,11 +1532,11 @@ __global__ void __launch_bounds__(NT4, 1) gemm4q_kernel(BigArgs g) {
   int m0, n0;
   tile_base(L, baseA, baseB, m0, n0);
 #pragma unroll 1
-  for (int j = 0; j < 16; ++j) stage_part(baseA, baseB, 0, j);                 // pair 0 -> slot 0
+  for (int j = 0; j < 16; ++j) stage_part(baseA, baseB, R5 ? j >> 3 : 0, j);                 // pair 0
 #pragma unroll 1
-  for (int j = 0; j < 16; ++j) stage_part(baseA + BKP, baseB + pstepB, 1, j);  // pair 1 -> slot 1
+  for (int j = 0; j < 16; ++j) stage_part(baseA + BKP, baseB + pstepB, R5 ? 2 + (j >> 3) : 1, j);  // pair 1
   f32x4 acc[8][8];
-  int ps0 = 0;                  // pair slot of the tile's pair 0
+  int ps0 = 0;                  // pair slot of the tile's pair 0 (R5: operand slot of its A, 0..4)
   bool landed = false;          // the tile's pairs 0 and 1 retired (cross-staged and waited for)
   for (;;) {
     const int Ln = L + G;
@@ -1534,12 +1548,15 @@ __global__ void __launch_bounds__(NT4, 1) gemm4q_kernel(BigArgs g) {
     if (!landed) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");      // pair 0 (pair 1 younger)
     raw_barrier();
     bf16x8 fa[2][8], fb[2][8];
+    // R5 operand-slot arithmetic: slot + c mod 5 for 0 <= c <= 5 (uniform, on the SALU)
+    auto add5 = [](int x, int c) { const int y = x + c; return y >= 5 ? y - 5 : y; };
     {
-      const bf16* img0 = lds + ps0 * PSLOT;
+      const bf16* img0 = lds + (R5 ? ps0 * HSLOT : ps0 * PSLOT);
+      const bf16* imb0 = R5 ? lds + add5(ps0, 1) * HSLOT : img0;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         fa[0][i] = rdA(img0, C0{}, i);
-        fb[0][i] = rdB(img0, C0{}, i);
+        fb[0][i] = rdB(imb0, C0{}, i);
       }
     }
     // K-tile s = 2 t + H of pair t (slot ps = (ps0 + t) & 1): its fragments are in fa / fb[H]; the next
@@ -1548,14 +1565,19 @@ __global__ void __launch_bounds__(NT4, 1) gemm4q_kernel(BigArgs g) {
     // TAIL (the last two pairs): whether there is a next K-tile to read and what to stage are decided at
     // run time; in the steady state (t + 2 < np) both are compile-time true, so the K-tile body carries no
     // branch and hipcc's waitcnt pass sees straight-line LDS reads
-    auto ktile = [&](auto Hc, int t, auto Ic, auto Tc) __attribute__((always_inline)) {
+    // hA (R5): operand slot of pair t's A
+    auto ktile = [&](auto Hc, int t, int hA, auto Ic, auto Tc) __attribute__((always_inline)) {
       constexpr int H = decltype(Hc)::value;
       constexpr bool INIT = decltype(Ic)::value, TAIL = decltype(Tc)::value;
-      const int ps = (ps0 + t) & 1;
+      const int ps = R5 ? hA : (ps0 + t) & 1;
       const bool more = !TAIL || H == 0 || t + 1 < np;
-      const bf16* nimg = lds + (H == 0 ? ps : ps ^ 1) * PSLOT;
+      // next K-tile's images: R5 operand slots of pair t (H = 0) or t + 1 (H = 1)
+      const bf16* nimg = R5 ? lds + add5(hA, 2 * H) * HSLOT : lds + (H == 0 ? ps : ps ^ 1) * PSLOT;
+      const bf16* nimb = R5 ? lds + add5(hA, 2 * H + 1) * HSLOT : nimg;
       const bool own = !TAIL || t + 2 < np;
-      const bool st = H == 1 && (own || more_tiles);
+      // R5: both K-tiles stage (A of pair t + 2 into pair t - 1's B slot, B into pair t's A slot)
+      const bool st = (R5 || H == 1) && (own || more_tiles);
+      const int sslot = R5 ? (H == 0 ? add5(hA, 4) : hA) : ps;
       const bf16* sA = own ? baseA + (t + 2) * BKP : nA + (t + 2 - np) * BKP;
       const bf16* sB = own ? baseB + (t + 2) * pstepB : nB + (t + 2 - np) * pstepB;
       auto mma = [&](int s8, int jj) {
@@ -1569,21 +1591,24 @@ __global__ void __launch_bounds__(NT4, 1) gemm4q_kernel(BigArgs g) {
         if (more) fa[H ^ 1][s8] = rdA(nimg, HN{}, s8);
         __builtin_amdgcn_sched_barrier(0);
         mma(s8, 1);
-        if (more) fb[H ^ 1][s8] = rdB(nimg, HN{}, s8);
+        if (more) fb[H ^ 1][s8] = rdB(nimb, HN{}, s8);
         __builtin_amdgcn_sched_barrier(0);
         if (EEGF_P_STAGGER) {     // wave w: its two parts after MFMAs 2 w and 2 w + 1 of the group
           if (H == 1 && st && wave == 0) stage_part(sA, sB, ps, 2 * s8);
           __builtin_amdgcn_sched_barrier(0);
         }
         mma(s8, 2);
-        if (EEGF_P_STAGGER ? H == 1 && st && wave == 1 : H == 1 && st) stage_part(sA, sB, ps, 2 * s8);
+        if (R5) {
+          if (st) stage_part(sA, sB, sslot, 8 * H + s8);
+        } else if (EEGF_P_STAGGER ? H == 1 && st && wave == 1 : H == 1 && st) stage_part(sA, sB, ps, 2 * s8);
         if (EEGF_P_STAGGER && H == 1 && st && wave == 0) stage_part(sA, sB, ps, 2 * s8 + 1);
         __builtin_amdgcn_sched_barrier(0);
         mma(s8, 3);
         if (EEGF_P_STAGGER && H == 1 && st && wave == 1) stage_part(sA, sB, ps, 2 * s8 + 1);
         __builtin_amdgcn_sched_barrier(0);
         mma(s8, 4);
-        if (EEGF_P_STAGGER ? H == 1 && st && wave == 2 : H == 1 && st) stage_part(sA, sB, ps, 2 * s8 + (EEGF_P_STAGGER ? 0 : 1));
+        if (!R5 && (EEGF_P_STAGGER ? H == 1 && st && wave == 2 : H == 1 && st))
+          stage_part(sA, sB, ps, 2 * s8 + (EEGF_P_STAGGER ? 0 : 1));
         __builtin_amdgcn_sched_barrier(0);
         mma(s8, 5);
         if (EEGF_P_STAGGER && H == 1 && st && wave == 2) stage_part(sA, sB, ps, 2 * s8 + 1);
@@ -1598,29 +1623,41 @@ __global__ void __launch_bounds__(NT4, 1) gemm4q_kernel(BigArgs g) {
       if (H == 0) {
         // pair t + 1 (staged during pair t - 1's odd K-tile, the only DMAs in flight) must have landed
         // before the next K-tile reads its fragments; the barrier also frees pair t's slot for pair t + 2
-        if ((!TAIL || t + 1 < np) && !(landed && t == 0)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // (R5: except this K-tile's 8 A parts of pair t + 2)
+        if (R5) {
+          if (!TAIL || t + 1 < np) {
+            if (st) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          }
+        } else if ((!TAIL || t + 1 < np) && !(landed && t == 0)) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         raw_barrier();
       }
     };
     using F = std::false_type;
     using T = std::true_type;
+    int hA = ps0;
     if (np > 2) {
-      ktile(C0{}, 0, T{}, F{});
-      ktile(C1{}, 0, F{}, F{});
+      ktile(C0{}, 0, hA, T{}, F{});
+      ktile(C1{}, 0, hA, F{}, F{});
     } else {
-      ktile(C0{}, 0, T{}, T{});
-      ktile(C1{}, 0, F{}, T{});
+      ktile(C0{}, 0, hA, T{}, T{});
+      ktile(C1{}, 0, hA, F{}, T{});
     }
+    hA = add5(hA, 2);
 #pragma unroll 1
     for (int t = 1; t + 2 < np; ++t) {
-      ktile(C0{}, t, F{}, F{});
-      ktile(C1{}, t, F{}, F{});
+      ktile(C0{}, t, hA, F{}, F{});
+      ktile(C1{}, t, hA, F{}, F{});
+      hA = add5(hA, 2);
     }
 #pragma unroll 1
     for (int t = max(1, np - 2); t < np; ++t) {
-      ktile(C0{}, t, F{}, T{});
-      ktile(C1{}, t, F{}, T{});
+      ktile(C0{}, t, hA, F{}, T{});
+      ktile(C1{}, t, hA, F{}, T{});
+      hA = add5(hA, 2);
     }
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
     const int mrow = m0 + wm * 128 + (lane & 15);
@@ -1638,7 +1675,7 @@ __global__ void __launch_bounds__(NT4, 1) gemm4q_kernel(BigArgs g) {
     baseA = nA;
     baseB = nB;
     landed = true;
-    ps0 = (ps0 + np) & 1;
+    ps0 = R5 ? hA : (ps0 + np) & 1;
   }
 }
 
@@ -1858,7 +1895,8 @@ int launch_big(const BigArgs& a, int splits, hipStream_t s) {
       // whole-line staging (gemm4q) for the forward layout (both operands K-contiguous) where K splits
       // into >= 2 pairs of K-tiles: 3-4 % faster there; with a k-major B (input gradients, already whole
       // lines) its shallower 2-pair ring lost 1-6 % (profiles/r4i_gemm_ab.log), so those stay on gemm4p
-      const bool q = g_gemm4q == 1 && BKC && a.K % BKP == 0 && a.K >= 2 * BKP;
+      // (key 14 = 2: the input gradients on gemm4q too)
+      const bool q = g_gemm4q >= 1 && (BKC || g_gemm4q == 2) && a.K % BKP == 0 && a.K >= 2 * BKP;
       if constexpr (EPI == EPI_NONE) {
         if (acc && q) hipLaunchKernelGGL((gemm4q_kernel<BKC, EPI, true>), grid, dim3(NT4), 0, s, ap);
         if (acc && !q) hipLaunchKernelGGL((gemm4p_kernel<BKC, EPI, true>), grid, dim3(NT4), 0, s, ap);
@@ -2099,7 +2137,7 @@ extern "C" int eegf_tune(int key, int value) {
   if (key == 10) { const int o = g_ln_fwd768; g_ln_fwd768 = value; return o; }
   if (key == 12) { const int o = g_store_nt; if (value < 0 || value > 1) return EEGF_ERR_ARG; g_store_nt = value; return o; }
   if (key == 11) { const int o = g_gemm4p; if (value < 0 || value > 3) return EEGF_ERR_ARG; g_gemm4p = value; return o; }
-  if (key == 14) { const int o = g_gemm4q; if (value < 0 || value > 1) return EEGF_ERR_ARG; g_gemm4q = value; return o; }
+  if (key == 14) { const int o = g_gemm4q; if (value < 0 || value > 2) return EEGF_ERR_ARG; g_gemm4q = value; return o; }
   if (key == 13) { const int o = g_cu_reserve; if (value < 0 || value >= cu_count()) return EEGF_ERR_ARG; g_cu_reserve = value; return o; }
   if (key == 6) { const int o = g_ln_rpw; if (value < 1 || value > 64) return EEGF_ERR_ARG; g_ln_rpw = value; return o; }
   return EEGF_ERR_ARG;

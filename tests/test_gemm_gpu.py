@@ -599,7 +599,8 @@ def test_gemm_persistent_dgrad(epi, M, N, K):
     aux = torch.randn(M, N, device="cuda").to(torch.bfloat16) if epi == "mul_aux" else None
     c0 = torch.randn(M, N, device="cuda").to(torch.bfloat16)
     outs = []
-    for k11, k14 in ((1, 1), (0, 1), (1, 0)):
+    # (key 11, key 14): default (gemm4p), non-persistent, persistent gemm4p, gemm4q with the k-major B
+    for k11, k14 in ((1, 1), (0, 1), (1, 0), (1, 2)):
         old, old14 = _tune(11, k11), _tune(14, k14)
         try:
             if epi == "none_beta":
@@ -612,7 +613,8 @@ def test_gemm_persistent_dgrad(epi, M, N, K):
         finally:
             _tune(11, old)
             _tune(14, old14)
-    assert torch.equal(outs[0], outs[2])          # gemm4q == gemm4p bit for bit
+    assert torch.equal(outs[0], outs[2])          # gemm4p (default) == gemm4p (key 14 = 0)
+    assert torch.equal(outs[0], outs[3])          # gemm4q with a k-major B == gemm4p bit for bit
     if epi == "none_beta":
         ref = c0.double() + dy.double() @ w.double()
     else:
