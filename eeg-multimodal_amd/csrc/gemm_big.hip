@@ -1087,6 +1087,8 @@ DEV void p_store_tile(const BigArgs& g, f32x4 (&acc)[8][8], const f32x4 (&biasv)
   // accumulator layout.
   const int nst = n0 + wn * 128 + 16 * g_odd(lane) + 8 * (lane >> 5);     // + 32 jp
   constexpr bool in_tile = IN_EPI;
+  // the input tile (aux, or C for beta) whole, one wait before the first store: streaming it two rows
+  // ahead of the stores measured the same (profiles/r4y2_epilogue_pipe_ab.log)
   uint4 cin[8][4];
   if (IN_EPI && in_tile) {
     const bf16* src = EPI == EPI_MUL_AUX ? g.aux : (const bf16*)g.C;
@@ -1437,6 +1439,9 @@ constexpr int HSLOT = TM * BKP;                        // one operand of a pair 
 #ifndef EEGF_Q_RING5
 #define EEGF_Q_RING5 1
 #endif
+#ifndef EEGF_Q_SPOS
+#define EEGF_Q_SPOS 4      // R5: the group's LDS-DMA part goes after its MFMA EEGF_Q_SPOS (0..7)
+#endif
 template <bool BKC, int EPI, bool ACC = false>
 __global__ void __launch_bounds__(NT4, 1) gemm4q_kernel(BigArgs g) {
   constexpr bool HAS_BIAS = EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_D;
@@ -1587,36 +1592,45 @@ __global__ void __launch_bounds__(NT4, 1) gemm4q_kernel(BigArgs g) {
       using HN = std::integral_constant<int, H ^ 1>;
 #pragma unroll
       for (int s8 = 0; s8 < 8; ++s8) {
+        auto r5st = [&](int pos) __attribute__((always_inline)) {
+          if (R5 && pos == EEGF_Q_SPOS && st) stage_part(sA, sB, sslot, 8 * H + s8);
+        };
         mma(s8, 0);
         if (more) fa[H ^ 1][s8] = rdA(nimg, HN{}, s8);
+        r5st(0);
         __builtin_amdgcn_sched_barrier(0);
         mma(s8, 1);
         if (more) fb[H ^ 1][s8] = rdB(nimb, HN{}, s8);
+        r5st(1);
         __builtin_amdgcn_sched_barrier(0);
         if (EEGF_P_STAGGER) {     // wave w: its two parts after MFMAs 2 w and 2 w + 1 of the group
           if (H == 1 && st && wave == 0) stage_part(sA, sB, ps, 2 * s8);
           __builtin_amdgcn_sched_barrier(0);
         }
         mma(s8, 2);
-        if (R5) {
-          if (st) stage_part(sA, sB, sslot, 8 * H + s8);
-        } else if (EEGF_P_STAGGER ? H == 1 && st && wave == 1 : H == 1 && st) stage_part(sA, sB, ps, 2 * s8);
+        r5st(2);
+        if (!R5 && (EEGF_P_STAGGER ? H == 1 && st && wave == 1 : H == 1 && st)) stage_part(sA, sB, ps, 2 * s8);
         if (EEGF_P_STAGGER && H == 1 && st && wave == 0) stage_part(sA, sB, ps, 2 * s8 + 1);
         __builtin_amdgcn_sched_barrier(0);
         mma(s8, 3);
+        r5st(3);
         if (EEGF_P_STAGGER && H == 1 && st && wave == 1) stage_part(sA, sB, ps, 2 * s8 + 1);
         __builtin_amdgcn_sched_barrier(0);
         mma(s8, 4);
+        r5st(4);
         if (!R5 && (EEGF_P_STAGGER ? H == 1 && st && wave == 2 : H == 1 && st))
           stage_part(sA, sB, ps, 2 * s8 + (EEGF_P_STAGGER ? 0 : 1));
         __builtin_amdgcn_sched_barrier(0);
         mma(s8, 5);
+        r5st(5);
         if (EEGF_P_STAGGER && H == 1 && st && wave == 2) stage_part(sA, sB, ps, 2 * s8 + 1);
         __builtin_amdgcn_sched_barrier(0);
         mma(s8, 6);
+        r5st(6);
         if (EEGF_P_STAGGER && H == 1 && st && wave == 3) stage_part(sA, sB, ps, 2 * s8);
         __builtin_amdgcn_sched_barrier(0);
         mma(s8, 7);
+        r5st(7);
         if (EEGF_P_STAGGER && H == 1 && st && wave == 3) stage_part(sA, sB, ps, 2 * s8 + 1);
         __builtin_amdgcn_sched_barrier(0);
       }
