@@ -1871,7 +1871,7 @@ int g_store_nt = [] { const char* e = getenv("EEGF_STORE_NT"); return e ? atoi(e
 int g_gemm4p = [] { const char* e = getenv("EEGF_GEMM4P"); return e ? atoi(e) : 1; }();
 // key 14: the persistent GEMM's staging: 1 (default) whole 128-B lines (gemm4q) where K % 64 == 0 and
 // K >= 128, 0 gemm4p's 64-B half lines everywhere
-int g_gemm4q = [] { const char* e = getenv("EEGF_GEMM4Q"); return e ? atoi(e) : 1; }();
+int g_gemm4q = [] { const char* e = getenv("EEGF_GEMM4Q"); return e ? atoi(e) : 2; }();
 int cu_count() {
   static const int cus = [] {
     int dev = 0, n = 256;
@@ -1906,10 +1906,11 @@ int launch_big(const BigArgs& a, int splits, hipStream_t s) {
       ap.store_nt = g_store_nt;
       bool acc = false;
       if constexpr (EPI == EPI_NONE) acc = a.beta != 0.f;
-      // whole-line staging (gemm4q) for the forward layout (both operands K-contiguous) where K splits
-      // into >= 2 pairs of K-tiles: 3-4 % faster there; with a k-major B (input gradients, already whole
-      // lines) its shallower 2-pair ring lost 1-6 % (profiles/r4i_gemm_ab.log), so those stay on gemm4p
-      // (key 14 = 2: the input gradients on gemm4q too)
+      // whole-line staging (gemm4q) wherever K splits into >= 2 pairs of K-tiles (key 14 = 2, default):
+      // the forward layout (both operands K-contiguous) 3-6 % faster; the input gradients (k-major B)
+      // lost 1-6 % on its first, two-pair-slot ring (profiles/r4i_gemm_ab.log) and gain 3-5 % on the
+      // five-slot one (the K-contiguous dY in whole lines; profiles/r4ze_dgrad_gemm4q_ab.log).
+      // key 14 = 1: forward layout only, 0: gemm4p everywhere
       const bool q = g_gemm4q >= 1 && (BKC || g_gemm4q == 2) && a.K % BKP == 0 && a.K >= 2 * BKP;
       if constexpr (EPI == EPI_NONE) {
         if (acc && q) hipLaunchKernelGGL((gemm4q_kernel<BKC, EPI, true>), grid, dim3(NT4), 0, s, ap);

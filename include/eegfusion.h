@@ -88,9 +88,10 @@ int eegf_tune(int key, int value);
 /*   key 13: CUs left free by the persistent kernels (the 256x256 GEMM and the L = 256 attention grids
  *          launch cu_count - value workgroups; 0 = default): room for RCCL's kernels during the
  *          backward when world > 1 (tools/overlap_proxy.py prices it).
- *   key 14: 1 (default) = the forward GEMMs with both operands K-contiguous and K % 64 == 0 run on
- *          gemm4q (K-tile pairs staged in whole 128-B lines), 0 = on gemm4p, 2 = the input gradients
- *          (k-major B) on gemm4q too; bit-identical results (tests/test_gemm_gpu.py), env EEGF_GEMM4Q. */
+ *   key 14: the persistent GEMMs with K % 64 == 0, K >= 128 on gemm4q (K-tile pairs staged in whole
+ *          128-B lines, five 32-KB operand slots): 2 (default) every such GEMM, 1 the forward layout
+ *          (both operands K-contiguous) only, 0 none (gemm4p); bit-identical results
+ *          (tests/test_gemm_gpu.py), env EEGF_GEMM4Q. */
 /* Diagnostics (no reference counterpart): every following 256-row GEMM launch of the 8-wave / 4-wave
  * kernels writes 4 s_memrealtime stamps per workgroup (start, prologue done, K-loop done, epilogue
  * issued, slot 4 the CU id) into buf = int64 [grid.y][grid.x][8]; nullptr switches it off.  tools/gemm_phases.py. */

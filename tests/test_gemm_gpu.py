@@ -542,8 +542,11 @@ def test_gemm_4h_dgrad(epi, M, N, K):
 # nk = K / 32 K-tiles: 24, 24, 3, 1, 96, and the ring-edge cases 5..7 (a full 5-slot ring, no cross-tile
 # staging) and 8 (the first cross-staged shape: the next tile's K-tiles 0..4 landed before it starts),
 # each with three rounds per CU on a 256-CU grid (768 tiles)
+# K = 128 / 320: gemm4q with 2 / 5 K-tile pairs per tile (its five operand slots advance 2 np mod 5 per
+# tile: 4 and 0), several tiles per CU
 P_SHAPES = [(65536, 2304, 768), (4096, 768, 768), (8192, 3072, 96), (2048, 1024, 32), (16384, 768, 3072),
-            (16384, 3072, 160), (16384, 3072, 192), (16384, 3072, 224), (16384, 3072, 256)]
+            (16384, 3072, 160), (16384, 3072, 192), (16384, 3072, 224), (16384, 3072, 256), (16384, 3072, 128),
+            (16384, 3072, 320)]
 
 
 @pytest.mark.parametrize("epi", ["bias", "bias_gelu", "bias_gelu_d", "gelu_noaux", "none"])
@@ -559,8 +562,8 @@ def test_gemm_persistent_fwd(epi, M, N, K):
     b = torch.randn(N, device="cuda")
     e = "bias_gelu" if epi == "gelu_noaux" else epi
     outs = []
-    # (key 11, key 14): persistent with whole-line staging (gemm4q, default), persistent gemm4p, non-persistent
-    for k11, k14 in ((1, 1), (0, 1), (1, 0)):
+    # (key 11, key 14): persistent with whole-line staging (gemm4q), non-persistent, persistent gemm4p
+    for k11, k14 in ((1, 2), (0, 2), (1, 0)):
         old, old14 = _tune(11, k11), _tune(14, k14)
         try:
             aux = torch.full((M, N), float("nan"), device="cuda", dtype=torch.bfloat16) \
@@ -599,7 +602,7 @@ def test_gemm_persistent_dgrad(epi, M, N, K):
     aux = torch.randn(M, N, device="cuda").to(torch.bfloat16) if epi == "mul_aux" else None
     c0 = torch.randn(M, N, device="cuda").to(torch.bfloat16)
     outs = []
-    # (key 11, key 14): default (gemm4p), non-persistent, persistent gemm4p, gemm4q with the k-major B
+    # (key 11, key 14): forward-only gemm4q (so gemm4p here), non-persistent, gemm4p, gemm4q (default)
     for k11, k14 in ((1, 1), (0, 1), (1, 0), (1, 2)):
         old, old14 = _tune(11, k11), _tune(14, k14)
         try:
@@ -613,7 +616,7 @@ def test_gemm_persistent_dgrad(epi, M, N, K):
         finally:
             _tune(11, old)
             _tune(14, old14)
-    assert torch.equal(outs[0], outs[2])          # gemm4p (default) == gemm4p (key 14 = 0)
+    assert torch.equal(outs[0], outs[2])          # gemm4p (key 14 = 1) == gemm4p (key 14 = 0)
     assert torch.equal(outs[0], outs[3])          # gemm4q with a k-major B == gemm4p bit for bit
     if epi == "none_beta":
         ref = c0.double() + dy.double() @ w.double()
