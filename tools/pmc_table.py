@@ -43,11 +43,12 @@ GROUPS = {     # bf16 instantiations appear mangled in rocprofv3's CSV (DF16b), 
     "qkv_fwd": ("gemm8_kernelILb1ELb1ELi1EDF16bLb0E",),
     "ffn2_fwd": ("gemm4w_kernelILb1ELb1ELi1EDF16bLb0E",),
     "dgrad_qkv_ffn1": ("gemm4w_kernelILb1ELb0ELi0EDF16bLb0E", "gemm4p_kernel<false, 0, true>",
-                       "gemm4p_kernelILb0ELi0ELb1E"),
+                       "gemm4p_kernelILb0ELi0ELb1E", "gemm4q_kernel<false, 0, true>"),
     "ao_fwd": ("gemm4h_kernelILb1ELi1E", "gemm4h_kernel<true, 1>"),
     "dgrad_out": ("gemm4h_kernelILb0ELi0E", "gemm4h_kernel<false, 0>", "gemm4p_kernel<false, 0, false>",
-                  "gemm4p_kernelILb0ELi0ELb0E"),
-    "dgrad_ffn2": ("gemm8_kernelILb1ELb0ELi9EDF16bLb0E", "gemm4p_kernel<false, 9, false>", "gemm4p_kernelILb0ELi9ELb0E"),
+                  "gemm4p_kernelILb0ELi0ELb0E", "gemm4q_kernel<false, 0, false>"),
+    "dgrad_ffn2": ("gemm8_kernelILb1ELb0ELi9EDF16bLb0E", "gemm4p_kernel<false, 9, false>", "gemm4p_kernelILb0ELi9ELb0E",
+                   "gemm4q_kernel<false, 9, false>"),
     "wgrad": ("gemm4w_kernel<false, false, 0, float, true", "gemm4w_kernelILb0ELb0ELi0EfLb1E"),
     "attn_fwd": ("attn_fwd256_kernel",),
     "attn_bwd": ("attn_bwd256_kernel",),
