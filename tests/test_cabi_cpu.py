@@ -37,3 +37,23 @@ def test_argument_errors_return_status_without_gpu():
                          1.0, 0.0, 1.0, None, 0, None) == _lib.ERR_ARG
     assert lib.eegf_attn_fwd(1, 2, 11, 256, None, 2304, None, 0.125, 0.0, 0, 0, None, 768, None, None, None) == _lib.ERR_ARG
     assert lib.eegf_adam(0, None, None, None, None, None, 1e-3, 0.9, 0.999, 1e-8, 0.0, 1.0, 1, None) == _lib.ERR_ARG
+
+
+def test_tune_routing_keys_validate_and_restore_without_gpu():
+    """eegf_tune is host state only: the GEMM routing keys report the production defaults (key 11 = 1
+    persistent GEMM, key 14 = 2 gemm4q for every eligible shape), refuse out-of-range values with
+    EEGF_ERR_ARG and return the previous value when set."""
+    import os
+
+    from eegfusion import _lib
+    lib = _lib.lib()
+    lib.eegf_tune.argtypes = [_lib.i32, _lib.i32]
+    for key, default, hi in ((11, 1, 3), (14, 2, 2)):
+        env = {11: "EEGF_GEMM4P", 14: "EEGF_GEMM4Q"}[key]
+        old = lib.eegf_tune(key, default)
+        if env not in os.environ:
+            assert old == default, (key, old)
+        assert lib.eegf_tune(key, hi + 1) == _lib.ERR_ARG
+        assert lib.eegf_tune(key, -1) == _lib.ERR_ARG
+        assert lib.eegf_tune(key, 0) == default
+        assert lib.eegf_tune(key, old) == 0
