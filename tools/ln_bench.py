@@ -1,6 +1,7 @@
 """A/B of eegf_ln_fwd rows-per-wave (eegf_tune key 6) at the BERT shape: 65536 x 768 bf16, residual,
 attention-output dropout (mode 1, p 0.1), residual-sum store (pass 2) and without it (pass 1).
 Prints us per call and the algorithmic GB/s; checks every variant's output equals rpw=1's."""
+import os
 import sys
 from pathlib import Path
 
@@ -23,11 +24,12 @@ s = torch.empty_like(y)
 mean = torch.empty(R, device=dev)
 rstd = torch.empty(R, device=dev)
 st = torch.cuda.current_stream()
+P = float(os.environ.get("LNB_P", "0.1"))   # dropout probability of the forward (LNB_P=0: no RNG)
 
 
 def run(save):
     call("eegf_ln_fwd", BF16, R, W, x.data_ptr(), r.data_ptr(), None, 1, None, gam.data_ptr(), bet.data_ptr(),
-         1e-12, 0.1, 1, 7, 11, y.data_ptr(), s.data_ptr() if save else None, mean.data_ptr(), rstd.data_ptr(),
+         1e-12, P, 1, 7, 11, y.data_ptr(), s.data_ptr() if save else None, mean.data_ptr(), rstd.data_ptr(),
          st.cuda_stream)
 
 
