@@ -1417,25 +1417,25 @@ __global__ void __launch_bounds__(NT4, 1) gemm4p_kernel(BigArgs g) {
 // that pattern and 46 B/cycle in 8 rows x 128 B (profiles/r4e_dma_line_pattern.log), while a 256x256
 // K-tile needs 32 KB per 1,024 MFMA cycles, so gemm4p's forward K-loop ran at the DMA ceiling (its
 // no-staging probe: FFN2 forward 283 -> 207 us, profiles/r4c_gemm_probe_ab.log).  Here:
-//   * the ring holds K-tile PAIRS (64 deep): 2 pair slots of 64 KB, each [256 rows][64 k] per
+//   * the ring holds K-tile PAIRS (64 deep) in operand images of 32 KB: [256 rows][64 k] per
 //     K-contiguous operand (16-B chunk c of row r stored at c ^ (r & 7): conflict-free ds_read_b128),
 //     [64 k][256 cols] per k-major operand (gemm4p's swz_k image, two K-tiles stacked);
-//   * pair t + 2 is staged during the odd (second) K-tile of pair t into pair t's slot (free since
-//     the barrier that ended pair t's even K-tile) and waited for at the end of the next even K-tile:
-//     one vmcnt + one barrier per pair, none at odd K-tiles;
+//   * default (EEGF_Q_RING5): five operand slots, A of pair u in slot 2u mod 5 and B in 2u + 1 mod 5;
+//     pair t + 2's A is staged during pair t's even K-tile (into pair t - 1's B slot), its B during the
+//     odd one (into pair t's A slot, free since the barrier that ended the even K-tile): 32 KB per
+//     K-tile, one part per 8-MFMA group.  The first form (EEGF_Q_RING5=0, two 64-KB pair slots) staged
+//     all of pair t + 2 in pair t's odd K-tile: 64 KB there and none in the even one;
+//   * one vmcnt + one barrier per pair (end of the even K-tile), none at odd K-tiles;
 //   * the same MFMA K order as gemm4p (bitwise identical results), the same epilogue (p_store_tile) and
-//     cross-tile staging (the last two odd K-tiles stage the next tile's pairs 0 and 1).
+//     cross-tile staging (the last two pairs stage the next tile's pairs 0 and 1).
 // Needs K % 64 == 0 and K >= 128 (launch_big routes other shapes to gemm4p).
 constexpr int BKP = 64, PSLOT = 2 * TM * BKP;          // K per pair, elements per pair slot (64 KB)
 constexpr int HSLOT = TM * BKP;                        // one operand of a pair (32 KB)
 #ifndef EEGF_Q_NOP
 #define EEGF_Q_NOP 0
 #endif
-// EEGF_Q_RING5 1: the 160 KB of LDS as a ring of five 32-KB operand slots (A of pair u in slot 2u mod 5, B
-// in 2u + 1 mod 5) instead of two 64-KB pair slots, so pair t + 2's A is staged during pair t's EVEN
-// K-tile (into pair t - 1's B slot) and its B during the odd one (into pair t's A slot): 32 KB of LDS-DMA
-// per K-tile at an even rate instead of 64 KB in every odd K-tile (above the 46 B/cycle the CU's DMA
-// path moves in whole lines, profiles/r4e_dma_line_pattern.log); same waits and barriers, same MFMA order
+// EEGF_Q_RING5 1 (default): the five-slot ring above; 64 KB per odd K-tile was above the 46 B/cycle the
+// CU's DMA path moves in whole lines (forward GEMMs 3-6 % faster, profiles/r4u_gemm4q_ring5_ab.log)
 #ifndef EEGF_Q_RING5
 #define EEGF_Q_RING5 1
 #endif
