@@ -10,4 +10,4 @@ for r in 1 2; do
     EEGF_LIB=$lib timeout -k 10 120 python -u tools/ln_bench.py >> $O/${TAG}_ln.log 2>&1 || exit 1
   done
 done
-grep -v amdgpu.ids $O/${TAG}_ln.log | grep "==\|rpw 16"
+grep -v amdgpu.ids $O/${TAG}_ln.log | grep "==\|rpw 16\|rpw 32"
