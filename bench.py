@@ -45,8 +45,10 @@ METRIC = "samples/sec at batch 256, 64ch×256 EEG + 32-d action, 1/2/4/8 GPUs"
 PMC_FILE = "pmc_r4zl.json"          # profiles/: tools/pmc_table.py output (HBM bytes, MFMA busy per group)
 # probed kernel groups (HIP events around each launch on the launch stream, engine.probe)
 KERNEL_GROUPS = {
-    "ffn1_fwd": "BertIntermediate GEMM + bias + GELU (+GELU' saved in pass 2), 65536x3072x768 (persistent kernel)",
+    "ffn1_fwd": "BertIntermediate GEMM + bias + GELU, pass 1 (no save), 65536x3072x768",
+    "ffn1_fwd_gd": "BertIntermediate GEMM + bias + GELU + GELU' saved for the backward, pass 2, 65536x3072x768",
     "qkv_fwd": "fused Q|K|V projection GEMM + bias, 65536x2304x768",
+    "ao_fwd": "attention output projection GEMM + bias, 65536x768x768",
     "ffn2_fwd": "BertOutput GEMM + bias, 65536x768x3072",
     "attn_fwd": "fused self-attention forward (QK^T, softmax, dropout, PV), 256x12 heads x 256^2 x 64",
     "attn_bwd": "fused self-attention backward (dQ, dK, dV)",
@@ -55,6 +57,34 @@ KERNEL_GROUPS = {
     "dgrad_out": "input gradient through the attention output projection, 65536x768x768",
     "dgrad_ffn2": "input gradient through BertOutput with the GELU' product, 65536x3072x768",
     "wgrad": "weight gradients (split-K over 65536 tokens) with the bias gradients fused (row sums)",
+}
+# The kernel (rocprof symbol) each probed group runs on: the roofline object reports the SYMBOL with the
+# most time per step, combining the groups that share it, with the PMC traffic of that symbol
+# (profiles/PMC_FILE key).  Algorithmic bytes per launch: A + W + C (+ aux) of each shape, bf16.
+R_TOK = 256 * L
+KERNEL_SYMBOLS = {
+    "gemm4q_kernel<true, 1, false>": {
+        "tags": ("qkv_fwd", "ao_fwd", "ffn2_fwd"), "pmc": "fwd_bias_qkv_ao_ffn2",
+        "what": "persistent 256x256 bf16 GEMM, bias epilogue: the QKV, attention-output and FFN2 forwards",
+        "bytes": {"qkv_fwd": 2 * (R_TOK * 768 + 2304 * 768 + R_TOK * 2304),
+                  "ao_fwd": 2 * (R_TOK * 768 + 768 * 768 + R_TOK * 768),
+                  "ffn2_fwd": 2 * (R_TOK * 3072 + 768 * 3072 + R_TOK * 768)}},
+    "gemm4w_kernel<false, false, 0, float, true> + splitk_rowsum_reduce": {
+        "tags": ("wgrad",), "pmc": "wgrad",
+        "what": "split-K weight-gradient GEMM with the bias row sums, and its fixed-order slab reduction"},
+    "gemm4q_kernel<false, 0, true>": {
+        "tags": ("dgrad_qkv", "dgrad_ffn1"), "pmc": "dgrad_qkv_ffn1",
+        "what": "persistent GEMM, input gradients accumulating onto the residual gradient (beta = 1)"},
+    "gemm4q_kernel<true, 8, false>": {"tags": ("ffn1_fwd_gd",), "pmc": "ffn1_fwd",
+                                      "what": "persistent GEMM, FFN1 + bias + GELU + GELU' (pass 2)"},
+    "gemm4q_kernel<true, 2, false>": {"tags": ("ffn1_fwd",), "pmc": "ffn1_fwd",
+                                      "what": "persistent GEMM, FFN1 + bias + GELU (pass 1)"},
+    "gemm4q_kernel<false, 9, false>": {"tags": ("dgrad_ffn2",), "pmc": "dgrad_ffn2",
+                                       "what": "persistent GEMM, FFN2 input gradient x GELU'"},
+    "gemm4q_kernel<false, 0, false>": {"tags": ("dgrad_out",), "pmc": "dgrad_out",
+                                       "what": "persistent GEMM, attention-output input gradient"},
+    "attn_bwd256_kernel<true>": {"tags": ("attn_bwd",), "pmc": "attn_bwd", "what": "L = 256 attention backward"},
+    "attn_fwd256_kernel<true, false>": {"tags": ("attn_fwd",), "pmc": "attn_fwd", "what": "L = 256 attention forward"},
 }
 
 
@@ -72,7 +102,7 @@ def parse_args(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=16,
                     help="CPU-baseline batch of the live sample (bounded: ~10-30 s of CPU work)")
-    ap.add_argument("--cpu-iters", type=int, default=2, help="CPU-baseline timed iterations after one warm-up")
+    ap.add_argument("--cpu-iters", type=int, default=3, help="CPU-baseline timed iterations after one warm-up")
     ap.add_argument("--cpu-warm-batch", type=int, default=0,
                     help="batch of the CPU-baseline warm-up iteration (0 = --cpu-batch; the batch-256 sample "
                          "warms up at 16: thread pool and allocator, not another 2-4 minutes of page faults)")
@@ -416,21 +446,45 @@ def main():
         value = world * B * steps / total_dt
         ks = probe_stats(probe_all)
         step_tf = value / world * flops_per_sample(args.variant) / 1e12
-        # the dominant kernel group: largest total time among the probed groups of this run
-        dom_tag = max(ks, key=lambda t: ks[t]["avg_ms"] * ks[t]["launches"]) if ks else None
-        dom = ks.get(dom_tag)
-        pmc = load_profile_json(PMC_FILE, dom_tag) or {}
-        roofline = {"kernel": f"{dom_tag}: {KERNEL_GROUPS.get(dom_tag, '')} (the largest probed kernel group by "
-                              f"time in this run: {dom['avg_ms'] * dom['launches'] / steps:.2f} ms per step)"
-                              if dom else None,
+        # the dominant kernel: the rocprof symbol with the largest total probed time in this run (the groups
+        # that share a symbol combined: achieved = their FLOPs / their time), with that symbol's PMC traffic
+        sym_stats = {}
+        for sym, d in KERNEL_SYMBOLS.items():
+            parts = [ks[t] for t in d["tags"] if t in ks]
+            if not parts:
+                continue
+            n = sum(p["launches"] for p in parts)
+            ms = sum(p["avg_ms"] * p["launches"] for p in parts)
+            fl = sum(p["flops_per_launch"] * p["launches"] for p in parts)
+            by = d.get("bytes")
+            alg = (sum(by[t] * ks[t]["launches"] for t in d["tags"] if t in ks) / n) if by else None
+            sym_stats[sym] = {"launches": n, "ms": ms, "flops_per_launch": fl / n, "avg_ms": ms / n,
+                              "tflops": fl / (ms * 1e-3) / 1e12, "alg_bytes": alg}
+        dom_sym = max(sym_stats, key=lambda k: sym_stats[k]["ms"]) if sym_stats else None
+        dom = sym_stats.get(dom_sym)
+        pmc = load_profile_json(PMC_FILE, KERNEL_SYMBOLS[dom_sym]["pmc"]) if dom else None
+        pmc = pmc or {}
+        roofline = {"kernel": (f"{dom_sym}: {KERNEL_SYMBOLS[dom_sym]['what']} (the kernel with the most time per "
+                               f"step in this run: {dom['ms'] / steps:.2f} ms over {dom['launches'] / steps:.0f} "
+                               f"launches; probe groups {', '.join(KERNEL_SYMBOLS[dom_sym]['tags'])})")
+                    if dom else None,
                     "bound": "mfma", "achieved": round(dom["tflops"], 1) if dom else None, "peak": PEAK_BF16,
                     "unit": "TFLOP/s", "frac": round(dom["tflops"] / PEAK_BF16, 4) if dom else None,
-                    "traffic": pmc.get("hbm_bytes_per_launch"), "mfma_busy": pmc.get("mfma_busy"),
-                    "pmc_round": pmc.get("round"),
+                    "traffic": pmc.get("hbm_bytes_per_launch"),
+                    "algorithmic_bytes_per_launch": dom["alg_bytes"] if dom else None,
+                    "mfma_busy": pmc.get("mfma_busy"), "pmc_round": pmc.get("round"),
                     "avg_ms": round(dom["avg_ms"], 4) if dom else None,
                     "flops_per_launch": dom["flops_per_launch"] if dom else None}
-        f1 = ks.get("ffn1_fwd")
-        ffn1 = load_profile_json(PMC_FILE, "ffn1_fwd") or {}      # both FFN1 forms (pass 1 GELU, pass 2 + GELU')
+        kernels_by_symbol = {k: {"ms_per_step": round(v["ms"] / steps, 3), "avg_ms": round(v["avg_ms"], 4),
+                                 "tflops": round(v["tflops"], 1), "frac": round(v["tflops"] / PEAK_BF16, 4)}
+                             for k, v in sorted(sym_stats.items(), key=lambda kv: -kv[1]["ms"])}
+        f1p = [ks[t] for t in ("ffn1_fwd", "ffn1_fwd_gd") if t in ks]     # both FFN1 forms (pass 1, pass 2)
+        f1 = None
+        if f1p:
+            n1 = sum(p["launches"] for p in f1p)
+            ms1 = sum(p["avg_ms"] * p["launches"] for p in f1p)
+            f1 = {"avg_ms": ms1 / n1, "tflops": sum(p["flops_per_launch"] * p["launches"] for p in f1p) / (ms1 * 1e-3) / 1e12}
+        ffn1 = load_profile_json(PMC_FILE, "ffn1_fwd") or {}
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "samples/s", "n_gpus": world, "steps": steps,
             "warmup": args.warmup, "ms_per_step": round(total_dt / steps * 1e3, 3), "higher_is_better": True,
@@ -452,6 +506,7 @@ def main():
                               "flops_per_sample": flops_per_sample(args.variant)},
             "kernels": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                         for k, v in ks.items()},
+            "kernels_by_symbol": kernels_by_symbol,
             "loss": float(loss[-1].item()),
         }
         if len(sweep) > 1 or feawei is not None:
@@ -464,6 +519,12 @@ def main():
             # the BASELINE.md §3 sample (batch 256, 1 warm-up + 3 timed) measured on a GPU box's host by
             # `bench.py --cpu-baseline-only --cpu-batch 256 --cpu-iters 3`: too long for the default run
             ref = load_profile_json("cpu_baseline_b256.json", args.variant)
+            if args.cpu_batch != B:
+                cb["deviation"] = (f"live sample at batch {args.cpu_batch} (BASELINE.md section 3 asks for batch {B}, "
+                                   f"1 warm-up + >= 3 timed iterations in the same run: about 107 s per batch-256 "
+                                   f"iteration on a GPU box's 16-CPU share, minutes more than the default run may "
+                                   f"take); the batch-256 sample, measured by bench.py --cpu-baseline-only "
+                                   f"--cpu-batch 256 --cpu-iters 3 on a GPU box, is batch256_measured")
             if ref:
                 cb["batch256_measured"] = ref
             out["cpu_baseline"] = cb

@@ -40,6 +40,7 @@ struct BigArgs {
   long long* ts;         // diagnostics (eegf_gemm_big_timestamps): per-workgroup phase times, null = off
   int group_m;           // tile raster: 0 row-major, G > 0 groups of G row panels walked column by column
   int store_nt = 0;      // gemm4p: epilogue stores with the non-temporal hint
+  int order = 0;         // gemm4q persistent tile order (eegf_tune key 15, see q_walk)
 };
 // key 9: -1 (default) = groups of 4 row panels when the grid is at least 8 tile columns wide (the
 // K = 768 forward / input-gradient GEMMs with N >= 2304: +2-4 %, profiles/r2r_group.log), row-major
@@ -1218,8 +1219,13 @@ __global__ void __launch_bounds__(NT4, 1) gemm4p_kernel(BigArgs g) {
     tile_coords(g, l, tiles_m, tiles_n, tm, tn);
     m0 = __builtin_amdgcn_readfirstlane(tm * TM);
     n0 = __builtin_amdgcn_readfirstlane(tn * TN);
-    bA = g.A + (long)m0 * g.lda;
-    bB = BKC ? g.B + (long)n0 * g.ldb : g.B + n0;
+    int am = m0, bn = n0;
+    if ((g.order & 3) == 2) {    // timing probe: operands from an L2-resident panel set (wrong results)
+      am = __builtin_amdgcn_readfirstlane((((tm & 3) + 4 * (blockIdx.x & 7)) % tiles_m) * TM);
+      bn = __builtin_amdgcn_readfirstlane((tn & 3) % tiles_n * TN);
+    }
+    bA = g.A + (long)am * g.lda;
+    bB = BKC ? g.B + (long)bn * g.ldb : g.B + bn;
   };
   auto stage_first = [&](const bf16* bA, const bf16* bB) {   // K-tiles 0 .. NSLOT4-1 -> slots 0 .. 4
     for (int kt = 0; kt < NSLOT4; ++kt)
@@ -1442,6 +1448,26 @@ constexpr int HSLOT = TM * BKP;                        // one operand of a pair 
 #ifndef EEGF_Q_SPOS
 #define EEGF_Q_SPOS 4      // R5: the group's LDS-DMA part goes after its MFMA EEGF_Q_SPOS (0..7)
 #endif
+// Persistent tile walk of gemm4q (eegf_tune key 15).  order 0 (default): round r of workgroup b takes
+// logical tile r * G + xcd_remap(b), so each round an XCD runs the next contiguous block of 32 tiles of
+// the whole grid.  order 1 (XCD-blocked): XCD x = b % 8 owns the contiguous logical range
+// [x chunk, (x + 1) chunk) of the grouped raster and its G / 8 workgroups walk it in rounds, so an
+// XCD's consecutive rounds stay on the same row panels.  order 2 is a timing probe only (wrong
+// results): every tile reads its operands from 4 row x 4 column panels per XCD (L2-resident), stores
+// where order 0 would.  Probe bits (timing only, wrong results): + 4 no epilogue stores, + 8 no LDS-DMA
+// after the first tile's prologue (the K-loop reads stale LDS), + 16 stores from even workgroups only,
+// + 32 odd workgroups start (g.ksplit / 100) us late (desynchronised epilogues; the delay counts).
+struct QWalk {
+  int L, end, step;
+};
+DEV QWalk q_walk(const BigArgs& g, int ntiles) {
+  const int G = gridDim.x, b = blockIdx.x;
+  if ((g.order & 3) == 1 && G % 8 == 0 && G >= 16) {
+    const int x = b & 7, chunk = (ntiles + 7) / 8;
+    return {x * chunk + (b >> 3), min(ntiles, (x + 1) * chunk), G >> 3};
+  }
+  return {xcd_remap(b, G), ntiles, G};
+}
 template <bool BKC, int EPI, bool ACC = false>
 __global__ void __launch_bounds__(NT4, 1) gemm4q_kernel(BigArgs g) {
   constexpr bool HAS_BIAS = EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_D;
@@ -1454,8 +1480,13 @@ __global__ void __launch_bounds__(NT4, 1) gemm4q_kernel(BigArgs g) {
   const int tiles_n = g.N / TN, tiles_m = g.M / TM, ntiles = tiles_m * tiles_n;
   const int G = gridDim.x;
   const int np = g.K / BKP;                            // pairs per tile (>= 2)
-  int L = xcd_remap(blockIdx.x, G);
-  if (L >= ntiles) return;
+  const QWalk walk = q_walk(g, ntiles);
+  int L = walk.L;
+  if (L >= walk.end) return;
+  if ((g.order & 32) && (blockIdx.x & 1)) {      // timing probe: desynchronise the odd workgroups
+    const long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < g.ksplit) __builtin_amdgcn_s_sleep(2);
+  }
 
   // Staging, 16 parts per pair and wave (8 A, 8 B), each one wave-instruction of 1 KB.
   // K-contiguous part j: rows (8 wave + j) 8 + lane / 8, 16-B chunk lane & 7 of the row's 128 B, read from
@@ -1480,11 +1511,15 @@ __global__ void __launch_bounds__(NT4, 1) gemm4q_kernel(BigArgs g) {
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr_of(lds));
   // ps: pair slot (its A image at 0, B at TM * BKP) or, R5, the operand slot of the part (A parts j < 8,
   // B parts j >= 8)
-  auto stage_part = [&](const bf16* bA, const bf16* bB, int ps, int j) __attribute__((always_inline)) {
+  // NopC: wait states after the M0 write.  The K-loop's bases are SALU-computed (isa_lint: no
+  // VALU-written base within 5 states of any of its DMAs), so its DMAs need only the 1 state after the
+  // M0 write (EEGF_Q_NOP); the prologue's come right after tile_base's v_readfirstlane and keep 3, as
+  // gemm4p's do (once per tile: free), so they stay safe whatever the codegen puts in between
+  using QNOP = std::integral_constant<int, EEGF_Q_NOP>;
+  using PNOP = std::integral_constant<int, 3>;
+  auto stage_part = [&](const bf16* bA, const bf16* bB, int ps, int j, auto NopC) __attribute__((always_inline)) {
     const int jj = j & 7, pr = wave * 8 + jj;
-    // bases SALU-computed in this kernel (isa_lint: no VALU-written base within 5 states of any of its
-    // DMAs), so the DMA needs only the 1 state after its M0 write
-    constexpr int NOP = EEGF_Q_NOP;
+    constexpr int NOP = decltype(NopC)::value;
     const int b0 = R5 ? ps * HSLOT : ps * PSLOT + TM * BKP;    // element offset of the B image
     if (j < 8) {
       glds16_asm_sa<NOP>(bA + (long)pr * 8 * g.lda, voffA, lds0 + 2u * ((R5 ? ps * HSLOT : ps * PSLOT) + pr * 8 * BKP));
@@ -1499,8 +1534,13 @@ __global__ void __launch_bounds__(NT4, 1) gemm4q_kernel(BigArgs g) {
     tile_coords(g, l, tiles_m, tiles_n, tm, tn);
     m0 = __builtin_amdgcn_readfirstlane(tm * TM);
     n0 = __builtin_amdgcn_readfirstlane(tn * TN);
-    bA = g.A + (long)m0 * g.lda;
-    bB = BKC ? g.B + (long)n0 * g.ldb : g.B + n0;
+    int am = m0, bn = n0;
+    if ((g.order & 3) == 2) {    // timing probe: operands from an L2-resident panel set (wrong results)
+      am = __builtin_amdgcn_readfirstlane((((tm & 3) + 4 * (blockIdx.x & 7)) % tiles_m) * TM);
+      bn = __builtin_amdgcn_readfirstlane((tn & 3) % tiles_n * TN);
+    }
+    bA = g.A + (long)am * g.lda;
+    bB = BKC ? g.B + (long)bn * g.ldb : g.B + bn;
   };
   // fragments.  K-contiguous [256][64] image: half h of a pair (K-tile 2t + h) is chunk 4 h + fq of rows
   // r0 + fr (r0 % 16 == 0, so the swizzle is fr & 7); k-major: gemm4p's rd_col offsets, half 1 32 k-rows on
@@ -1537,15 +1577,15 @@ __global__ void __launch_bounds__(NT4, 1) gemm4q_kernel(BigArgs g) {
   int m0, n0;
   tile_base(L, baseA, baseB, m0, n0);
 #pragma unroll 1
-  for (int j = 0; j < 16; ++j) stage_part(baseA, baseB, R5 ? j >> 3 : 0, j);                 // pair 0
+  for (int j = 0; j < 16; ++j) stage_part(baseA, baseB, R5 ? j >> 3 : 0, j, PNOP{});                 // pair 0
 #pragma unroll 1
-  for (int j = 0; j < 16; ++j) stage_part(baseA + BKP, baseB + pstepB, R5 ? 2 + (j >> 3) : 1, j);  // pair 1
+  for (int j = 0; j < 16; ++j) stage_part(baseA + BKP, baseB + pstepB, R5 ? 2 + (j >> 3) : 1, j, PNOP{});  // pair 1
   f32x4 acc[8][8];
   int ps0 = 0;                  // pair slot of the tile's pair 0 (R5: operand slot of its A, 0..4)
   bool landed = false;          // the tile's pairs 0 and 1 retired (cross-staged and waited for)
   for (;;) {
-    const int Ln = L + G;
-    const bool more_tiles = Ln < ntiles;
+    const int Ln = L + walk.step;
+    const bool more_tiles = Ln < walk.end;
     int m0n = 0, n0n = 0;
     const bf16* nA = nullptr;
     const bf16* nB = nullptr;
@@ -1581,7 +1621,7 @@ __global__ void __launch_bounds__(NT4, 1) gemm4q_kernel(BigArgs g) {
       const bf16* nimb = R5 ? lds + add5(hA, 2 * H + 1) * HSLOT : nimg;
       const bool own = !TAIL || t + 2 < np;
       // R5: both K-tiles stage (A of pair t + 2 into pair t - 1's B slot, B into pair t's A slot)
-      const bool st = (R5 || H == 1) && (own || more_tiles);
+      const bool st = (R5 || H == 1) && (own || more_tiles) && !(g.order & 8);
       const int sslot = R5 ? (H == 0 ? add5(hA, 4) : hA) : ps;
       const bf16* sA = own ? baseA + (t + 2) * BKP : nA + (t + 2 - np) * BKP;
       const bf16* sB = own ? baseB + (t + 2) * pstepB : nB + (t + 2 - np) * pstepB;
@@ -1593,7 +1633,7 @@ __global__ void __launch_bounds__(NT4, 1) gemm4q_kernel(BigArgs g) {
 #pragma unroll
       for (int s8 = 0; s8 < 8; ++s8) {
         auto r5st = [&](int pos) __attribute__((always_inline)) {
-          if (R5 && pos == EEGF_Q_SPOS && st) stage_part(sA, sB, sslot, 8 * H + s8);
+          if (R5 && pos == EEGF_Q_SPOS && st) stage_part(sA, sB, sslot, 8 * H + s8, QNOP{});
         };
         mma(s8, 0);
         if (more) fa[H ^ 1][s8] = rdA(nimg, HN{}, s8);
@@ -1604,34 +1644,34 @@ __global__ void __launch_bounds__(NT4, 1) gemm4q_kernel(BigArgs g) {
         r5st(1);
         __builtin_amdgcn_sched_barrier(0);
         if (EEGF_P_STAGGER) {     // wave w: its two parts after MFMAs 2 w and 2 w + 1 of the group
-          if (H == 1 && st && wave == 0) stage_part(sA, sB, ps, 2 * s8);
+          if (H == 1 && st && wave == 0) stage_part(sA, sB, ps, 2 * s8, QNOP{});
           __builtin_amdgcn_sched_barrier(0);
         }
         mma(s8, 2);
         r5st(2);
-        if (!R5 && (EEGF_P_STAGGER ? H == 1 && st && wave == 1 : H == 1 && st)) stage_part(sA, sB, ps, 2 * s8);
-        if (EEGF_P_STAGGER && H == 1 && st && wave == 0) stage_part(sA, sB, ps, 2 * s8 + 1);
+        if (!R5 && (EEGF_P_STAGGER ? H == 1 && st && wave == 1 : H == 1 && st)) stage_part(sA, sB, ps, 2 * s8, QNOP{});
+        if (EEGF_P_STAGGER && H == 1 && st && wave == 0) stage_part(sA, sB, ps, 2 * s8 + 1, QNOP{});
         __builtin_amdgcn_sched_barrier(0);
         mma(s8, 3);
         r5st(3);
-        if (EEGF_P_STAGGER && H == 1 && st && wave == 1) stage_part(sA, sB, ps, 2 * s8 + 1);
+        if (EEGF_P_STAGGER && H == 1 && st && wave == 1) stage_part(sA, sB, ps, 2 * s8 + 1, QNOP{});
         __builtin_amdgcn_sched_barrier(0);
         mma(s8, 4);
         r5st(4);
         if (!R5 && (EEGF_P_STAGGER ? H == 1 && st && wave == 2 : H == 1 && st))
-          stage_part(sA, sB, ps, 2 * s8 + (EEGF_P_STAGGER ? 0 : 1));
+          stage_part(sA, sB, ps, 2 * s8 + (EEGF_P_STAGGER ? 0 : 1), QNOP{});
         __builtin_amdgcn_sched_barrier(0);
         mma(s8, 5);
         r5st(5);
-        if (EEGF_P_STAGGER && H == 1 && st && wave == 2) stage_part(sA, sB, ps, 2 * s8 + 1);
+        if (EEGF_P_STAGGER && H == 1 && st && wave == 2) stage_part(sA, sB, ps, 2 * s8 + 1, QNOP{});
         __builtin_amdgcn_sched_barrier(0);
         mma(s8, 6);
         r5st(6);
-        if (EEGF_P_STAGGER && H == 1 && st && wave == 3) stage_part(sA, sB, ps, 2 * s8);
+        if (EEGF_P_STAGGER && H == 1 && st && wave == 3) stage_part(sA, sB, ps, 2 * s8, QNOP{});
         __builtin_amdgcn_sched_barrier(0);
         mma(s8, 7);
         r5st(7);
-        if (EEGF_P_STAGGER && H == 1 && st && wave == 3) stage_part(sA, sB, ps, 2 * s8 + 1);
+        if (EEGF_P_STAGGER && H == 1 && st && wave == 3) stage_part(sA, sB, ps, 2 * s8 + 1, QNOP{});
         __builtin_amdgcn_sched_barrier(0);
       }
       if (H == 0) {
@@ -1681,7 +1721,7 @@ __global__ void __launch_bounds__(NT4, 1) gemm4q_kernel(BigArgs g) {
     // the next tile's pairs 0 and 1 (cross-staged) retired before the first store
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    p_store_tile<EPI, ACC>(g, acc, biasv, mrow, n0, wn, lane);
+    if (!(g.order & 4) && !((g.order & 16) && (blockIdx.x & 1))) p_store_tile<EPI, ACC>(g, acc, biasv, mrow, n0, wn, lane);
     if (!more_tiles) break;
     L = Ln;
     m0 = m0n;
@@ -1881,6 +1921,8 @@ int cu_count() {
   return cus;
 }
 int g_cu_reserve = 0;      // eegf_tune key 13
+int g_tile_order = [] { const char* e = getenv("EEGF_TILE_ORDER"); return e ? atoi(e) : 0; }();   // key 15
+int g_probe_delay = [] { const char* e = getenv("EEGF_PROBE_DELAY"); return e ? atoi(e) : 0; }();   // key 16: the key-15 + 32 probe's start delay, s_memrealtime ticks (100 MHz)
 }  // namespace
 // workgroups of a persistent grid: every CU but the reserved ones (room for RCCL kernels, key 13)
 int persistent_cus() {
@@ -1904,6 +1946,8 @@ int launch_big(const BigArgs& a, int splits, hipStream_t s) {
       const dim3 grid(tiles < persistent_cus() ? tiles : persistent_cus());
       BigArgs ap = a;
       ap.store_nt = g_store_nt;
+      ap.order = g_tile_order;
+      if (g_tile_order & 32) ap.ksplit = g_probe_delay;
       bool acc = false;
       if constexpr (EPI == EPI_NONE) acc = a.beta != 0.f;
       // whole-line staging (gemm4q) wherever K splits into >= 2 pairs of K-tiles (key 14 = 2, default):
@@ -2154,6 +2198,8 @@ extern "C" int eegf_tune(int key, int value) {
   if (key == 11) { const int o = g_gemm4p; if (value < 0 || value > 3) return EEGF_ERR_ARG; g_gemm4p = value; return o; }
   if (key == 14) { const int o = g_gemm4q; if (value < 0 || value > 2) return EEGF_ERR_ARG; g_gemm4q = value; return o; }
   if (key == 13) { const int o = g_cu_reserve; if (value < 0 || value >= cu_count()) return EEGF_ERR_ARG; g_cu_reserve = value; return o; }
+  if (key == 15) { const int o = g_tile_order; if (value < 0 || value > 63 || (value & 3) == 3) return EEGF_ERR_ARG; g_tile_order = value; return o; }
+  if (key == 16) { const int o = g_probe_delay; g_probe_delay = value; return o; }
   if (key == 6) { const int o = g_ln_rpw; if (value < 1 || value > 64) return EEGF_ERR_ARG; g_ln_rpw = value; return o; }
   return EEGF_ERR_ARG;
 }

@@ -63,7 +63,30 @@ def build(verbose: bool = False, jobs: int | None = None) -> Path:
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+        _lint(LIB_PATH)
     return LIB_PATH
+
+
+def _lint(lib: Path) -> None:
+    """The post-link ISA lint (tools/isa_lint.py) as a failing build step: the hand-written LDS-DMA asm
+    relies on wait states hipcc never inserts inside asm (a VALU-written SGPR base read within 5 states,
+    an M0 write within 1, a sign-extended address word), so a library with any such site is renamed
+    aside and the build fails instead of shipping it."""
+    tool = ROOT.parent / "tools" / "isa_lint.py"
+    if not tool.exists():              # a package copied without the repository's tools/
+        return
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("eegf_isa_lint", tool)
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules[spec.name] = mod           # the tool's dataclasses resolve their module by name
+    spec.loader.exec_module(mod)
+    findings, _ = mod.lint(lib)
+    if findings:
+        bad = lib.with_name(lib.name + ".hazards")
+        lib.replace(bad)
+        head = "\n".join(f"  {f.kind}: {f.func} @0x{f.addr:x}: '{f.inst}' {f.states} state(s) after '{f.writer}'"
+                          for f in findings[:10])
+        raise RuntimeError(f"ISA lint: {len(findings)} hazard site(s) in {lib.name} (moved to {bad.name}):\n{head}")
 
 
 if __name__ == "__main__":

@@ -769,7 +769,7 @@ class FusionEngine:
             self._ev_end("attn_fwd", ev, 4.0 * B * NH * L * L * DH)
             ao = self.ws.get("ao", R * HID, self.dt).view(R, HID)
             self.linear(ctx, self.W(pre + "attention.output.dense.weight"), self.F(pre + "attention.output.dense.bias"),
-                        ao, R)
+                        ao, R, tag="ao_fwd")
             a1 = self.empty(R, HID)
             s1, m1, r1 = (self.empty(R, HID), self._f32(R), self._f32(R)) if save else (None, None, None)
             self.ln_fwd(ao, h, pre + "attention.output.LayerNorm", R, a1, s1, m1, r1, 1e-12, pdrop, 1,
@@ -778,7 +778,8 @@ class FusionEngine:
             ffgd = self.empty(R, FFN) if save else None
             ffact = self.empty(R, FFN) if save else self.ws.get("ffact", R * FFN, self.dt).view(R, FFN)
             self.linear(a1, self.W(pre + "intermediate.dense.weight"), self.F(pre + "intermediate.dense.bias"), ffact,
-                        R, epi=_lib.EPI_BIAS_GELU_D if save else _lib.EPI_BIAS_GELU, aux=ffgd, tag="ffn1_fwd")
+                        R, epi=_lib.EPI_BIAS_GELU_D if save else _lib.EPI_BIAS_GELU, aux=ffgd,
+                        tag="ffn1_fwd_gd" if save else "ffn1_fwd")
             fo = self.ws.get("fo", R * HID, self.dt).view(R, HID)
             self.linear(ffact, self.W(pre + "output.dense.weight"), self.F(pre + "output.dense.bias"), fo, R,
                         tag="ffn2_fwd")

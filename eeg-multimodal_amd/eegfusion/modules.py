@@ -92,20 +92,27 @@ _LAYER_MATRICES = ("attention.self.query.weight", "attention.self.key.weight", "
 
 
 def _qkv_first_order(named):
-    """Arena order: each BERT layer's six weight matrices first and back to back (Q|K|V adjacent, so
-    the fused QKV projection reads one [2304, 768] matrix; the whole block is one contiguous
-    gradient range that the DDP reducer all-reduces as soon as that layer's backward is done),
-    then its Q/K/V biases (adjacent) and the remaining vectors in module order."""
+    """Arena order: every BERT layer's six weight matrices first, layer after layer with no gap (Q|K|V
+    adjacent, so the fused QKV projection reads one [2304, 768] matrix; each layer's block is one
+    contiguous gradient range that the DDP reducer all-reduces as soon as that layer's backward is
+    done, and the blocks of consecutive layers are adjacent, so a reducer bucket of several layers is
+    one contiguous range too), then the remaining parameters in module order with each layer's Q/K/V
+    biases adjacent."""
     named = list(named)
     byname = dict(named)
     out, seen = [], set()
+    for n, _ in named:
+        if n.endswith("attention.self.query.weight"):
+            base = n[: -len("attention.self.query.weight")]
+            for k in _LAYER_MATRICES:
+                out.append((base + k, byname[base + k]))
+                seen.add(base + k)
     for n, p in named:
         if n in seen:
             continue
-        if n.endswith("attention.self.query.weight"):
-            base = n[: -len("attention.self.query.weight")]
-            for k in _LAYER_MATRICES + ("attention.self.query.bias", "attention.self.key.bias",
-                                        "attention.self.value.bias"):
+        if n.endswith("attention.self.query.bias"):
+            base = n[: -len("attention.self.query.bias")]
+            for k in ("attention.self.query.bias", "attention.self.key.bias", "attention.self.value.bias"):
                 out.append((base + k, byname[base + k]))
                 seen.add(base + k)
         else:
@@ -157,9 +164,12 @@ class FusionModel(nn.Module):
     def __init__(self, variant: str, contract: str = "T", eps: float = 1.0, eps_mode: str = "newfrac",
                  dtype: torch.dtype = torch.float32, eeg_channels: int = 64, act_dim: int = 32, frame_dim: int = 512,
                  with_dp: bool = True, dp_init: torch.Tensor | None = None, dropout: float = 0.1, seed: int = 980616,
-                 tau: float = 1.0, modal: str = "ti"):
+                 tau: float = 1.0, modal: str = "ti", host_path: bool = False):
         super().__init__()
         self._variant, self._contract, self._modal = variant, contract, modal
+        # host_path=True: run the torch-op host path (cpu_path) while the model is in host memory even
+        # when a GPU is present (e.g. CPU evaluation beside a busy GPU); otherwise that case is refused
+        self.host_path = bool(host_path)
         # module sets of the custom_models variants (models.py:28-272): no BERT in IICA, no visual
         # encoder in TTCA, a TransformerEncoder instead of the decoder in TISC
         if modal != "ii":
@@ -255,10 +265,11 @@ class FusionModel(nn.Module):
                                "call model.cuda()")
         # the host path serves machines without a GPU (BASELINE configs[0]); on a GPU machine a model
         # left in host memory is almost always a forgotten .cuda() and would run orders of magnitude
-        # slower without a word, so it is refused unless asked for explicitly
-        if torch.cuda.is_available() and os.environ.get("EEGF_HOST_PATH") != "1":
+        # slower without a word, so it is refused unless the model asks for it (host_path=True, or the
+        # process-wide EEGF_HOST_PATH=1 for scripts that cannot pass the argument)
+        if torch.cuda.is_available() and not self.host_path and os.environ.get("EEGF_HOST_PATH") != "1":
             raise RuntimeError("eegfusion: the model is in host memory while a GPU is present; call model.cuda() "
-                               "(or set EEGF_HOST_PATH=1 to run the torch-op host path on purpose)")
+                               "(or construct it with host_path=True to run the torch-op host path on purpose)")
         return True
 
     def _run(self, batch: dict, hard: bool) -> torch.Tensor:

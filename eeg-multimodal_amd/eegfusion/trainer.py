@@ -90,16 +90,21 @@ class GradReducer:
     but the ranges are still recorded (`self.log`), so a single-GPU test can check coverage.
     """
 
-    def __init__(self, bucket_elems: int = 32 << 20, scale_in_optimizer: bool = False, coalesce_elems: int = 1 << 20):
-        self.bucket = bucket_elems
+    def __init__(self, bucket_elems: int = 32 << 20, scale_in_optimizer: bool = False, coalesce_elems: int = 1 << 20,
+                 merge_elems: int = 0):
+        self.bucket = int(bucket_elems)
         # ranges shorter than this, issued together, are gathered into one staging buffer and reduced by
         # one collective (the 37 bias / LayerNorm / embedding ranges of the BERT step at finish(), the
         # 23 decoder / head matrices before the encoder backward): one RCCL launch instead of dozens of
-        # latency-bound small ones; 0 disables
-        self.coalesce = int(coalesce_elems)
+        # latency-bound small ones; 0 disables.  At most half a bucket, so two always share one.
+        self.coalesce = min(int(coalesce_elems), self.bucket // 2)
+        # ready() ranges are held until they add up to merge_elems, then issued together (adjacent
+        # ranges merged: consecutive BERT layers' blocks are adjacent in the arena, so a bucket of k
+        # layers is one collective); 0 (default) issues every ready() group at once
+        self.merge = int(merge_elems)
         self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
         self.scale_in_optimizer = bool(scale_in_optimizer)
-        self.works, self.todo, self.log, self.staged = [], set(), [], []
+        self.works, self.todo, self.log, self.staged, self.pending = [], set(), [], [], []
         self.n_coalesced = 0            # staged collectives issued since begin()
         self.arena = None
 
@@ -121,7 +126,7 @@ class GradReducer:
         return arena.ranges(names)
 
     def begin(self, arena, names):
-        self.arena, self.todo, self.works, self.log, self.staged = arena, set(names), [], [], []
+        self.arena, self.todo, self.works, self.log, self.staged, self.pending = arena, set(names), [], [], [], []
         self.n_coalesced = 0
 
     def ready(self, names):
@@ -129,35 +134,67 @@ class GradReducer:
         if not names:
             return
         self.todo.difference_update(names)
-        self._launch(self.ranges(self.arena, names))
+        rngs = self.ranges(self.arena, names)
+        if self.merge <= 0:
+            self._launch(rngs)
+            return
+        self.pending += rngs
+        if sum(hi - lo for lo, hi in self.pending) >= self.merge:
+            self._flush()
+
+    def _flush(self):
+        if self.pending:
+            rngs, self.pending = _merge_adjacent(self.pending), []
+            self._launch(rngs)
+
+    def plan(self, rngs) -> list[list[tuple[int, int]]]:
+        """The collectives for these ranges, in issue order: each entry is a list of ranges reduced by one
+        collective.  Runs of small ranges (< coalesce elements) are gathered into groups of at most one
+        bucket (staged through one buffer); a small range that would sit alone is reduced on its own;
+        every other range is cut into bucket-sized pieces."""
+        rngs = list(rngs)
+        small = [r for r in rngs if r[1] - r[0] < self.coalesce]
+        groups, cur, n = [], [], 0
+        for r in small:
+            if cur and n + r[1] - r[0] > self.bucket:
+                groups.append(cur)
+                cur, n = [], 0
+            cur.append(r)
+            n += r[1] - r[0]
+        if cur:
+            groups.append(cur)
+        out = [g for g in groups if len(g) > 1]
+        alone = {g[0] for g in groups if len(g) == 1}
+        for lo, hi in rngs:
+            if hi - lo < self.coalesce and (lo, hi) not in alone:
+                continue
+            out += [[(i, min(hi, i + self.bucket))] for i in range(lo, hi, self.bucket)]
+        return out
 
     def _launch(self, rngs):
-        g = self.arena.grad
-        rngs = list(rngs)
-        small = [(lo, hi) for lo, hi in rngs if hi - lo < self.coalesce]
-        while len(small) > 1:               # gather runs of small ranges (<= one bucket each) into one buffer
-            grp, n = [], 0
-            while small and n + small[0][1] - small[0][0] <= self.bucket:
-                grp.append(small.pop(0))
-                n += grp[-1][1] - grp[-1][0]
-            if len(grp) < 2:
-                small = grp + small
-                break
-            rngs = [r for r in rngs if r not in grp]
+        for grp in self.plan(rngs):
             self.log.extend(grp)
-            self.n_coalesced += 1
-            if self.world > 1:
-                buf = torch.cat([g[lo:hi] for lo, hi in grp])
-                self.works.append(dist.all_reduce(buf, op=dist.ReduceOp.SUM, async_op=True))
-                self.staged.append((grp, buf))
-        for lo, hi in rngs:
-            for i in range(lo, hi, self.bucket):
-                j = min(hi, i + self.bucket)
-                self.log.append((i, j))
-                if self.world > 1:
-                    self.works.append(dist.all_reduce(g[i:j], op=dist.ReduceOp.SUM, async_op=True))
+            if len(grp) > 1:
+                self.n_coalesced += 1
+                self._issue_staged(grp)
+            else:
+                self._issue(*grp[0])
+
+    def _issue(self, lo: int, hi: int):
+        """one collective over the arena gradient range [lo, hi)"""
+        if self.world > 1:
+            self.works.append(dist.all_reduce(self.arena.grad[lo:hi], op=dist.ReduceOp.SUM, async_op=True))
+
+    def _issue_staged(self, grp):
+        """one collective over several ranges gathered into a staging buffer (copied back in finish)"""
+        if self.world > 1:
+            g = self.arena.grad
+            buf = torch.cat([g[lo:hi] for lo, hi in grp])
+            self.works.append(dist.all_reduce(buf, op=dist.ReduceOp.SUM, async_op=True))
+            self.staged.append((grp, buf))
 
     def finish(self, lo: int, hi: int):
+        self._flush()
         if self.todo:
             self._launch(self.ranges(self.arena, self.todo))
             self.todo = set()
@@ -170,6 +207,17 @@ class GradReducer:
         self.staged = []
         if self.world > 1 and not self.scale_in_optimizer:
             self.arena.grad[lo:hi].mul_(1.0 / self.world)
+
+
+def _merge_adjacent(rngs):
+    """sorted ranges with touching neighbours joined (consecutive BERT layer blocks become one range)"""
+    out = []
+    for lo, hi in sorted(rngs):
+        if out and lo <= out[-1][1]:
+            out[-1] = (out[-1][0], max(out[-1][1], hi))
+        else:
+            out.append((lo, hi))
+    return out
 
 
 class PriGumbelTrainer:

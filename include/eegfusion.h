@@ -91,7 +91,14 @@ int eegf_tune(int key, int value);
  *   key 14: the persistent GEMMs with K % 64 == 0, K >= 128 on gemm4q (K-tile pairs staged in whole
  *          128-B lines, five 32-KB operand slots): 2 (default) every such GEMM, 1 the forward layout
  *          (both operands K-contiguous) only, 0 none (gemm4p); bit-identical results
- *          (tests/test_gemm_gpu.py), env EEGF_GEMM4Q. */
+ *          (tests/test_gemm_gpu.py), env EEGF_GEMM4Q.
+ *   key 15: gemm4q's persistent tile walk: 0 (default) round-major (each round an XCD takes the next
+ *          32 tiles of the whole grid), 1 XCD-blocked (each XCD walks its own contiguous eighth of the
+ *          grouped raster), 2 a timing probe with L2-resident operands (wrong results); probe bits
+ *          (timing only, wrong results): + 4 no epilogue stores, + 8 no staging after the prologue,
+ *          + 16 stores from even workgroups only, + 32 odd workgroups start key-16 ticks (100 MHz)
+ *          late; env EEGF_TILE_ORDER.
+ *   key 16: the start delay of the key-15 + 32 probe. */
 /* Diagnostics (no reference counterpart): every following 256-row GEMM launch of the 8-wave / 4-wave
  * kernels writes 4 s_memrealtime stamps per workgroup (start, prologue done, K-loop done, epilogue
  * issued, slot 4 the CU id) into buf = int64 [grid.y][grid.x][8]; nullptr switches it off.  tools/gemm_phases.py. */

@@ -111,7 +111,7 @@ def test_host_model_refuses_device_inputs():
 
 def test_host_model_refused_when_a_gpu_is_present(monkeypatch):
     """A model left in host memory on a GPU machine is a forgotten .cuda(): refused with a pointer to it,
-    unless EEGF_HOST_PATH=1 asks for the host path explicitly."""
+    unless the model asks for the host path explicitly (host_path=True, or EEGF_HOST_PATH=1)."""
     from eegfusion.modules import ConcatModel
     m = ConcatModel(contract="W", dropout=0.0)
     x = torch.empty(0)
@@ -124,6 +124,8 @@ def test_host_model_refused_when_a_gpu_is_present(monkeypatch):
     monkeypatch.setattr(torch.cuda, "is_available", lambda: False)
     monkeypatch.delenv("EEGF_HOST_PATH")
     assert m._host(x)
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    assert ConcatModel(contract="W", dropout=0.0, host_path=True)._host(x)
 
 
 def test_host_tokens_cut_only_without_dropout(monkeypatch):

@@ -230,7 +230,7 @@ def test_attention_fwd_bwd(dt, L, masked, pdrop, use_bits):
 
 @pytest.mark.parametrize("pdrop", [1e-6, 0.1])
 def test_attention256_exports_keep_bits(pdrop):
-    """The L = 256 forward with a drop_bits buffer (the engine's path since round 4): identical output
+    """The L = 256 forward with a drop_bits buffer (the engine's path with cfg.attn_bits / EEGF_ATTN_BITS=1): identical output
     bits to the forward without it, the exported mask equals the Philox replay (p = 1e-6 < 2^-16: every
     probability kept, all-ones words), and the backward reading the bits equals the one regenerating."""
     lib = _lib()

@@ -92,6 +92,12 @@ def run(name, M, N, Kd, layout, epi, iters=20):
         r = {v: [] for v in VARIANTS}
         for _ in range(5):
             for v in VARIANTS:
+                if KEY is not None:       # --key=K: the variants are values of eegf_tune key K
+                    lib.eegf_tune(KEY, v)
+                    f()
+                    torch.cuda.synchronize()
+                    r[v].append(timed(f, iters))
+                    continue
                 # -1: default routing; 0: 2-phase 8-wave; 4: 8-phase 8-wave; 8: 4-wave (key 1 = 6);
                 # 9: default routing with the 256x128 two-workgroup kernel for every short-K GEMM (key 8)
                 # 20 + G: default routing with the grouped tile raster of G row panels (key 9)
@@ -101,12 +107,15 @@ def run(name, M, N, Kd, layout, epi, iters=20):
                 f()
                 torch.cuda.synchronize()
                 r[v].append(timed(f, iters))
-        lib.eegf_tune(1, -1)
-        lib.eegf_tune(8, 2)
-        lib.eegf_tune(9, -1)
+        if KEY is not None:
+            lib.eegf_tune(KEY, VARIANTS[0])
+        else:
+            lib.eegf_tune(1, -1)
+            lib.eegf_tune(8, 2)
+            lib.eegf_tune(9, -1)
         med = {v: sorted(x)[len(x) // 2] for v, x in r.items()}
         tt = timed(tf, iters)
-        print(f"{name:16s} {M}x{N}x{Kd} " + " | ".join(f"v{v} {tf_(med[v]):6.1f}" for v in med)
+        print(f"{name:16s} {M}x{N}x{Kd} " + " | ".join(f"v{v} {tf_(med[v]):6.1f} ({med[v] * 1e3:5.1f} us)" for v in med)
               + f" | torch {tf_(tt):6.1f} TF", flush=True)
         return
     res = []
@@ -121,6 +130,7 @@ def run(name, M, N, Kd, layout, epi, iters=20):
 
 
 AB = "--ab" in sys.argv
+KEY = next((int(a.split("=")[1]) for a in sys.argv if a.startswith("--key=")), None)
 VARIANTS = [int(x) for x in next((a.split("=")[1] for a in sys.argv if a.startswith("--variants=")), "-1,0,4,8").split(",")]
 
 

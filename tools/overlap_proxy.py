@@ -13,7 +13,12 @@ all-reduce kernel) on a side stream, and reports
     whether it finished before the backward's last kernel (how much of the "all-reduce" overlapped);
   * the same with the persistent grids capped at cu_count - k (eegf_tune key 13) for k in --reserve.
 
+The proxy reducer is the shipped GradReducer with only its collectives replaced, so the ranges, the
+coalesced small-range groups and the merged multi-layer buckets (--merge) are the ones a world > 1
+step issues.
+
 Usage: python tools/overlap_proxy.py [--rounds 5] [--steps 6] [--wgs 32] [--passes 2] [--reserve 0,8,16]
+       [--merge 0,21233664,42467328]
 """
 import argparse
 import json
@@ -32,7 +37,9 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--wgs", type=int, default=32)
     ap.add_argument("--passes", type=int, default=2)
-    ap.add_argument("--reserve", default="0,8,16")
+    ap.add_argument("--reserve", default="0")
+    ap.add_argument("--merge", default="0",
+                    help="comma-separated GradReducer merge_elems values to compare (0: one collective per layer)")
     args = ap.parse_args()
     from eegfusion import _lib
     from eegfusion._lib import call
@@ -40,39 +47,50 @@ def main():
     from eegfusion.trainer import GradReducer, PriGumbelTrainer
 
     class ProxyReducer(GradReducer):
-        """GradReducer whose 'all-reduce' is the ring proxy on a side stream (timed per range)."""
+        """The shipped GradReducer (its plan: coalesced small ranges, merged layer buckets, bucket cuts)
+        with every collective replaced by the ring proxy on a side stream (timed per collective)."""
 
-        def __init__(self, on):
-            super().__init__(scale_in_optimizer=True)
+        def __init__(self, on, merge):
+            super().__init__(scale_in_optimizer=True, merge_elems=merge)
             self.on = on
             self.side = torch.cuda.Stream()
             self.recs, self.bwd_end = [], None
 
-        def _launch(self, rngs):
-            g = self.arena.grad
-            for lo, hi in rngs:
-                for i in range(lo, hi, self.bucket):
-                    j = min(hi, i + self.bucket)
-                    self.log.append((i, j))
-                    n = (j - i) // 4 * 4
-                    if not self.on or n <= 0 or (g[i:].data_ptr() & 15):
-                        continue
-                    issue = torch.cuda.Event(enable_timing=True)
-                    issue.record()                                  # compute stream reached grad_ready
-                    self.side.wait_event(issue)
-                    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                    s.record(self.side)
-                    call("eegf_ring_proxy", n, args.passes, args.wgs, g[i:].data_ptr(), self.side.cuda_stream)
-                    e.record(self.side)
-                    self.recs.append((issue, s, e, n * 4))
+        def _proxy(self, ptr, n):
+            n = n // 4 * 4
+            if not self.on or n <= 0 or (ptr & 15):
+                return
+            issue = torch.cuda.Event(enable_timing=True)
+            issue.record()                                  # compute stream reached grad_ready
+            self.side.wait_event(issue)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record(self.side)
+            call("eegf_ring_proxy", n, args.passes, args.wgs, ptr, self.side.cuda_stream)
+            e.record(self.side)
+            self.recs.append((issue, s, e, n * 4))
+
+        def _issue(self, lo, hi):
+            self._proxy(self.arena.grad[lo:].data_ptr(), hi - lo)
+
+        def _issue_staged(self, grp):
+            if self.on:                                     # the staging copy runs on the compute stream
+                g = self.arena.grad
+                buf = torch.cat([g[lo:hi] for lo, hi in grp])
+                self.staged.append((grp, buf))
+                self._proxy(buf.data_ptr(), buf.numel())
 
         def finish(self, lo, hi):
+            self._flush()
             if self.todo:
                 self._launch(self.ranges(self.arena, self.todo))
                 self.todo = set()
             self.bwd_end = torch.cuda.Event(enable_timing=True)
             self.bwd_end.record()                                   # the backward's last kernel is done here
             torch.cuda.current_stream().wait_stream(self.side)
+            g = self.arena.grad
+            for grp, buf in self.staged:
+                torch._foreach_copy_([g[a:b] for a, b in grp], list(buf.split([b - a for a, b in grp])))
+            self.staged = []
 
     lib = _lib.lib()
     dev = torch.device("cuda")
@@ -84,8 +102,9 @@ def main():
              "act": torch.randn(B, 32, generator=gen, device=dev) * 0.5}
     labels = (torch.rand(B, generator=gen, device=dev) < 0.66).long()
     reserves = [int(x) for x in args.reserve.split(",")]
-    modes = [(r, on) for r in reserves for on in (False, True)]
-    trainers = {mode: PriGumbelTrainer(m.engine, lr=1e-6, reducer=ProxyReducer(mode[1])) for mode in modes}
+    merges = [int(float(x)) for x in args.merge.split(",")]
+    modes = [(r, False, 0) for r in reserves] + [(r, True, mg) for r in reserves for mg in merges]
+    trainers = {mode: PriGumbelTrainer(m.engine, lr=1e-6, reducer=ProxyReducer(mode[1], mode[2])) for mode in modes}
     times = {mode: [] for mode in modes}
     stats = {mode: [] for mode in modes}
     old = lib.eegf_tune(13, 0)
@@ -118,7 +137,7 @@ def main():
     for mode in modes:
         t = sorted(times[mode])
         med = t[len(t) // 2]
-        row = {"cu_reserve": mode[0], "proxy": mode[1], "ms_per_step": round(med, 3),
+        row = {"cu_reserve": mode[0], "proxy": mode[1], "merge_elems": mode[2], "ms_per_step": round(med, 3),
                "samples_per_s": round(B / med * 1e3, 1), "all_ms": [round(x, 3) for x in times[mode]]}
         st = stats[mode]
         if st:

@@ -1,7 +1,8 @@
 // ubench.hip — issue cost of single VALU instructions on gfx950 (diagnostic, tools/ubench.py).
 // Each wave runs ITERS x 8 independent copies of one instruction (8 separate destination registers,
 // so throughput, not latency, is measured) between two s_memtime stamps; cycles per instruction =
-// delta / (ITERS * 8).  Launched with 1 or 2 waves per SIMD.
+// delta / (ITERS * 8).  Launched with 1 or 2 waves per SIMD; the s_memrealtime (100 MHz) delta gives
+// the wall time, so the SIMD's aggregate issue rate at 2 waves is comparable with 1.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -12,11 +13,12 @@
                : "v"(a), "v"(b))
 
 template <int OP>
-__global__ void __launch_bounds__(256) ubench_kernel(int iters, uint32_t seed, long long* cyc, uint32_t* sink) {
+__global__ void __launch_bounds__(512) ubench_kernel(int iters, uint32_t seed, long long* cyc, uint32_t* sink) {
   uint32_t r0 = seed ^ threadIdx.x, r1 = r0 + 1, r2 = r0 + 2, r3 = r0 + 3, r4 = r0 + 4, r5 = r0 + 5, r6 = r0 + 6,
            r7 = r0 + 7;
   uint32_t a = seed * 3u + threadIdx.x, b = seed * 7u + 1u;
   const long long t0 = __builtin_amdgcn_s_memtime();
+  const long long r0t = __builtin_amdgcn_s_memrealtime();
   for (int i = 0; i < iters; ++i) {
     if constexpr (OP == 0) BODY8("v_add_u32");
     if constexpr (OP == 1) BODY8("v_mul_lo_u32");
@@ -57,7 +59,11 @@ __global__ void __launch_bounds__(256) ubench_kernel(int iters, uint32_t seed, l
     }
   }
   const long long t1 = __builtin_amdgcn_s_memtime();
-  if (threadIdx.x % 64 == 0) cyc[blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64] = t1 - t0;
+  const long long r1t = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x % 64 == 0) {     // [wave][2]: s_memtime ticks, s_memrealtime ticks (100 MHz)
+    cyc[2 * (blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64)] = t1 - t0;
+    cyc[2 * (blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) + 1] = r1t - r0t;
+  }
   sink[blockIdx.x * blockDim.x + threadIdx.x] = r0 ^ r1 ^ r2 ^ r3 ^ r4 ^ r5 ^ r6 ^ r7;
 }
 

@@ -15,17 +15,20 @@ def main():
     lib = ctypes.CDLL(str(Path(__file__).resolve().parent / "libubench.so"))
     blocks, iters = 256, 2000
     torch.zeros(1, device="cuda")
-    for threads in (256,):
+    for threads in (256, 512):
         for op, name in enumerate(OPS):
-            cyc = torch.zeros(blocks * threads // 64, dtype=torch.int64, device="cuda")
+            cyc = torch.zeros(2 * blocks * threads // 64, dtype=torch.int64, device="cuda")
             sink = torch.zeros(blocks * threads, dtype=torch.int32, device="cuda")
             for _ in range(2):
                 rc = lib.ubench(op, blocks, threads, iters, ctypes.c_void_p(cyc.data_ptr()),
                                 ctypes.c_void_p(sink.data_ptr()))
                 assert rc == 0, rc
             torch.cuda.synchronize()
-            c = cyc.double().sort().values
-            print(f"{name:16s} waves/SIMD {threads // 256}: {float(c[len(c) // 2]) / (iters * 8):6.2f} cyc/inst",
+            c = cyc.view(-1, 2)[:, 0].double().sort().values
+            rt = cyc.view(-1, 2)[:, 1].double().sort().values
+            ns = float(rt[len(rt) // 2]) * 10.0 / (iters * 8)       # wall ns per instruction of one wave
+            print(f"{name:16s} waves/SIMD {threads // 256}: {float(c[len(c) // 2]) / (iters * 8):6.2f} cyc/inst "
+                  f"(s_memtime)  {ns:6.3f} ns/inst per wave  SIMD rate {threads // 256 / ns:6.3f} inst/ns",
                   flush=True)
 
 
