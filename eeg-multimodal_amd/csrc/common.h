@@ -224,34 +224,33 @@ DEV float gelu_grad(float x) {
   const float e = __expf(-0.5f * x * x);
   return 0.5f * (1.0f + erf_half(x, e)) + x * 0.39894228040143268f * e;
 }
-// Packed-fp32 GELU on pairs (v_pk_fma/mul_f32 for the polynomial and products; exp2/rcp per lane):
-// the same A&S 7.1.26 erf as erf_half, ~35 % fewer VALU slots than two scalar evaluations.
+// Packed-fp32 GELU on pairs: the upper normal tail q = 1 - Phi(|x|) = phi(x) t P(t), t = 1 / (1 + p |x|)
+// (A&S 26.2.17, the same approximation as erf_half's 7.1.26 with its constants folded: |error| of Phi
+// <= 7.5e-8), phi(x) = exp2(-x^2 log2(e) / 2 - log2(sqrt(2 pi))) the normal density, so
+// Phi(x) = 0.5 + copysign(0.5 - q, x), gelu = x Phi and gelu' = Phi + x phi.  19 VALU per pair (gelu'), 18
+// (gelu): the epilogue that runs it is VALU-issue-bound (profiles/r5d_sink_ab.log, r5j_*).
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 DEV void gelu2(f32x2 x, f32x2& gl, f32x2* gd) {
   const f32x2 x2 = x * x;
-  const f32x2 ea = x2 * (-0.72134752044448170f);               // -x^2/2 * log2(e)
-  f32x2 e;
+  const f32x2 ea = x2 * (-0.72134752044448170f) + (-1.3257480647361593f);     // log2 phi(x)
+  f32x2 e;                                                                     // phi(x)
   e.x = __builtin_amdgcn_exp2f(ea.x);
   e.y = __builtin_amdgcn_exp2f(ea.y);
-  f32x2 ax;
-  ax.x = fabsf(x.x);
-  ax.y = fabsf(x.y);
-  const f32x2 d = ax * 0.23164189758523371f + 1.0f;            // 1 + p |x|/sqrt2
-  f32x2 t;
-  t.x = __builtin_amdgcn_rcpf(d.x);
-  t.y = __builtin_amdgcn_rcpf(d.y);
-  f32x2 poly = t * 1.061405429f + (-1.453152027f);
-  poly = poly * t + 1.421413741f;
-  poly = poly * t + (-0.284496736f);
-  poly = poly * t + 0.254829592f;
+  f32x2 t;                               // scalar FMAs take |x| as a free source modifier
+  t.x = __builtin_amdgcn_rcpf(fmaf(fabsf(x.x), 0.23164188826636040f, 1.0f));
+  t.y = __builtin_amdgcn_rcpf(fmaf(fabsf(x.y), 0.23164188826636040f, 1.0f));
+  f32x2 poly = t * 1.3302744295891231f + (-1.8212559791077754f);
+  poly = poly * t + 1.7814779365698128f;
+  poly = poly * t + (-0.35656378124891560f);
+  poly = poly * t + 0.31938153025994087f;
   poly = poly * t;
-  const f32x2 u = (poly * e) * (-0.5f) + 0.5f;                 // (1 - erf(|x|/sqrt2)) / 2 mirrored
-  f32x2 us;
-  us.x = copysignf(u.x, x.x);
-  us.y = copysignf(u.y, x.y);
-  const f32x2 h = us + 0.5f;                                   // Phi(x) = (1 + erf(x/sqrt2)) / 2
+  const f32x2 qm = poly * e + (-0.5f);                                         // q - 0.5 <= 0
+  f32x2 us;                                                                    // sign(x) (0.5 - q)
+  us.x = copysignf(qm.x, x.x);
+  us.y = copysignf(qm.y, x.y);
+  const f32x2 h = us + 0.5f;                                                   // Phi(x)
   gl = x * h;
-  if (gd) *gd = (x * e) * 0.39894228040143268f + h;            // Phi(x) + x phi(x)
+  if (gd) *gd = x * e + h;                                                     // Phi(x) + x phi(x)
 }
 
 // gelu(x) and gelu'(x) together (one exp, one erf): the forward stores gelu' for the backward
