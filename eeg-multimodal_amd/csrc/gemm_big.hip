@@ -1072,39 +1072,11 @@ DEV void load_tile16(uint4 (&c)[8][4], const bf16* const (&p)[8]) {
       : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "v"(p[4]), "v"(p[5]), "v"(p[6]), "v"(p[7])
       : "memory");
 }
-// the 64-column forms for gemm4q's 8-wave layout (128 x 64 wave tiles): 4 bias quads, 2 chunks per row
-DEV void load_bias4(f32x4 (&b)[4], const float* p) {
-  asm volatile(
-      "global_load_dwordx4 %0, %4, off\n\tglobal_load_dwordx4 %1, %4, off offset:64\n\t"
-      "global_load_dwordx4 %2, %4, off offset:128\n\tglobal_load_dwordx4 %3, %4, off offset:192\n\t"
-      "s_waitcnt vmcnt(0)"
-      : "=&v"(b[0]), "=&v"(b[1]), "=&v"(b[2]), "=&v"(b[3])
-      : "v"(p)
-      : "memory");
-}
-DEV void load_tile8(uint4 (&c)[8][2], const bf16* const (&p)[8]) {
-  asm volatile(
-      "global_load_dwordx4 %0, %16, off\n\tglobal_load_dwordx4 %1, %16, off offset:64\n\t"
-      "global_load_dwordx4 %2, %17, off\n\tglobal_load_dwordx4 %3, %17, off offset:64\n\t"
-      "global_load_dwordx4 %4, %18, off\n\tglobal_load_dwordx4 %5, %18, off offset:64\n\t"
-      "global_load_dwordx4 %6, %19, off\n\tglobal_load_dwordx4 %7, %19, off offset:64\n\t"
-      "global_load_dwordx4 %8, %20, off\n\tglobal_load_dwordx4 %9, %20, off offset:64\n\t"
-      "global_load_dwordx4 %10, %21, off\n\tglobal_load_dwordx4 %11, %21, off offset:64\n\t"
-      "global_load_dwordx4 %12, %22, off\n\tglobal_load_dwordx4 %13, %22, off offset:64\n\t"
-      "global_load_dwordx4 %14, %23, off\n\tglobal_load_dwordx4 %15, %23, off offset:64\n\t"
-      "s_waitcnt vmcnt(0)"
-      : "=&v"(c[0][0]), "=&v"(c[0][1]), "=&v"(c[1][0]), "=&v"(c[1][1]), "=&v"(c[2][0]), "=&v"(c[2][1]),
-        "=&v"(c[3][0]), "=&v"(c[3][1]), "=&v"(c[4][0]), "=&v"(c[4][1]), "=&v"(c[5][0]), "=&v"(c[5][1]),
-        "=&v"(c[6][0]), "=&v"(c[6][1]), "=&v"(c[7][0]), "=&v"(c[7][1])
-      : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "v"(p[4]), "v"(p[5]), "v"(p[6]), "v"(p[7])
-      : "memory");
-}
 // Epilogue of the persistent 256x256 kernels (gemm4p / gemm4q): bias / GELU / GELU' / aux product /
 // beta C from the AGPR accumulators straight to global memory in the widened 16-B store layout.
 // biasv: the lane's bias quads (HAS_BIAS); mrow = m0 + wm 128 + (lane & 15).
-// NJ: 16-column blocks per wave (8: 128 x 128 wave tiles; 4: gemm4q's 8-wave 128 x 64 tiles)
-template <int EPI, bool ACC, int NJ = 8>
-DEV void p_store_tile(const BigArgs& g, f32x4 (&acc)[8][NJ], const f32x4 (&biasv)[NJ], int mrow, int n0, int wn,
+template <int EPI, bool ACC>
+DEV void p_store_tile(const BigArgs& g, f32x4 (&acc)[8][8], const f32x4 (&biasv)[8], int mrow, int n0, int wn,
                       int lane) {
   constexpr bool HAS_BIAS = EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_D;
   constexpr bool IN_EPI = (EPI == EPI_NONE && ACC) || EPI == EPI_MUL_AUX;
@@ -1114,20 +1086,18 @@ DEV void p_store_tile(const BigArgs& g, f32x4 (&acc)[8][NJ], const f32x4 (&biasv
   // odd those of block 2 jp + 1 (cdna_hip_programming.md T21, 16-lane form) -> one 16-B store each.
   // The swap is an involution: applied to an input tile read in that layout it restores the
   // accumulator layout.
-  constexpr int NP = NJ / 2;                 // 16-B store chunks per row and lane (column-block pairs)
-  const int nst = n0 + wn * 16 * NJ + 16 * g_odd(lane) + 8 * (lane >> 5);     // + 32 jp
+  const int nst = n0 + wn * 128 + 16 * g_odd(lane) + 8 * (lane >> 5);     // + 32 jp
   constexpr bool in_tile = IN_EPI;
   // the input tile (aux, or C for beta) whole, one wait before the first store: streaming it two rows
   // ahead of the stores measured the same (profiles/r4y2_epilogue_pipe_ab.log)
-  uint4 cin[8][NP];
+  uint4 cin[8][4];
   if (IN_EPI && in_tile) {
     const bf16* src = EPI == EPI_MUL_AUX ? g.aux : (const bf16*)g.C;
     const long ld = EPI == EPI_MUL_AUX ? g.ldaux : g.ldc;
     const bf16* rows[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) rows[i] = src + (long)(mrow + 16 * i) * ld + nst;
-    if constexpr (NP == 4) load_tile16(cin, rows);
-    else load_tile8(cin, rows);
+    load_tile16(cin, rows);
   }
 
   bf16* Cb = (bf16*)g.C;
@@ -1145,7 +1115,7 @@ DEV void p_store_tile(const BigArgs& g, f32x4 (&acc)[8][NJ], const f32x4 (&biasv
   for (int i = 0; i < 8; ++i) {
     const long m = mrow + 16 * i;
 #pragma unroll
-    for (int jp = 0; jp < NP; ++jp) {
+    for (int jp = 0; jp < 4; ++jp) {
       bf16x4 o[2], o2[2], ci[2];
       if (IN_EPI && in_tile) {     // input chunk back to the accumulator layout (blocks 2 jp, 2 jp + 1)
         const uint4 c4 = cin[i][jp];
@@ -1456,12 +1426,11 @@ __global__ void __launch_bounds__(NT4, 1) gemm4p_kernel(BigArgs g) {
 //   * the ring holds K-tile PAIRS (64 deep) in operand images of 32 KB: [256 rows][64 k] per
 //     K-contiguous operand (16-B chunk c of row r stored at c ^ (r & 7): conflict-free ds_read_b128),
 //     [64 k][256 cols] per k-major operand (gemm4p's swz_k image, two K-tiles stacked);
-//   * five operand slots, A of pair u in slot 2u mod 5 and B in 2u + 1 mod 5; pair t + 2's A is staged
-//     during pair t's even K-tile (into pair t - 1's B slot), its B during the odd one (into pair t's A
-//     slot, free since the barrier that ended the even K-tile): 32 KB per K-tile, one part per 8-MFMA
-//     group.  The first form (round 4, two 64-KB pair slots) staged all of pair t + 2 in pair t's odd
-//     K-tile: 64 KB there and none in the even one, above the 46 B/cycle the CU's DMA path moves in
-//     whole lines (the five slots: forward GEMMs 3-6 % faster, profiles/r4u_gemm4q_ring5_ab.log);
+//   * default (EEGF_Q_RING5): five operand slots, A of pair u in slot 2u mod 5 and B in 2u + 1 mod 5;
+//     pair t + 2's A is staged during pair t's even K-tile (into pair t - 1's B slot), its B during the
+//     odd one (into pair t's A slot, free since the barrier that ended the even K-tile): 32 KB per
+//     K-tile, one part per 8-MFMA group.  The first form (EEGF_Q_RING5=0, two 64-KB pair slots) staged
+//     all of pair t + 2 in pair t's odd K-tile: 64 KB there and none in the even one;
 //   * one vmcnt + one barrier per pair (end of the even K-tile), none at odd K-tiles;
 //   * the same MFMA K order as gemm4p (bitwise identical results), the same epilogue (p_store_tile) and
 //     cross-tile staging (the last two pairs stage the next tile's pairs 0 and 1).
@@ -1471,12 +1440,13 @@ constexpr int HSLOT = TM * BKP;                        // one operand of a pair 
 #ifndef EEGF_Q_NOP
 #define EEGF_Q_NOP 0
 #endif
-// EEGF_Q_RING5 0 selects the round-4 two-pair-slot ring (a probe; the default is the five-slot ring)
+// EEGF_Q_RING5 1 (default): the five-slot ring above; 64 KB per odd K-tile was above the 46 B/cycle the
+// CU's DMA path moves in whole lines (forward GEMMs 3-6 % faster, profiles/r4u_gemm4q_ring5_ab.log)
 #ifndef EEGF_Q_RING5
 #define EEGF_Q_RING5 1
 #endif
 #ifndef EEGF_Q_SPOS
-#define EEGF_Q_SPOS 4      // the 4-wave group's LDS-DMA part goes after its MFMA EEGF_Q_SPOS (0..7)
+#define EEGF_Q_SPOS 4      // R5: the group's LDS-DMA part goes after its MFMA EEGF_Q_SPOS (0..7)
 #endif
 // Persistent tile walk of gemm4q (eegf_tune key 15).  order 0 (default): round r of workgroup b takes
 // logical tile r * G + xcd_remap(b), so each round an XCD runs the next contiguous block of 32 tiles of
@@ -1763,252 +1733,6 @@ __global__ void __launch_bounds__(NT4, 1) gemm4q_kernel(BigArgs g) {
   }
 }
 
-// gemm8q: gemm4q with NW = 8 waves (the body also compiles for NW = 4, which is NOT what gemm4q runs:
-// hipcc spills that form's fragment offsets into the K-loop).  8: 2 x 4 waves of 128 x 64 (128 accumulator AGPRs + 128
-// VGPRs each), two waves per SIMD: the same K-loop, ring and MFMA K order (bitwise the same results),
-// but the epilogue's VALU runs at the SIMD's two-wave issue rate -- one wave issues a plain VALU
-// instruction every ~3.6 ns, two waves each at that rate (profiles/r5f_valu_issue.log), and the
-// bias / GELU / GELU' / aux-product epilogue is VALU-issue-bound (profiles/r5d_sink_ab.log).
-template <bool BKC, int EPI, bool ACC = false, int NW = 8>
-__global__ void __launch_bounds__(NW * 64, 1) gemm8q_kernel(BigArgs g) {
-  constexpr bool HAS_BIAS = EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_D;
-  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
-  constexpr int NJ = NW == 4 ? 8 : 4;                  // 16-column blocks per wave
-  constexpr int WN = 16 * NJ;                          // wave tile columns (rows: 128)
-  constexpr int PW = 32 / NW;                          // staging parts per operand, pair and wave
-  // the K-tile's staging parts: NW 4 one per 8-MFMA group (after MFMA EEGF_Q_SPOS), NW 8 one every
-  // other 4-MFMA group (after its MFMA 2)
-  constexpr int SPOS = NW == 4 ? EEGF_Q_SPOS : 2;
-  __shared__ __attribute__((aligned(16))) bf16 lds[5 * HSLOT];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = NW == 4 ? wave >> 1 : wave >> 2, wn = NW == 4 ? wave & 1 : wave & 3;
-  const int tiles_n = g.N / TN, tiles_m = g.M / TM, ntiles = tiles_m * tiles_n;
-  const int np = g.K / BKP;                            // pairs per tile (>= 2)
-  const QWalk walk = q_walk(g, ntiles);
-  int L = walk.L;
-  if (L >= walk.end) return;
-  if ((g.order & 32) && (blockIdx.x & 1)) {      // timing probe: desynchronise the odd workgroups
-    const long long t0 = __builtin_amdgcn_s_memrealtime();
-    while (__builtin_amdgcn_s_memrealtime() - t0 < g.ksplit) __builtin_amdgcn_s_sleep(2);
-  }
-
-  // Staging, 2 PW parts per pair and wave (PW A, PW B), each one wave-instruction of 1 KB; the
-  // workgroup's 32 parts per operand are numbered pr = PW wave + jj.
-  // K-contiguous part pr: rows 8 pr + lane / 8, 16-B chunk lane & 7 of the row's 128 B, read from
-  // source chunk (lane & 7) ^ (row & 7); row & 7 = lane / 8 for every part, so one per-lane offset serves
-  // all parts (a part's first row is a uniform offset of the SGPR base).
-  // k-major part pr: k-rows 2 pr + lane / 32 (512 B each), 16-B column chunk (lane & 31) ^ swz_k(k);
-  // swz_k reads k bits 0, 1, 3 = lane / 32, pr & 1, (pr >> 2) & 1: four per-lane offsets.
-  const int kr = lane >> 3;
-  const uint32_t voffA = (uint32_t)(((long)kr * g.lda + ((lane & 7) ^ kr) * 8) * 2);
-  uint32_t voffB[4];
-  if (BKC) {
-    voffB[0] = (uint32_t)(((long)kr * g.ldb + ((lane & 7) ^ kr) * 8) * 2);
-  } else {
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int k = ((v & 1) << 1) | ((v >> 1) << 3) | (lane >> 5);
-      voffB[v] = (uint32_t)(((long)(lane >> 5) * g.ldb + ((lane & 31) ^ swz_k(k)) * 8) * 2);
-    }
-  }
-  const long pstepB = BKC ? BKP : (long)BKP * g.ldb;
-  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr_of(lds));
-  // ps: the operand slot of the part (A parts j < PW, B parts j >= PW)
-  // NopC: wait states after the M0 write.  The K-loop's bases are SALU-computed (isa_lint: no
-  // VALU-written base within 5 states of any of its DMAs), so its DMAs need only the 1 state after the
-  // M0 write (EEGF_Q_NOP); the prologue's come right after tile_base's v_readfirstlane and keep 3, as
-  // gemm4p's do (once per tile: free), so they stay safe whatever the codegen puts in between
-  using QNOP = std::integral_constant<int, EEGF_Q_NOP>;
-  using PNOP = std::integral_constant<int, 3>;
-  auto stage_part = [&](const bf16* bA, const bf16* bB, int ps, int j, auto NopC) __attribute__((always_inline)) {
-    const int jj = j % PW, pr = wave * PW + jj;
-    constexpr int NOP = decltype(NopC)::value;
-    if (j < PW) {
-      glds16_asm_sa<NOP>(bA + (long)pr * 8 * g.lda, voffA, lds0 + 2u * (ps * HSLOT + pr * 8 * BKP));
-    } else if (BKC) {
-      glds16_asm_sa<NOP>(bB + (long)pr * 8 * g.ldb, voffB[0], lds0 + 2u * (ps * HSLOT + pr * 8 * BKP));
-    } else {
-      glds16_asm_sa<NOP>(bB + (long)pr * 2 * g.ldb, voffB[(pr & 1) | (((pr >> 2) & 1) << 1)],
-                         lds0 + 2u * (ps * HSLOT + pr * 2 * TN));
-    }
-  };
-  auto tile_base = [&](int l, const bf16*& bA, const bf16*& bB, int& m0, int& n0) {
-    int tm, tn;
-    tile_coords(g, l, tiles_m, tiles_n, tm, tn);
-    m0 = __builtin_amdgcn_readfirstlane(tm * TM);
-    n0 = __builtin_amdgcn_readfirstlane(tn * TN);
-    int am = m0, bn = n0;
-    if ((g.order & 3) == 2) {    // timing probe: operands from an L2-resident panel set (wrong results)
-      am = __builtin_amdgcn_readfirstlane((((tm & 3) + 4 * (blockIdx.x & 7)) % tiles_m) * TM);
-      bn = __builtin_amdgcn_readfirstlane((tn & 3) % tiles_n * TN);
-    }
-    bA = g.A + (long)am * g.lda;
-    bB = BKC ? g.B + (long)bn * g.ldb : g.B + bn;
-  };
-  // fragments.  K-contiguous [256][64] image: half h of a pair (K-tile 2t + h) is chunk 4 h + fq of rows
-  // r0 + fr (r0 % 16 == 0, so the swizzle is fr & 7); k-major: gemm4p's rd_col offsets, half 1 32 k-rows on
-  const int fr = lane & 15, fq = lane >> 4;
-  const int offA0 = (wm * 128 + fr) * BKP + ((fq ^ (fr & 7)) << 3);
-  const int offA1 = (wm * 128 + fr) * BKP + (((4 + fq) ^ (fr & 7)) << 3);
-  const int offB0 = (wn * WN + fr) * BKP + ((fq ^ (fr & 7)) << 3);
-  const int offB1 = (wn * WN + fr) * BKP + (((4 + fq) ^ (fr & 7)) << 3);
-  int tB0[NJ], tB1[NJ];
-  if (!BKC) {
-#pragma unroll
-    for (int i = 0; i < NJ; ++i) {
-      const int q = fr >> 2, p4 = fr & 3;
-      const int col = wn * WN + 16 * i + 4 * p4, ch = col >> 3, off = col & 7;
-      const int ka = 8 * fq + q, kb = ka + 4;
-      tB0[i] = ka * TN + (((ch ^ swz_k(ka)) << 3) | off);
-      tB1[i] = kb * TN + (((ch ^ swz_k(kb)) << 3) | off);
-    }
-  }
-  auto rdA = [&](const bf16* img, auto Hc, int i) {
-    return *(const bf16x8*)(img + (decltype(Hc)::value ? offA1 : offA0) + i * 16 * BKP);
-  };
-  auto rdB = [&](const bf16* img, auto Hc, int i) {
-    constexpr int h = decltype(Hc)::value;
-    return BKC ? *(const bf16x8*)(img + (h ? offB1 : offB0) + i * 16 * BKP)
-               : rd_col_off(img + h * 32 * TN, tB0[i], tB1[i]);
-  };
-  using C0 = std::integral_constant<int, 0>;
-  using C1 = std::integral_constant<int, 1>;
-
-  const bf16* baseA;
-  const bf16* baseB;
-  int m0, n0;
-  tile_base(L, baseA, baseB, m0, n0);
-#pragma unroll 1
-  for (int j = 0; j < 2 * PW; ++j) stage_part(baseA, baseB, j / PW, j, PNOP{});                      // pair 0
-#pragma unroll 1
-  for (int j = 0; j < 2 * PW; ++j) stage_part(baseA + BKP, baseB + pstepB, 2 + j / PW, j, PNOP{});    // pair 1
-  f32x4 acc[8][NJ];
-  int ps0 = 0;                  // operand slot of the tile's pair-0 A (0..4)
-  bool landed = false;          // the tile's pairs 0 and 1 retired (cross-staged and waited for)
-  for (;;) {
-    const int Ln = L + walk.step;
-    const bool more_tiles = Ln < walk.end;
-    int m0n = 0, n0n = 0;
-    const bf16* nA = nullptr;
-    const bf16* nB = nullptr;
-    if (more_tiles) tile_base(Ln, nA, nB, m0n, n0n);
-    if (!landed) {                                         // pair 0 (pair 1's 2 PW parts younger)
-      if constexpr (NW == 4) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    }
-    raw_barrier();
-    bf16x8 fa[2][8], fb[2][NJ];
-    // operand-slot arithmetic: slot + c mod 5 for 0 <= c <= 5 (uniform, on the SALU)
-    auto add5 = [](int x, int c) { const int y = x + c; return y >= 5 ? y - 5 : y; };
-    {
-      const bf16* img0 = lds + ps0 * HSLOT;
-      const bf16* imb0 = lds + add5(ps0, 1) * HSLOT;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) fa[0][i] = rdA(img0, C0{}, i);
-#pragma unroll
-      for (int i = 0; i < NJ; ++i) fb[0][i] = rdB(imb0, C0{}, i);
-    }
-    // K-tile s = 2 t + H of pair t: its fragments are in fa / fb[H]; the next K-tile's are read into
-    // [H ^ 1] (H = 0: the same slots' half 1; H = 1: pair t + 1's half 0).  Pair t + 2's A is staged
-    // during pair t's even K-tile (into pair t - 1's B slot), its B during the odd one (into pair t's A
-    // slot, free since the barrier that ended the even K-tile): 32 KB per K-tile.
-    // TAIL (the last two pairs): whether there is a next K-tile to read and what to stage are decided at
-    // run time; in the steady state (t + 2 < np) both are compile-time true, so the K-tile body carries no
-    // branch and hipcc's waitcnt pass sees straight-line LDS reads
-    // hA: operand slot of pair t's A
-    auto ktile = [&](auto Hc, int t, int hA, auto Ic, auto Tc) __attribute__((always_inline)) {
-      constexpr int H = decltype(Hc)::value;
-      constexpr bool INIT = decltype(Ic)::value, TAIL = decltype(Tc)::value;
-      const bool more = !TAIL || H == 0 || t + 1 < np;
-      // next K-tile's images: operand slots of pair t (H = 0) or t + 1 (H = 1)
-      const bf16* nimg = lds + add5(hA, 2 * H) * HSLOT;
-      const bf16* nimb = lds + add5(hA, 2 * H + 1) * HSLOT;
-      const bool own = !TAIL || t + 2 < np;
-      const bool st = (own || more_tiles) && !(g.order & 8);
-      const int sslot = H == 0 ? add5(hA, 4) : hA;
-      const bf16* sA = own ? baseA + (t + 2) * BKP : nA + (t + 2 - np) * BKP;
-      const bf16* sB = own ? baseB + (t + 2) * pstepB : nB + (t + 2 - np) * pstepB;
-      auto mma = [&](int s8, int jj) {
-        if (INIT) mma16_acc0(acc[s8][jj], fb[H][jj], fa[H][s8]);
-        else mma16_acc(acc[s8][jj], fb[H][jj], fa[H][s8]);
-      };
-      using HN = std::integral_constant<int, H ^ 1>;
-#pragma unroll
-      for (int s8 = 0; s8 < 8; ++s8) {
-#pragma unroll
-        for (int jj = 0; jj < NJ; ++jj) {
-          mma(s8, jj);
-          if (jj == 0 && more) fa[H ^ 1][s8] = rdA(nimg, HN{}, s8);
-          if (jj == 1 && more && s8 < NJ) fb[H ^ 1][s8] = rdB(nimb, HN{}, s8);
-          if (jj == SPOS && st && (NW == 4 || (s8 & 1) == 0))
-            stage_part(sA, sB, sslot, PW * H + (NW == 4 ? s8 : s8 >> 1), QNOP{});
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-      if (H == 0) {
-        // pair t + 1 (staged during pair t - 1) must have landed before the next K-tile reads its
-        // fragments; the barrier also frees pair t's slots for pair t + 2 (except this K-tile's PW A
-        // parts of pair t + 2, the younger ones)
-        if (!TAIL || t + 1 < np) {
-          if (st) {
-            if constexpr (NW == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-          } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        raw_barrier();
-      }
-    };
-    using F = std::false_type;
-    using T = std::true_type;
-    int hA = ps0;
-    if (np > 2) {
-      ktile(C0{}, 0, hA, T{}, F{});
-      ktile(C1{}, 0, hA, F{}, F{});
-    } else {
-      ktile(C0{}, 0, hA, T{}, T{});
-      ktile(C1{}, 0, hA, F{}, T{});
-    }
-    hA = add5(hA, 2);
-#pragma unroll 1
-    for (int t = 1; t + 2 < np; ++t) {
-      ktile(C0{}, t, hA, F{}, F{});
-      ktile(C1{}, t, hA, F{}, F{});
-      hA = add5(hA, 2);
-    }
-#pragma unroll 1
-    for (int t = max(1, np - 2); t < np; ++t) {
-      ktile(C0{}, t, hA, F{}, T{});
-      ktile(C1{}, t, hA, F{}, T{});
-      hA = add5(hA, 2);
-    }
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-    const int mrow = m0 + wm * 128 + (lane & 15);
-    const int ncol = n0 + wn * WN + 4 * (lane >> 4);
-    f32x4 biasv[NJ];
-    if (HAS_BIAS) {
-      if constexpr (NJ == 8) load_bias8(biasv, g.bias + ncol);
-      else load_bias4(biasv, g.bias + ncol);
-    }
-    // the next tile's pairs 0 and 1 (cross-staged) retired before the first store
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    if (!(g.order & 4) && !((g.order & 16) && (blockIdx.x & 1)))
-      p_store_tile<EPI, ACC, NJ>(g, acc, biasv, mrow, n0, wn, lane);
-    if (!more_tiles) break;
-    L = Ln;
-    m0 = m0n;
-    n0 = n0n;
-    baseA = nA;
-    baseB = nB;
-    landed = true;
-    ps0 = hA;
-  }
-}
-
 // ---------------------------------------------------------------------------------------------
 // 4-wave 256x128 kernel for the K = 768 bf16-output GEMMs with heavy epilogues (QKV and FFN1
 // forward with bias / GELU / GELU', the out-projection, the input gradients with an activation
@@ -2197,8 +1921,6 @@ int cu_count() {
   return cus;
 }
 int g_cu_reserve = 0;      // eegf_tune key 13
-// key 17: gemm4q's waves per workgroup: 4 (one 128 x 128 wave tile per SIMD) or 8 (two 128 x 64 per SIMD)
-int g_gemm4q_nw = [] { const char* e = getenv("EEGF_GEMM4Q_NW"); return e ? atoi(e) : 4; }();
 int g_tile_order = [] { const char* e = getenv("EEGF_TILE_ORDER"); return e ? atoi(e) : 0; }();   // key 15
 int g_probe_delay = [] { const char* e = getenv("EEGF_PROBE_DELAY"); return e ? atoi(e) : 0; }();   // key 16: the key-15 + 32 probe's start delay, s_memrealtime ticks (100 MHz)
 }  // namespace
@@ -2234,14 +1956,11 @@ int launch_big(const BigArgs& a, int splits, hipStream_t s) {
       // five-slot one (the K-contiguous dY in whole lines; profiles/r4ze_dgrad_gemm4q_ab.log).
       // key 14 = 1: forward layout only, 0: gemm4p everywhere
       const bool q = g_gemm4q >= 1 && (BKC || g_gemm4q == 2) && a.K % BKP == 0 && a.K >= 2 * BKP;
-      const bool w8 = q && g_gemm4q_nw == 8;
       if constexpr (EPI == EPI_NONE) {
-        if (acc && q && !w8) hipLaunchKernelGGL((gemm4q_kernel<BKC, EPI, true>), grid, dim3(NT4), 0, s, ap);
-        if (acc && w8) hipLaunchKernelGGL((gemm8q_kernel<BKC, EPI, true>), grid, dim3(512), 0, s, ap);
+        if (acc && q) hipLaunchKernelGGL((gemm4q_kernel<BKC, EPI, true>), grid, dim3(NT4), 0, s, ap);
         if (acc && !q) hipLaunchKernelGGL((gemm4p_kernel<BKC, EPI, true>), grid, dim3(NT4), 0, s, ap);
       }
-      if (!acc && q && !w8) hipLaunchKernelGGL((gemm4q_kernel<BKC, EPI>), grid, dim3(NT4), 0, s, ap);
-      if (!acc && w8) hipLaunchKernelGGL((gemm8q_kernel<BKC, EPI>), grid, dim3(512), 0, s, ap);
+      if (!acc && q) hipLaunchKernelGGL((gemm4q_kernel<BKC, EPI>), grid, dim3(NT4), 0, s, ap);
       if (!acc && !q) hipLaunchKernelGGL((gemm4p_kernel<BKC, EPI>), grid, dim3(NT4), 0, s, ap);
       return (int)hipGetLastError();
     }
@@ -2480,7 +2199,6 @@ extern "C" int eegf_tune(int key, int value) {
   if (key == 14) { const int o = g_gemm4q; if (value < 0 || value > 2) return EEGF_ERR_ARG; g_gemm4q = value; return o; }
   if (key == 13) { const int o = g_cu_reserve; if (value < 0 || value >= cu_count()) return EEGF_ERR_ARG; g_cu_reserve = value; return o; }
   if (key == 15) { const int o = g_tile_order; if (value < 0 || value > 63 || (value & 3) == 3) return EEGF_ERR_ARG; g_tile_order = value; return o; }
-  if (key == 17) { const int o = g_gemm4q_nw; if (value != 4 && value != 8) return EEGF_ERR_ARG; g_gemm4q_nw = value; return o; }
   if (key == 16) { const int o = g_probe_delay; g_probe_delay = value; return o; }
   if (key == 6) { const int o = g_ln_rpw; if (value < 1 || value > 64) return EEGF_ERR_ARG; g_ln_rpw = value; return o; }
   return EEGF_ERR_ARG;
