@@ -1734,6 +1734,213 @@ __global__ void __launch_bounds__(NT4, 1) gemm4q_kernel(BigArgs g) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// gemm4r: gemm4q with ROLLING A fragments.  Each A fragment is used by one 8-MFMA group, so it is read
+// two groups ahead (across the K-tile boundary too) into four register sets instead of a whole K-tile
+// ahead into sixteen: 48 fewer VGPRs in the K-loop.  The price is the ring: pair t's A image is read
+// until the end of its odd K-tile, so it cannot take pair t + 2's B there as gemm4q's ring does.
+// Instead A images rotate through three slots and B images through two (A of global pair u in slot
+// 2 (u mod 3), B in 1 + 2 (u mod 2)): pair t + 2's A is staged during pair t's even K-tile into pair
+// t - 1's A slot (free since the barrier that ends pair t - 1's odd K-tile -- a second barrier per
+// pair), its B during the odd K-tile into pair t's B slot (read during pair t - 1's odd and pair t's
+// even K-tile, free since the barrier that ends the even one): still 32 KB per K-tile.  The same MFMA K
+// order and epilogue as gemm4q / gemm4p (bitwise the same results).  eegf_tune key 18.
+template <bool BKC, int EPI, bool ACC = false>
+__global__ void __launch_bounds__(NT4, 1) gemm4r_kernel(BigArgs g) {
+  constexpr bool HAS_BIAS = EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_D;
+  __shared__ __attribute__((aligned(16))) bf16 lds[5 * HSLOT];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int tiles_n = g.N / TN, tiles_m = g.M / TM, ntiles = tiles_m * tiles_n;
+  const int np = g.K / BKP;
+  const QWalk walk = q_walk(g, ntiles);
+  int L = walk.L;
+  if (L >= walk.end) return;
+
+  const int kr = lane >> 3;
+  const uint32_t voffA = (uint32_t)(((long)kr * g.lda + ((lane & 7) ^ kr) * 8) * 2);
+  uint32_t voffB[4];
+  if (BKC) {
+    voffB[0] = (uint32_t)(((long)kr * g.ldb + ((lane & 7) ^ kr) * 8) * 2);
+  } else {
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int j = (v & 1) | ((v >> 1) << 2);
+      const int k = (wave * 8 + j) * 2 + (lane >> 5);
+      voffB[v] = (uint32_t)(((long)(lane >> 5) * g.ldb + ((lane & 31) ^ swz_k(k)) * 8) * 2);
+    }
+  }
+  const long pstepB = BKC ? BKP : (long)BKP * g.ldb;
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr_of(lds));
+  using QNOP = std::integral_constant<int, EEGF_Q_NOP>;
+  using PNOP = std::integral_constant<int, 3>;
+  // part j < 8: an A part into slot ps; j >= 8: a B part (gemm4q's mapping)
+  auto stage_part = [&](const bf16* bA, const bf16* bB, int ps, int j, auto NopC) __attribute__((always_inline)) {
+    const int jj = j & 7, pr = wave * 8 + jj;
+    constexpr int NOP = decltype(NopC)::value;
+    if (j < 8) {
+      glds16_asm_sa<NOP>(bA + (long)pr * 8 * g.lda, voffA, lds0 + 2u * (ps * HSLOT + pr * 8 * BKP));
+    } else if (BKC) {
+      glds16_asm_sa<NOP>(bB + (long)pr * 8 * g.ldb, voffB[0], lds0 + 2u * (ps * HSLOT + pr * 8 * BKP));
+    } else {
+      glds16_asm_sa<NOP>(bB + (long)pr * 2 * g.ldb, voffB[(jj & 1) | ((jj >> 2) << 1)], lds0 + 2u * (ps * HSLOT + pr * 2 * TN));
+    }
+  };
+  auto tile_base = [&](int l, const bf16*& bA, const bf16*& bB, int& m0, int& n0) {
+    int tm, tn;
+    tile_coords(g, l, tiles_m, tiles_n, tm, tn);
+    m0 = __builtin_amdgcn_readfirstlane(tm * TM);
+    n0 = __builtin_amdgcn_readfirstlane(tn * TN);
+    bA = g.A + (long)m0 * g.lda;
+    bB = BKC ? g.B + (long)n0 * g.ldb : g.B + n0;
+  };
+  const int fr = lane & 15, fq = lane >> 4;
+  const int offA0 = (wm * 128 + fr) * BKP + ((fq ^ (fr & 7)) << 3);
+  const int offA1 = (wm * 128 + fr) * BKP + (((4 + fq) ^ (fr & 7)) << 3);
+  const int offB0 = (wn * 128 + fr) * BKP + ((fq ^ (fr & 7)) << 3);
+  const int offB1 = (wn * 128 + fr) * BKP + (((4 + fq) ^ (fr & 7)) << 3);
+  int tB0[8], tB1[8];
+  if (!BKC) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int q = fr >> 2, p4 = fr & 3;
+      const int col = wn * 128 + 16 * i + 4 * p4, ch = col >> 3, off = col & 7;
+      const int ka = 8 * fq + q, kb = ka + 4;
+      tB0[i] = ka * TN + (((ch ^ swz_k(ka)) << 3) | off);
+      tB1[i] = kb * TN + (((ch ^ swz_k(kb)) << 3) | off);
+    }
+  }
+  auto rdA = [&](const bf16* img, auto Hc, int i) {
+    return *(const bf16x8*)(img + (decltype(Hc)::value ? offA1 : offA0) + i * 16 * BKP);
+  };
+  auto rdB = [&](const bf16* img, auto Hc, int i) {
+    constexpr int h = decltype(Hc)::value;
+    return BKC ? *(const bf16x8*)(img + (h ? offB1 : offB0) + i * 16 * BKP)
+               : rd_col_off(img + h * 32 * TN, tB0[i], tB1[i]);
+  };
+  using C0 = std::integral_constant<int, 0>;
+  using C1 = std::integral_constant<int, 1>;
+  auto anext = [](int a) { return a >= 4 ? a - 4 : a + 2; };      // A slot of the next pair: 0 -> 2 -> 4 -> 0
+
+  const bf16* baseA;
+  const bf16* baseB;
+  int m0, n0;
+  tile_base(L, baseA, baseB, m0, n0);
+#pragma unroll 1
+  for (int j = 0; j < 16; ++j) stage_part(baseA, baseB, j < 8 ? 0 : 1, j, PNOP{});                    // pair 0
+#pragma unroll 1
+  for (int j = 0; j < 16; ++j) stage_part(baseA + BKP, baseB + pstepB, j < 8 ? 2 : 3, j, PNOP{});    // pair 1
+  f32x4 acc[8][8];
+  int aS0 = 0, bS0 = 1;         // slots of the tile's pair-0 A and B
+  bool landed = false;
+  for (;;) {
+    const int Ln = L + walk.step;
+    const bool more_tiles = Ln < walk.end;
+    int m0n = 0, n0n = 0;
+    const bf16* nA = nullptr;
+    const bf16* nB = nullptr;
+    if (more_tiles) tile_base(Ln, nA, nB, m0n, n0n);
+    if (!landed) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");      // pair 0 (pair 1 younger)
+    raw_barrier();
+    bf16x8 fa[4], fb[2][8];
+    {
+      const bf16* img0 = lds + aS0 * HSLOT;
+      const bf16* imb0 = lds + bS0 * HSLOT;
+      fa[0] = rdA(img0, C0{}, 0);
+      fa[1] = rdA(img0, C0{}, 1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) fb[0][i] = rdB(imb0, C0{}, i);
+    }
+    auto ktile = [&](auto Hc, int t, int aS, int bS, auto Ic, auto Tc) __attribute__((always_inline)) {
+      constexpr int H = decltype(Hc)::value;
+      constexpr bool INIT = decltype(Ic)::value, TAIL = decltype(Tc)::value;
+      const bool more = !TAIL || H == 0 || t + 1 < np;
+      const bf16* cimg = lds + aS * HSLOT;                                // this K-tile's A (half H)
+      const bf16* nimg = H == 0 ? cimg : lds + anext(aS) * HSLOT;         // the next K-tile's A
+      const bf16* nimb = lds + (H == 0 ? bS : (bS ^ 2)) * HSLOT;           // the next K-tile's B
+      const bool own = !TAIL || t + 2 < np;
+      const bool st = own || more_tiles;
+      const int sslot = H == 0 ? anext(anext(aS)) : bS;                   // pair t + 2's A / B slot
+      const bf16* sA = own ? baseA + (t + 2) * BKP : nA + (t + 2 - np) * BKP;
+      const bf16* sB = own ? baseB + (t + 2) * pstepB : nB + (t + 2 - np) * pstepB;
+      using HN = std::integral_constant<int, H ^ 1>;
+#pragma unroll
+      for (int s8 = 0; s8 < 8; ++s8) {
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+          if (INIT) mma16_acc0(acc[s8][jj], fb[H][jj], fa[s8 & 3]);
+          else mma16_acc(acc[s8][jj], fb[H][jj], fa[s8 & 3]);
+          if (jj == 0) {
+            if (s8 + 2 < 8) fa[(s8 + 2) & 3] = rdA(cimg, Hc, s8 + 2);
+            else if (more) fa[(s8 + 2) & 3] = rdA(nimg, HN{}, s8 - 6);
+          }
+          if (jj == 1 && more) fb[H ^ 1][s8] = rdB(nimb, HN{}, s8);
+          if (jj == EEGF_Q_SPOS && st) stage_part(sA, sB, sslot, 8 * H + s8, QNOP{});
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      if (H == 0) {
+        // pair t + 1 (staged during pair t - 1) must have landed before the next K-tile reads its B; the
+        // barrier frees pair t's B slot for pair t + 2's B (this K-tile's 8 A parts are the younger ones)
+        if (!TAIL || t + 1 < np) {
+          if (st) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        raw_barrier();
+      } else if (!TAIL || t + 1 < np) {
+        // every wave is past its last read of pair t's A (consumed by this K-tile's MFMAs): pair t + 3's A
+        // may land in its slot from the next even K-tile on
+        raw_barrier();
+      }
+    };
+    using F = std::false_type;
+    using T = std::true_type;
+    int aS = aS0, bS = bS0;
+    if (np > 2) {
+      ktile(C0{}, 0, aS, bS, T{}, F{});
+      ktile(C1{}, 0, aS, bS, F{}, F{});
+    } else {
+      ktile(C0{}, 0, aS, bS, T{}, T{});
+      ktile(C1{}, 0, aS, bS, F{}, T{});
+    }
+    aS = anext(aS);
+    bS ^= 2;
+#pragma unroll 1
+    for (int t = 1; t + 2 < np; ++t) {
+      ktile(C0{}, t, aS, bS, F{}, F{});
+      ktile(C1{}, t, aS, bS, F{}, F{});
+      aS = anext(aS);
+      bS ^= 2;
+    }
+#pragma unroll 1
+    for (int t = max(1, np - 2); t < np; ++t) {
+      ktile(C0{}, t, aS, bS, F{}, T{});
+      ktile(C1{}, t, aS, bS, F{}, T{});
+      aS = anext(aS);
+      bS ^= 2;
+    }
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+    const int mrow = m0 + wm * 128 + (lane & 15);
+    const int ncol = n0 + wn * 128 + 4 * (lane >> 4);
+    f32x4 biasv[8];
+    if (HAS_BIAS) load_bias8(biasv, g.bias + ncol);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    p_store_tile<EPI, ACC>(g, acc, biasv, mrow, n0, wn, lane);
+    if (!more_tiles) break;
+    L = Ln;
+    m0 = m0n;
+    n0 = n0n;
+    baseA = nA;
+    baseB = nB;
+    landed = true;
+    aS0 = aS;
+    bS0 = bS;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // 4-wave 256x128 kernel for the K = 768 bf16-output GEMMs with heavy epilogues (QKV and FFN1
 // forward with bias / GELU / GELU', the out-projection, the input gradients with an activation
 // product): the same K-loop as gemm4w (asm LDS-DMA in the saddr form, next K-tile's fragments read
@@ -1921,6 +2128,8 @@ int cu_count() {
   return cus;
 }
 int g_cu_reserve = 0;      // eegf_tune key 13
+// key 18: the persistent GEMMs that take gemm4q on gemm4r (rolling A fragments) instead: 0 off, 1 on
+int g_gemm4r = [] { const char* e = getenv("EEGF_GEMM4R"); return e ? atoi(e) : 1; }();
 int g_tile_order = [] { const char* e = getenv("EEGF_TILE_ORDER"); return e ? atoi(e) : 0; }();   // key 15
 int g_probe_delay = [] { const char* e = getenv("EEGF_PROBE_DELAY"); return e ? atoi(e) : 0; }();   // key 16: the key-15 + 32 probe's start delay, s_memrealtime ticks (100 MHz)
 }  // namespace
@@ -1956,11 +2165,14 @@ int launch_big(const BigArgs& a, int splits, hipStream_t s) {
       // five-slot one (the K-contiguous dY in whole lines; profiles/r4ze_dgrad_gemm4q_ab.log).
       // key 14 = 1: forward layout only, 0: gemm4p everywhere
       const bool q = g_gemm4q >= 1 && (BKC || g_gemm4q == 2) && a.K % BKP == 0 && a.K >= 2 * BKP;
+      const bool r = q && g_gemm4r;
       if constexpr (EPI == EPI_NONE) {
-        if (acc && q) hipLaunchKernelGGL((gemm4q_kernel<BKC, EPI, true>), grid, dim3(NT4), 0, s, ap);
+        if (acc && r) hipLaunchKernelGGL((gemm4r_kernel<BKC, EPI, true>), grid, dim3(NT4), 0, s, ap);
+        if (acc && q && !r) hipLaunchKernelGGL((gemm4q_kernel<BKC, EPI, true>), grid, dim3(NT4), 0, s, ap);
         if (acc && !q) hipLaunchKernelGGL((gemm4p_kernel<BKC, EPI, true>), grid, dim3(NT4), 0, s, ap);
       }
-      if (!acc && q) hipLaunchKernelGGL((gemm4q_kernel<BKC, EPI>), grid, dim3(NT4), 0, s, ap);
+      if (!acc && r) hipLaunchKernelGGL((gemm4r_kernel<BKC, EPI>), grid, dim3(NT4), 0, s, ap);
+      if (!acc && q && !r) hipLaunchKernelGGL((gemm4q_kernel<BKC, EPI>), grid, dim3(NT4), 0, s, ap);
       if (!acc && !q) hipLaunchKernelGGL((gemm4p_kernel<BKC, EPI>), grid, dim3(NT4), 0, s, ap);
       return (int)hipGetLastError();
     }
@@ -2199,6 +2411,7 @@ extern "C" int eegf_tune(int key, int value) {
   if (key == 14) { const int o = g_gemm4q; if (value < 0 || value > 2) return EEGF_ERR_ARG; g_gemm4q = value; return o; }
   if (key == 13) { const int o = g_cu_reserve; if (value < 0 || value >= cu_count()) return EEGF_ERR_ARG; g_cu_reserve = value; return o; }
   if (key == 15) { const int o = g_tile_order; if (value < 0 || value > 63 || (value & 3) == 3) return EEGF_ERR_ARG; g_tile_order = value; return o; }
+  if (key == 18) { const int o = g_gemm4r; if (value < 0 || value > 1) return EEGF_ERR_ARG; g_gemm4r = value; return o; }
   if (key == 16) { const int o = g_probe_delay; g_probe_delay = value; return o; }
   if (key == 6) { const int o = g_ln_rpw; if (value < 1 || value > 64) return EEGF_ERR_ARG; g_ln_rpw = value; return o; }
   return EEGF_ERR_ARG;

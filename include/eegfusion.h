@@ -98,7 +98,9 @@ int eegf_tune(int key, int value);
  *          (timing only, wrong results): + 4 no epilogue stores, + 8 no staging after the prologue,
  *          + 16 stores from even workgroups only, + 32 odd workgroups start key-16 ticks (100 MHz)
  *          late; env EEGF_TILE_ORDER.
- *   key 16: the start delay of the key-15 + 32 probe. */
+ *   key 16: the start delay of the key-15 + 32 probe.
+ *   key 18: the gemm4q-eligible GEMMs on gemm4r (rolling A fragments, A / B images in 3 + 2 ring slots,
+ *          bitwise the same results): 1 (default) on, 0 gemm4q; env EEGF_GEMM4R. */
 /* Diagnostics (no reference counterpart): every following 256-row GEMM launch of the 8-wave / 4-wave
  * kernels writes 4 s_memrealtime stamps per workgroup (start, prologue done, K-loop done, epilogue
  * issued, slot 4 the CU id) into buf = int64 [grid.y][grid.x][8]; nullptr switches it off.  tools/gemm_phases.py. */
