@@ -63,7 +63,7 @@ KERNEL_GROUPS = {
 # (profiles/PMC_FILE key).  Algorithmic bytes per launch: A + W + C (+ aux) of each shape, bf16.
 R_TOK = 256 * L
 KERNEL_SYMBOLS = {
-    "gemm4q_kernel<true, 1, false>": {
+    "gemm4r_kernel<true, 1, false>": {
         "tags": ("qkv_fwd", "ao_fwd", "ffn2_fwd"), "pmc": "fwd_bias_qkv_ao_ffn2",
         "what": "persistent 256x256 bf16 GEMM, bias epilogue: the QKV, attention-output and FFN2 forwards",
         "bytes": {"qkv_fwd": 2 * (R_TOK * 768 + 2304 * 768 + R_TOK * 2304),
@@ -72,16 +72,16 @@ KERNEL_SYMBOLS = {
     "gemm4w_kernel<false, false, 0, float, true> + splitk_rowsum_reduce": {
         "tags": ("wgrad",), "pmc": "wgrad",
         "what": "split-K weight-gradient GEMM with the bias row sums, and its fixed-order slab reduction"},
-    "gemm4q_kernel<false, 0, true>": {
+    "gemm4r_kernel<false, 0, true>": {
         "tags": ("dgrad_qkv", "dgrad_ffn1"), "pmc": "dgrad_qkv_ffn1",
         "what": "persistent GEMM, input gradients accumulating onto the residual gradient (beta = 1)"},
-    "gemm4q_kernel<true, 8, false>": {"tags": ("ffn1_fwd_gd",), "pmc": "ffn1_fwd",
+    "gemm4r_kernel<true, 8, false>": {"tags": ("ffn1_fwd_gd",), "pmc": "ffn1_fwd",
                                       "what": "persistent GEMM, FFN1 + bias + GELU + GELU' (pass 2)"},
-    "gemm4q_kernel<true, 2, false>": {"tags": ("ffn1_fwd",), "pmc": "ffn1_fwd",
+    "gemm4r_kernel<true, 2, false>": {"tags": ("ffn1_fwd",), "pmc": "ffn1_fwd",
                                       "what": "persistent GEMM, FFN1 + bias + GELU (pass 1)"},
-    "gemm4q_kernel<false, 9, false>": {"tags": ("dgrad_ffn2",), "pmc": "dgrad_ffn2",
+    "gemm4r_kernel<false, 9, false>": {"tags": ("dgrad_ffn2",), "pmc": "dgrad_ffn2",
                                        "what": "persistent GEMM, FFN2 input gradient x GELU'"},
-    "gemm4q_kernel<false, 0, false>": {"tags": ("dgrad_out",), "pmc": "dgrad_out",
+    "gemm4r_kernel<false, 0, false>": {"tags": ("dgrad_out",), "pmc": "dgrad_out",
                                        "what": "persistent GEMM, attention-output input gradient"},
     "attn_bwd256_kernel<true>": {"tags": ("attn_bwd",), "pmc": "attn_bwd", "what": "L = 256 attention backward"},
     "attn_fwd256_kernel<true, false>": {"tags": ("attn_fwd",), "pmc": "attn_fwd", "what": "L = 256 attention forward"},

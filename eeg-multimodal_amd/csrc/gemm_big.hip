@@ -1072,21 +1072,33 @@ DEV void load_tile16(uint4 (&c)[8][4], const bf16* const (&p)[8]) {
       : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "v"(p[4]), "v"(p[5]), "v"(p[6]), "v"(p[7])
       : "memory");
 }
-// Epilogue of the persistent 256x256 kernels (gemm4p / gemm4q): bias / GELU / GELU' / aux product /
-// beta C from the AGPR accumulators straight to global memory in the widened 16-B store layout.
-// biasv: the lane's bias quads (HAS_BIAS); mrow = m0 + wm 128 + (lane & 15).
-template <int EPI, bool ACC>
-DEV void p_store_tile(const BigArgs& g, f32x4 (&acc)[8][8], const f32x4 (&biasv)[8], int mrow, int n0, int wn,
-                      int lane) {
+// Epilogue of the persistent 256x256 kernels (gemm4p / gemm4q / gemm4r): bias / GELU / GELU' / aux
+// product / beta C from the AGPR accumulators in the widened 16-B store layout, handed to sink(i, jp,
+// o, o2) per lane chunk (o: column blocks 2 jp, 2 jp + 1 of the output C, o2: those of the second
+// output aux of EPI_BIAS_GELU(_D)), to be paired by pack16 into one 16-B store.
+// biasv: the lane's bias quads (HAS_BIAS); mrow = m0 + wm 128 + (lane & 15); nst: p_nst().
+// Stores: the epilogue is store-ISSUE-bound (0.25 MB per CU per tile with GELU': ~240 of 490 us per
+// launch went to 8-B stores, profiles/r3q_exp.log), so column blocks j = 2 jp, 2 jp + 1 are paired:
+// one v_permlane16_swap per dword gives lanes g even 8 contiguous columns of block 2 jp and lanes g
+// odd those of block 2 jp + 1 (cdna_hip_programming.md T21, 16-lane form) -> one 16-B store each.
+// The swap is an involution: applied to an input tile read in that layout it restores the
+// accumulator layout.
+DEV int p_nst(int n0, int wn, int lane) { return n0 + wn * 128 + 16 * g_odd(lane) + 8 * (lane >> 5); }  // + 32 jp
+DEV u32x4 pack16(bf16x4 a, bf16x4 b) {
+  uint2 ua = __builtin_bit_cast(uint2, a), ub = __builtin_bit_cast(uint2, b);
+  const auto rx = __builtin_amdgcn_permlane16_swap(ua.x, ub.x, false, false);
+  const auto ry = __builtin_amdgcn_permlane16_swap(ua.y, ub.y, false, false);
+  return u32x4{rx[0], ry[0], rx[1], ry[1]};
+}
+// non-temporal stores (eegf_tune key 12): 3-4 % off the store-bound epilogues, profiles/r4a_pol.log
+DEV void st_out(bf16* pp, u32x4 d, int nt) {
+  if (nt) asm volatile("global_store_dwordx4 %0, %1, off nt" :: "v"(pp), "v"(d) : "memory");
+  else *(u32x4*)pp = d;
+}
+template <int EPI, bool ACC, class Sink>
+DEV void p_epi_tile(const BigArgs& g, f32x4 (&acc)[8][8], const f32x4 (&biasv)[8], int mrow, int nst, Sink&& sink) {
   constexpr bool HAS_BIAS = EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_D;
   constexpr bool IN_EPI = (EPI == EPI_NONE && ACC) || EPI == EPI_MUL_AUX;
-  // Stores: the epilogue is store-ISSUE-bound (0.25 MB per CU per tile with GELU': ~240 of 490 us per
-  // launch went to 8-B stores, profiles/r3q_exp.log), so column blocks j = 2 jp, 2 jp + 1 are paired:
-  // one v_permlane16_swap per dword gives lanes g even 8 contiguous columns of block 2 jp and lanes g
-  // odd those of block 2 jp + 1 (cdna_hip_programming.md T21, 16-lane form) -> one 16-B store each.
-  // The swap is an involution: applied to an input tile read in that layout it restores the
-  // accumulator layout.
-  const int nst = n0 + wn * 128 + 16 * g_odd(lane) + 8 * (lane >> 5);     // + 32 jp
   constexpr bool in_tile = IN_EPI;
   // the input tile (aux, or C for beta) whole, one wait before the first store: streaming it two rows
   // ahead of the stores measured the same (profiles/r4y2_epilogue_pipe_ab.log)
@@ -1099,21 +1111,8 @@ DEV void p_store_tile(const BigArgs& g, f32x4 (&acc)[8][8], const f32x4 (&biasv)
     for (int i = 0; i < 8; ++i) rows[i] = src + (long)(mrow + 16 * i) * ld + nst;
     load_tile16(cin, rows);
   }
-
-  bf16* Cb = (bf16*)g.C;
-  auto st16 = [&](bf16* base, long ld, long m, int jp, bf16x4 a, bf16x4 b) {
-    uint2 ua = __builtin_bit_cast(uint2, a), ub = __builtin_bit_cast(uint2, b);
-    const auto rx = __builtin_amdgcn_permlane16_swap(ua.x, ub.x, false, false);
-    const auto ry = __builtin_amdgcn_permlane16_swap(ua.y, ub.y, false, false);
-    const u32x4 d = {rx[0], ry[0], rx[1], ry[1]};
-    bf16* pp = base + m * ld + nst + 32 * jp;
-    // non-temporal stores (eegf_tune key 12): 3-4 % off the store-bound epilogues, profiles/r4a_pol.log
-    if (g.store_nt) asm volatile("global_store_dwordx4 %0, %1, off nt" :: "v"(pp), "v"(d) : "memory");
-    else *(u32x4*)pp = d;
-  };
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    const long m = mrow + 16 * i;
 #pragma unroll
     for (int jp = 0; jp < 4; ++jp) {
       bf16x4 o[2], o2[2], ci[2];
@@ -1150,11 +1149,21 @@ DEV void p_store_tile(const BigArgs& g, f32x4 (&acc)[8][8], const f32x4 (&biasv)
           o[h][0] = (bf16)v[0]; o[h][1] = (bf16)v[1]; o[h][2] = (bf16)v[2]; o[h][3] = (bf16)v[3];
         }
       }
-      if ((EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_D) && (EPI == EPI_BIAS_GELU_D || g.aux))
-        st16(g.aux, g.ldaux, m, jp, o2[0], o2[1]);
-      st16(Cb, g.ldc, m, jp, o[0], o[1]);
+      sink(i, jp, o, o2);
     }
   }
+}
+template <int EPI, bool ACC>
+DEV void p_store_tile(const BigArgs& g, f32x4 (&acc)[8][8], const f32x4 (&biasv)[8], int mrow, int n0, int wn,
+                      int lane) {
+  const int nst = p_nst(n0, wn, lane);
+  bf16* Cb = (bf16*)g.C;
+  p_epi_tile<EPI, ACC>(g, acc, biasv, mrow, nst, [&](int i, int jp, const bf16x4 (&o)[2], const bf16x4 (&o2)[2]) {
+    const long m = mrow + 16 * i;
+    if ((EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_D) && (EPI == EPI_BIAS_GELU_D || g.aux))
+      st_out(g.aux + m * g.ldaux + nst + 32 * jp, pack16(o2[0], o2[1]), g.store_nt);
+    st_out(Cb + m * g.ldc + nst + 32 * jp, pack16(o[0], o[1]), g.store_nt);
+  });
 }
 
 #ifndef EEGF_P_READS
@@ -2166,14 +2175,19 @@ int launch_big(const BigArgs& a, int splits, hipStream_t s) {
       // key 14 = 1: forward layout only, 0: gemm4p everywhere
       const bool q = g_gemm4q >= 1 && (BKC || g_gemm4q == 2) && a.K % BKP == 0 && a.K >= 2 * BKP;
       const bool r = q && g_gemm4r;
-      if constexpr (EPI == EPI_NONE) {
-        if (acc && r) hipLaunchKernelGGL((gemm4r_kernel<BKC, EPI, true>), grid, dim3(NT4), 0, s, ap);
-        if (acc && q && !r) hipLaunchKernelGGL((gemm4q_kernel<BKC, EPI, true>), grid, dim3(NT4), 0, s, ap);
-        if (acc && !q) hipLaunchKernelGGL((gemm4p_kernel<BKC, EPI, true>), grid, dim3(NT4), 0, s, ap);
+      if (acc) {
+        if constexpr (EPI == EPI_NONE) {
+          if (r) hipLaunchKernelGGL((gemm4r_kernel<BKC, EPI, true>), grid, dim3(NT4), 0, s, ap);
+          else if (q) hipLaunchKernelGGL((gemm4q_kernel<BKC, EPI, true>), grid, dim3(NT4), 0, s, ap);
+          else hipLaunchKernelGGL((gemm4p_kernel<BKC, EPI, true>), grid, dim3(NT4), 0, s, ap);
+        }
+      } else if (r) {
+        hipLaunchKernelGGL((gemm4r_kernel<BKC, EPI>), grid, dim3(NT4), 0, s, ap);
+      } else if (q) {
+        hipLaunchKernelGGL((gemm4q_kernel<BKC, EPI>), grid, dim3(NT4), 0, s, ap);
+      } else {
+        hipLaunchKernelGGL((gemm4p_kernel<BKC, EPI>), grid, dim3(NT4), 0, s, ap);
       }
-      if (!acc && r) hipLaunchKernelGGL((gemm4r_kernel<BKC, EPI>), grid, dim3(NT4), 0, s, ap);
-      if (!acc && q && !r) hipLaunchKernelGGL((gemm4q_kernel<BKC, EPI>), grid, dim3(NT4), 0, s, ap);
-      if (!acc && !q) hipLaunchKernelGGL((gemm4p_kernel<BKC, EPI>), grid, dim3(NT4), 0, s, ap);
       return (int)hipGetLastError();
     }
   }

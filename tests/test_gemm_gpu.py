@@ -644,3 +644,42 @@ def test_gemm_persistent_falls_back_on_ragged_shapes():
         finally:
             _tune(11, old)
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("M,N,K", P_SHAPES)
+@pytest.mark.parametrize("epi", ["bias", "none", "mul_aux", "none_beta", "bias_gelu_d"])
+def test_gemm_persistent_ring_variants(epi, M, N, K):
+    """eegf_tune key 18: gemm4q (0) and gemm4r (1, default: rolling A fragments in a 3 + 2 slot ring, two
+    barriers per K-tile pair) give the same bits on every persistent shape and epilogue (pair counts
+    np = K / 64 of 2..48; the cross-tile staging of both rings)."""
+    k = _k()
+    torch.manual_seed(29)
+    fwd = epi in ("bias", "bias_gelu_d")      # the others on the input-gradient layout (k-major B)
+    x = (torch.randn(M, K, device="cuda") * 0.3).to(torch.bfloat16)
+    wf = (torch.randn(N, K, device="cuda") * 0.3).to(torch.bfloat16)
+    wd = (torch.randn(K, N, device="cuda") * 0.1).to(torch.bfloat16)
+    b = torch.randn(N, device="cuda")
+    aux = torch.randn(M, N, device="cuda").to(torch.bfloat16) if epi == "mul_aux" else None
+    c0 = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+    outs = []
+    for key in (0, 1):
+        old = _tune(18, key)
+        try:
+            if epi == "none_beta":
+                out = c0.clone()
+                k.linear_dgrad(x, wd, out=out, beta=1.0)
+                out = (out,)
+            elif not fwd:
+                out = (k.linear_dgrad(x, wd, epi=epi, aux=aux),)
+            else:
+                a2 = torch.full((M, N), float("nan"), device="cuda", dtype=torch.bfloat16) \
+                    if epi == "bias_gelu_d" else None
+                out = (k.linear(x, wf, None if epi == "none" else b, epi=epi, aux=a2), a2)
+            torch.cuda.synchronize()
+            outs.append(out)
+        finally:
+            _tune(18, old)
+    for o in outs[1:]:
+        for a, r in zip(o, outs[0]):
+            if r is not None:
+                assert torch.equal(a, r)

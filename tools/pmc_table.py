@@ -37,18 +37,22 @@ GROUPS = {     # bf16 instantiations appear mangled in rocprofv3's CSV (DF16b), 
                  "gemm4p_kernel<true, 2, false>", "gemm4p_kernel<true, 8, false>",
                  "gemm4p_kernelILb1ELi2ELb0E", "gemm4p_kernelILb1ELi8ELb0E",
                  # round 4: the K-contiguous forwards run on gemm4q (K-tile pairs in whole lines)
-                 "gemm4q_kernel<true, 2, false>", "gemm4q_kernel<true, 8, false>"),
+                 "gemm4q_kernel<true, 2, false>", "gemm4q_kernel<true, 8, false>",
+                 # round 5: gemm4r (rolling A fragments) replaces gemm4q
+                 "gemm4r_kernel<true, 2, false>", "gemm4r_kernel<true, 8, false>"),
     "fwd_bias_qkv_ao_ffn2": ("gemm4p_kernel<true, 1, false>", "gemm4p_kernelILb1ELi1ELb0E",
-                             "gemm4q_kernel<true, 1, false>"),
+                             "gemm4q_kernel<true, 1, false>", "gemm4r_kernel<true, 1, false>"),
     "qkv_fwd": ("gemm8_kernelILb1ELb1ELi1EDF16bLb0E",),
     "ffn2_fwd": ("gemm4w_kernelILb1ELb1ELi1EDF16bLb0E",),
     "dgrad_qkv_ffn1": ("gemm4w_kernelILb1ELb0ELi0EDF16bLb0E", "gemm4p_kernel<false, 0, true>",
-                       "gemm4p_kernelILb0ELi0ELb1E", "gemm4q_kernel<false, 0, true>"),
+                       "gemm4p_kernelILb0ELi0ELb1E", "gemm4q_kernel<false, 0, true>",
+                       "gemm4r_kernel<false, 0, true>"),
     "ao_fwd": ("gemm4h_kernelILb1ELi1E", "gemm4h_kernel<true, 1>"),
     "dgrad_out": ("gemm4h_kernelILb0ELi0E", "gemm4h_kernel<false, 0>", "gemm4p_kernel<false, 0, false>",
-                  "gemm4p_kernelILb0ELi0ELb0E", "gemm4q_kernel<false, 0, false>"),
+                  "gemm4p_kernelILb0ELi0ELb0E", "gemm4q_kernel<false, 0, false>",
+                  "gemm4r_kernel<false, 0, false>"),
     "dgrad_ffn2": ("gemm8_kernelILb1ELb0ELi9EDF16bLb0E", "gemm4p_kernel<false, 9, false>", "gemm4p_kernelILb0ELi9ELb0E",
-                   "gemm4q_kernel<false, 9, false>"),
+                   "gemm4q_kernel<false, 9, false>", "gemm4r_kernel<false, 9, false>"),
     "wgrad": ("gemm4w_kernel<false, false, 0, float, true", "gemm4w_kernelILb0ELb0ELi0EfLb1E"),
     "attn_fwd": ("attn_fwd256_kernel",),
     "attn_bwd": ("attn_bwd256_kernel",),
