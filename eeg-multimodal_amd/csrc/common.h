@@ -253,6 +253,49 @@ DEV void gelu2(f32x2 x, f32x2& gl, f32x2* gd) {
   if (gd) *gd = x * e + h;                                                     // Phi(x) + x phi(x)
 }
 
+// gelu2 on N independent pairs, every step issued for all N before the next: the same operations
+// (bitwise the same results), but each dependent packed FMA finds N - 1 others between it and its
+// source, so the hazard recognizer needs no s_nop (one per dependent v_pk_* pair otherwise)
+template <int N>
+DEV void gelu2n(const f32x2 (&x)[N], f32x2 (&gl)[N], f32x2 (*gd)[N]) {
+  f32x2 e[N], t[N], poly[N];
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    const f32x2 x2 = x[n] * x[n];
+    const f32x2 ea = x2 * (-0.72134752044448170f) + (-1.3257480647361593f);
+    e[n].x = __builtin_amdgcn_exp2f(ea.x);
+    e[n].y = __builtin_amdgcn_exp2f(ea.y);
+  }
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    t[n].x = __builtin_amdgcn_rcpf(fmaf(fabsf(x[n].x), 0.23164188826636040f, 1.0f));
+    t[n].y = __builtin_amdgcn_rcpf(fmaf(fabsf(x[n].y), 0.23164188826636040f, 1.0f));
+  }
+#pragma unroll
+  for (int n = 0; n < N; ++n) poly[n] = t[n] * 1.3302744295891231f + (-1.8212559791077754f);
+#pragma unroll
+  for (int n = 0; n < N; ++n) poly[n] = poly[n] * t[n] + 1.7814779365698128f;
+#pragma unroll
+  for (int n = 0; n < N; ++n) poly[n] = poly[n] * t[n] + (-0.35656378124891560f);
+#pragma unroll
+  for (int n = 0; n < N; ++n) poly[n] = poly[n] * t[n] + 0.31938153025994087f;
+#pragma unroll
+  for (int n = 0; n < N; ++n) poly[n] = poly[n] * t[n];
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    const f32x2 qm = poly[n] * e[n] + (-0.5f);
+    f32x2 us;
+    us.x = copysignf(qm.x, x[n].x);
+    us.y = copysignf(qm.y, x[n].y);
+    poly[n] = us + 0.5f;                                                       // Phi(x)
+  }
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    gl[n] = x[n] * poly[n];
+    if (gd) (*gd)[n] = x[n] * e[n] + poly[n];
+  }
+}
+
 // gelu(x) and gelu'(x) together (one exp, one erf): the forward stores gelu' for the backward
 DEV void gelu_fg(float x, float& gl, float& gd) {
   const float e = __expf(-0.5f * x * x);

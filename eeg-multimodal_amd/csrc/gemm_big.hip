@@ -1123,46 +1123,61 @@ DEV void p_epi_tile(const BigArgs& g, f32x4 (&acc)[8][8], const f32x4 (&biasv)[8
         ci[0] = __builtin_bit_cast(bf16x4, make_uint2(rx[0], ry[0]));
         ci[1] = __builtin_bit_cast(bf16x4, make_uint2(rx[1], ry[1]));
       }
+      float v[2][4];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int j = 2 * jp + h;
-        float v[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          v[r] = g.alpha * acc[i][j][r] + (HAS_BIAS ? biasv[j][r] : 0.f);
+          v[h][r] = g.alpha * acc[i][j][r] + (HAS_BIAS ? biasv[j][r] : 0.f);
           if (IN_EPI && in_tile) {
-            if (EPI == EPI_MUL_AUX) v[r] *= (float)ci[h][r];
-            else v[r] += g.beta * (float)ci[h][r];
+            if (EPI == EPI_MUL_AUX) v[h][r] *= (float)ci[h][r];
+            else v[h][r] += g.beta * (float)ci[h][r];
           }
         }
-        if (EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_D) {
-          f32x2 gl0, gl1, gd0, gd1;
-          gelu2(f32x2{v[0], v[1]}, gl0, EPI == EPI_BIAS_GELU_D ? &gd0 : nullptr);
-          gelu2(f32x2{v[2], v[3]}, gl1, EPI == EPI_BIAS_GELU_D ? &gd1 : nullptr);
+      }
+      if (EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_D) {
+        // the chunk's 4 pairs through gelu2n together (independent chains interleaved)
+        const f32x2 x[4] = {f32x2{v[0][0], v[0][1]}, f32x2{v[0][2], v[0][3]}, f32x2{v[1][0], v[1][1]},
+                            f32x2{v[1][2], v[1][3]}};
+        f32x2 gl[4], gd[4];
+        gelu2n<4>(x, gl, EPI == EPI_BIAS_GELU_D ? &gd : nullptr);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
           if (EPI == EPI_BIAS_GELU_D) {
-            o2[h][0] = (bf16)gd0.x; o2[h][1] = (bf16)gd0.y; o2[h][2] = (bf16)gd1.x; o2[h][3] = (bf16)gd1.y;
+            o2[h][0] = (bf16)gd[2 * h].x; o2[h][1] = (bf16)gd[2 * h].y;
+            o2[h][2] = (bf16)gd[2 * h + 1].x; o2[h][3] = (bf16)gd[2 * h + 1].y;
           } else {     // pre-activation
-            o2[h][0] = (bf16)v[0]; o2[h][1] = (bf16)v[1]; o2[h][2] = (bf16)v[2]; o2[h][3] = (bf16)v[3];
+            o2[h][0] = (bf16)v[h][0]; o2[h][1] = (bf16)v[h][1]; o2[h][2] = (bf16)v[h][2]; o2[h][3] = (bf16)v[h][3];
           }
-          o[h][0] = (bf16)gl0.x; o[h][1] = (bf16)gl0.y; o[h][2] = (bf16)gl1.x; o[h][3] = (bf16)gl1.y;
-        } else {
-          o[h][0] = (bf16)v[0]; o[h][1] = (bf16)v[1]; o[h][2] = (bf16)v[2]; o[h][3] = (bf16)v[3];
+          o[h][0] = (bf16)gl[2 * h].x; o[h][1] = (bf16)gl[2 * h].y;
+          o[h][2] = (bf16)gl[2 * h + 1].x; o[h][3] = (bf16)gl[2 * h + 1].y;
+        }
+      } else {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          o[h][0] = (bf16)v[h][0]; o[h][1] = (bf16)v[h][1]; o[h][2] = (bf16)v[h][2]; o[h][3] = (bf16)v[h][3];
         }
       }
       sink(i, jp, o, o2);
     }
   }
 }
-template <int EPI, bool ACC>
+// NT: the runtime store policy (gemm4p / gemm4q, eegf_tune key 12).  gemm4r takes plain stores only
+// (NT = false): a runtime policy puts a scalar branch around each of the tile's 64 stores, and those
+// block boundaries keep the scheduler from interleaving the GELU chains of neighbouring chunks (an
+// s_nop between most dependent packed FMAs)
+template <int EPI, bool ACC, bool NT = true>
 DEV void p_store_tile(const BigArgs& g, f32x4 (&acc)[8][8], const f32x4 (&biasv)[8], int mrow, int n0, int wn,
                       int lane) {
   const int nst = p_nst(n0, wn, lane);
   bf16* Cb = (bf16*)g.C;
+  const int nt = NT ? g.store_nt : 0;
   p_epi_tile<EPI, ACC>(g, acc, biasv, mrow, nst, [&](int i, int jp, const bf16x4 (&o)[2], const bf16x4 (&o2)[2]) {
     const long m = mrow + 16 * i;
     if ((EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_D) && (EPI == EPI_BIAS_GELU_D || g.aux))
-      st_out(g.aux + m * g.ldaux + nst + 32 * jp, pack16(o2[0], o2[1]), g.store_nt);
-    st_out(Cb + m * g.ldc + nst + 32 * jp, pack16(o[0], o[1]), g.store_nt);
+      st_out(g.aux + m * g.ldaux + nst + 32 * jp, pack16(o2[0], o2[1]), nt);
+    st_out(Cb + m * g.ldc + nst + 32 * jp, pack16(o[0], o[1]), nt);
   });
 }
 
@@ -1936,7 +1951,7 @@ __global__ void __launch_bounds__(NT4, 1) gemm4r_kernel(BigArgs g) {
     if (HAS_BIAS) load_bias8(biasv, g.bias + ncol);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    p_store_tile<EPI, ACC>(g, acc, biasv, mrow, n0, wn, lane);
+    p_store_tile<EPI, ACC, false>(g, acc, biasv, mrow, n0, wn, lane);
     if (!more_tiles) break;
     L = Ln;
     m0 = m0n;

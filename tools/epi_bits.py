@@ -1,0 +1,53 @@
+"""Bit-identity of the production GEMM epilogues across two library builds: runs every epilogue form
+of the persistent K = 768 GEMMs (bias, GELU with the pre-activation, GELU + GELU', the input gradients
+x aux and with beta = 1) on fixed seeded inputs at a production shape and prints one sha256 per output.
+Run it once per build (EEGF_LIB=<other .so> for the second) and compare the lines: a schedule-only
+change of an epilogue must print the same digests.
+usage: python tools/epi_bits.py [rows]"""
+import hashlib
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "eeg-multimodal_amd"))
+import torch  # noqa: E402
+
+from eegfusion import kernels as K  # noqa: E402
+
+
+def digest(t):
+    return hashlib.sha256(t.contiguous().view(torch.uint8).cpu().numpy().tobytes()).hexdigest()[:16]
+
+
+def main():
+    M = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
+    dev, dt = "cuda", torch.bfloat16
+    g = torch.Generator(device=dev).manual_seed(1234)
+    rn = lambda *s: torch.randn(*s, device=dev, dtype=torch.float32, generator=g)
+    for N, Kd in ((3072, 768), (2304, 768), (768, 3072)):
+        A = (rn(M, Kd) * 2).to(dt)
+        B = (rn(N, Kd) * 0.05).to(dt)
+        bias = rn(N)
+        for epi in ("bias", "bias_gelu", "bias_gelu_d"):
+            if epi != "bias" and N != 3072:
+                continue
+            C = torch.empty(M, N, device=dev, dtype=dt)
+            aux = torch.empty(M, N, device=dev, dtype=dt) if epi != "bias" else None
+            K.gemm(A, B, C, M=M, N=N, K=Kd, a_kc=1, b_kc=1, lda=Kd, ldb=Kd, ldc=N, epi=epi, bias=bias, aux=aux,
+                   ldaux=N)
+            torch.cuda.synchronize()
+            print(f"fwd   {N:5d}x{Kd:5d} {epi:12s} C {digest(C)}" + (f" aux {digest(aux)}" if aux is not None else ""))
+    # input gradients: dY [M, K] (k-contiguous) x W [K, N] (k-major)
+    for N, Kd, epi, beta in ((3072, 768, "mul_aux", 0.0), (3072, 768, "dgelu", 0.0), (768, 3072, "none", 1.0),
+                             (768, 2304, "none", 1.0), (768, 768, "none", 0.0)):
+        A = rn(M, Kd).to(dt)
+        B = (rn(Kd, N) * 0.05).to(dt)
+        C = (rn(M, N) * 0.01).to(dt)
+        aux = rn(M, N).to(dt) if epi != "none" else None
+        K.gemm(A, B, C, M=M, N=N, K=Kd, a_kc=1, b_kc=0, lda=Kd, ldb=N, ldc=N, epi=epi, aux=aux, ldaux=N, beta=beta)
+        torch.cuda.synchronize()
+        print(f"dgrad {N:5d}x{Kd:5d} {epi:8s} beta={beta:g} C {digest(C)}")
+
+
+if __name__ == "__main__":
+    main()
