@@ -68,6 +68,39 @@ def test_lint_flags_sign_extended_low_word_of_an_address():
     assert ok == []
 
 
+def _bias_issue():
+    return [f"global_load_dwordx4 v[{4 * j}:{4 * j + 3}], v[40:41], off" + (f" offset:{64 * j}" if j else "")
+            for j in range(8)]
+
+
+_WAIT = ["s_cmp_eq_u32 s4, 0", "s_cbranch_scc1 1 <k+0x0>", "s_waitcnt vmcnt(8)"]
+
+
+def test_lint_flags_a_copy_of_in_flight_bias_registers():
+    """gemm4r's split bias load: a copy of a destination register between the issue statement and its
+    counted wait reads data still being loaded (the first build of the split did that on one side of a
+    branch); MFMAs and other registers in between are fine."""
+    ok = isa_lint.lint_async("k", _prog(*_bias_issue(), "v_mfma_f32_16x16x32_bf16 a[0:3], v[48:51], v[52:55], a[0:3]",
+                                        *_WAIT, "v_mov_b64_e32 v[60:61], v[4:5]"))
+    assert ok == []
+    bad = isa_lint.lint_async("k", _prog(*_bias_issue(), "v_mov_b64_e32 v[60:61], v[4:5]", *_WAIT))
+    assert [x.kind for x in bad] == ["async_load_touch"]
+    # load_bias8 (issue + wait in one statement) is not a split load
+    assert isa_lint.async_issue_blocks(_prog(*_bias_issue(), "s_waitcnt vmcnt(0)", "v_mov_b32 v60, v4")) == []
+
+
+def test_lint_flags_an_accumulator_read_inside_the_mfma_latency():
+    """An asm MFMA is opaque to hipcc's hazard recognizer: a register-allocator copy of its accumulator
+    one state later read stale values (the first split-bias build of gemm4r)."""
+    mfma = "v_mfma_f32_16x16x32_bf16 a[8:11], v[96:99], v[248:251], a[8:11]"
+    bad = isa_lint.lint_mfma_d("k", _prog(mfma, "s_nop 0", "v_accvgpr_read_b32 v33, a11"))
+    assert [(x.kind, x.states) for x in bad] == [("mfma_d_read", 1)]
+    ok = isa_lint.lint_mfma_d("k", _prog(mfma, "s_nop 7", "s_nop 7", "v_accvgpr_read_b32 v33, a11"))
+    assert ok == []
+    other = isa_lint.lint_mfma_d("k", _prog(mfma, "v_accvgpr_read_b32 v33, a12"))     # not the MFMA's D
+    assert other == []
+
+
 @pytest.mark.skipif(not LIB.exists(), reason="libeegfusion.so not built (run __graft_entry__.build())")
 def test_shipped_library_has_no_vmem_sgpr_hazards():
     findings, counts = isa_lint.lint(LIB)

@@ -24,6 +24,18 @@ do", item 2).  This lint reads the shipped library, not the sources:
    returns ``int``): bit 31 of the address then sets bits 32..63, an illegal address on roughly half
    of all buffers (r4o: a GPU memory-access fault in the weight-gradient GEMM).
 
+4. ``async_load_touch`` — gemm4r issues its bias quads in one asm statement (``issue_bias8``: eight
+   ``global_load_dwordx4`` at offsets 0 .. 448 with no wait) and retires them in a later one
+   (``wait_vm_bias8``: ``s_cmp_eq_u32`` / ``s_cbranch_scc1`` / ``s_waitcnt vmcnt(8)``).  hipcc does not
+   know the destination VGPRs are still being written, so every control-flow path from the issue to
+   that wait is walked and any instruction naming a destination register is reported (a copy placed
+   there reads in-flight data: the first build of the split did exactly that on one side of a branch).
+
+5. ``mfma_d_read`` — a ``v_accvgpr_read`` / ``v_accvgpr_write`` of an AGPR that an MFMA wrote fewer than
+   12 wait states earlier (16 for the 32x32 shapes).  hipcc pads its own MFMAs, but the K-loops' MFMAs
+   are asm statements, and the register allocator may place an accumulator copy right after one (it
+   did when a 32-VGPR value was kept live across the last K-tile: wrong epilogue values).
+
 usage: python tools/isa_lint.py [path/to/libeegfusion.so] [--all]
 Exit status 1 when any hazard is found.  ``tests/test_isa_lint_cpu.py`` runs it on the built library.
 """
@@ -44,6 +56,7 @@ BUNDLE_MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
 ARCH = "gfx950"
 
 REQUIRED = {"valu_sgpr_vmem": 5, "salu_m0_lds_dma": 1}
+_VREG = re.compile(r"\bv\[(\d+):(\d+)\]|\bv(\d+)\b")
 SEXT32 = "0x200000"          # s_bfe_i64 operand: offset 0, width 32
 
 # VALU mnemonics whose second operand is an SGPR destination (carry-out / scale flag)
@@ -120,7 +133,14 @@ def disassemble(code: bytes) -> dict[str, list[Inst]]:
         if m and cur is not None:
             mnem, rest, addr = m.group(1), m.group(2).strip(), int(m.group(3), 16)
             ops = [o.strip().split()[0] for o in rest.split(",") if o.strip()] if rest else []
-            cur.append(Inst(addr, mnem, ops, f"{mnem} {rest}".strip()))
+            text = f"{mnem} {rest}".strip()
+            if mnem.startswith(("s_branch", "s_cbranch")):
+                # the branch target sits in objdump's trailing comment ("// addr: enc <func+0x..>"); keep it
+                # in the text, or no branch edge is ever followed
+                t = _TARGET.search(line)
+                if t:
+                    text += f" <{t.group(1)}+0x{t.group(2)}>"
+            cur.append(Inst(addr, mnem, ops, text))
     return funcs
 
 
@@ -213,11 +233,111 @@ def lint_function(name: str, insts: list[Inst]) -> list[Finding]:
     return out
 
 
+def vregs(text: str) -> set:
+    out = set()
+    for m in _VREG.finditer(text):
+        if m.group(3) is not None:
+            out.add(int(m.group(3)))
+        else:
+            out |= set(range(int(m.group(1)), int(m.group(2)) + 1))
+    return out
+
+
+def async_issue_blocks(insts: list[Inst]) -> list[tuple[int, set]]:
+    """(index after the block, destination VGPRs) of every issue-only bias load block."""
+    out = []
+    for k in range(len(insts) - 8):
+        blk = insts[k:k + 8]
+        if not all(i.mnem == "global_load_dwordx4" for i in blk):
+            continue
+        if k > 0 and insts[k - 1].mnem == "global_load_dwordx4":
+            continue
+        offs = [int(m.group(1)) if (m := re.search(r"offset:(\d+)", i.text)) else 0 for i in blk]
+        if offs != [64 * j for j in range(8)] or len({i.ops[1] for i in blk}) != 1:
+            continue
+        nxt = insts[k + 8]
+        if nxt.mnem == "s_waitcnt" and "vmcnt" in nxt.text:
+            continue                                # load_bias8: retired in the same statement
+        out.append((k + 8, set().union(*(vregs(i.ops[0]) for i in blk))))
+    return out
+
+
+def lint_async(name: str, insts: list[Inst]) -> list[Finding]:
+    by_addr = {ins.addr: k for k, ins in enumerate(insts)}
+    out = []
+    for start, dst in async_issue_blocks(insts):
+        seen, stack, touches = set(), [start], []
+        while stack:
+            j = stack.pop()
+            while j < len(insts) and j not in seen:
+                seen.add(j)
+                ins = insts[j]
+                if ins.mnem == "s_cmp_eq_u32" and j + 2 < len(insts) and insts[j + 1].mnem == "s_cbranch_scc1" and \
+                        insts[j + 2].mnem == "s_waitcnt" and "vmcnt" in insts[j + 2].text:
+                    break                           # wait_vm_bias8: retired on this path
+                if ins.mnem in ("s_endpgm", "s_setpc_b64"):
+                    break
+                if vregs(ins.text) & dst:
+                    touches.append(ins)
+                if ins.mnem.startswith(("s_branch", "s_cbranch")):
+                    m = _TARGET.search(ins.text)
+                    if m:
+                        tgt = insts[0].addr + int(m.group(2), 16)
+                        if tgt in by_addr:
+                            stack.append(by_addr[tgt])
+                    if ins.mnem == "s_branch":
+                        break
+                j += 1
+        for t in touches[:1]:
+            out.append(Finding("async_load_touch", name, insts[start - 8].addr, insts[start - 8].text, t.text, len(touches)))
+    return out
+
+
+_AREG = re.compile(r"\ba\[(\d+):(\d+)\]|\ba(\d+)\b")
+
+
+def aregs(op: str) -> set:
+    out = set()
+    for m in _AREG.finditer(op):
+        if m.group(3) is not None:
+            out.add(int(m.group(3)))
+        else:
+            out |= set(range(int(m.group(1)), int(m.group(2)) + 1))
+    return out
+
+
+def lint_mfma_d(name: str, insts: list[Inst]) -> list[Finding]:
+    """accvgpr read / write of an MFMA destination within its result latency (straight-line look-back)."""
+    out = []
+    for k, ins in enumerate(insts):
+        if not ins.mnem.startswith("v_accvgpr_") or len(ins.ops) < 2:
+            continue
+        touched = aregs(ins.ops[1] if ins.mnem.startswith("v_accvgpr_read") else ins.ops[0])
+        if not touched:
+            continue
+        acc, j = 0, k - 1
+        while j >= 0 and acc < 16:
+            p = insts[j]
+            if p.mnem in ("s_branch", "s_endpgm", "s_setpc_b64") or p.mnem.startswith("s_cbranch"):
+                break
+            if p.mnem.startswith("v_mfma") and p.ops and aregs(p.ops[0]) & touched:
+                need = 16 if "32x32" in p.mnem else 12
+                if acc < need:
+                    out.append(Finding("mfma_d_read", name, ins.addr, ins.text, p.text, acc))
+                break
+            acc += states(p)
+            j -= 1
+    return out
+
+
 def lint(so: Path) -> tuple[list[Finding], Counter]:
     findings, vmem = [], Counter()
     for code in bundles(so):
         for name, insts in disassemble(code).items():
             findings += lint_function(name, insts)
+            findings += lint_async(name, insts)
+            findings += lint_mfma_d(name, insts)
+            vmem["async_issue"] += len(async_issue_blocks(insts))
             vmem["lds_dma"] += sum(is_lds_dma(i) for i in insts)
             vmem["vmem"] += sum(bool(_VMEM.match(i.mnem)) for i in insts)
     return findings, vmem
@@ -228,7 +348,8 @@ def main(argv: list[str]) -> int:
     so = Path(args[0]) if args else Path(__file__).resolve().parents[1] / "eeg-multimodal_amd" / "eegfusion" / \
         "libeegfusion.so"
     findings, vmem = lint(so)
-    print(f"{so}: {vmem['vmem']} VMEM instructions ({vmem['lds_dma']} LDS-DMA), {len(findings)} hazards")
+    print(f"{so}: {vmem['vmem']} VMEM instructions ({vmem['lds_dma']} LDS-DMA, {vmem['async_issue']} split bias "
+          f"loads), {len(findings)} hazards")
     per = Counter((f.kind, f.func) for f in findings)
     for (kind, func), n in per.most_common():
         print(f"  {n:5d}  {kind:16s} {func}")
