@@ -711,6 +711,14 @@ DEV int sw4(int r) { return 3 * ((r >> 3) & 1); }
 DEV void mma16_acc(f32x4& acc, bf16x8 b, bf16x8 a) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
 }
+// the same MFMA with a VGPR accumulator (the weight-gradient row sums against a ones operand; every
+// AGPR holds the tile).  Its D is read only after the K-loop's closing s_nop padding (isa_lint
+// mfma_d_read checks both register files)
+// s_nop 2 first: hipcc does not pad a VALU write of an asm MFMA's source (it rebuilt the ones operand
+// with v_mov right before it: NaN row sums, isa_lint mfma_src_write)
+DEV void mma16_vacc(f32x4& acc, bf16x8 b, bf16x8 a) {
+  asm volatile("s_nop 2\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(b), "v"(a));
+}
 // first K-tile: the accumulator is DEFINED in AGPRs (srcC = 0), so no VGPR copy of it ever exists
 DEV void mma16_acc0(f32x4& acc, bf16x8 b, bf16x8 a) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(acc) : "v"(b), "v"(a));
@@ -731,8 +739,9 @@ DEV bf16x8 rd_col_off(const bf16* t, int o0, int o1) {
 // ds_read_b64_tr_b16 fragments: input-gradient B, weight-gradient A and B)
 // RS (weight gradients, A = dY k-major): the same kernel also sums every A row over K (the bias
 // gradient dY.sum(0) of the nn.Linear whose weight gradient this is): in workgroups of tile column 0,
-// wave (wm, wn) sums its row blocks s = 4 wn .. 4 wn + 3 from the A fragments it already holds,
-// partials -> rowsum_part[split][M].
+// wave (wm, wn) sums its row blocks s = 4 wn .. 4 wn + 3 by one MFMA per block and K-tile against a
+// ones operand, partials -> rowsum_part[split][M].  Spreading the blocks over the tile row's
+// workgroups (at most 2 per wave for 3 tile columns) measured the same (profiles/r5zd_ab_summary.log).
 template <bool AKC, bool BKC, int EPI, typename TO, bool RS = false>
 __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
   constexpr int LDS4 = NSLOT4 * SLOT4;
@@ -835,13 +844,16 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
     return BKC ? *(const bf16x8*)(img + offB + i * 16 * BK4) : rd_col_off(img, tB0[i], tB1[i]);
   };
   f32x4 acc[8][8];           // defined by the first K-tile's MFMAs (mma16_acc0)
-  // RS: per-lane fp32 partial row sums (row 16 s + (lane & 15), k-block lane >> 4) of the wave's 4 row
-  // blocks, summed on the VALU from the A fragments already in registers (16 VALU per fragment, in the
-  // MFMA shadows).  An MFMA against a ones operand would need 8+ more VGPRs: at 256 VGPRs + 256 AGPRs
-  // the compiler then shuttles the asm-pinned accumulators through v_accvgpr_read/write, which the
-  // hazard recognizer cannot time against the opaque asm MFMAs (wrong results, measured).
+  // RS: the row sums of the wave's 4 row blocks (s = 4 wn .. 4 wn + 3), one MFMA per block and K-tile
+  // against a ones operand into a VGPR accumulator: D[i][j] = sum over the K-tile's 32 k of A row 16 s + j
+  // for every i.  Summed on the VALU instead (16 VALU per fragment: 64 per K-tile beside 64 MFMAs) it
+  // made the whole launch 12 % slower than the plain weight gradient (profiles/r5zb_ab.log: the
+  // workgroups of tile column 0 are the critical path of a one-wave grid); 4 MFMAs are 6 % of the
+  // K-tile.  Not bitwise the VALU order; deterministic.
   const bool do_rs = RS && tn == 0;
-  float rsv[4] = {0.f, 0.f, 0.f, 0.f};
+  f32x4 rsacc[4] = {};
+  bf16x8 ones = __builtin_bit_cast(bf16x8, u32x4{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u});
+  asm volatile("" : "+v"(ones));     // opaque: kept in 4 VGPRs instead of rebuilt before every use
 
   // prologue: K-tiles 0 .. NSLOT4-1 staged; 0 and 1 retired
   ts_mark(g, 0);
@@ -928,17 +940,9 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
       if (EEGF_W_STAGGER && st && wave == 3) stage_part(sA, sB, slot, s, WNOP{});
       __builtin_amdgcn_sched_barrier(0);
       mma(s, 7);
-      // RS: row sums of this K-tile's A rows 16 s .. (lane & 15 -> row, every D column the same sum);
-      // compiler-visible MFMA (hazards against the VALU reads at the end are the compiler's)
+      // RS: row sums of this K-tile's A rows 16 s .. 16 s + 15 (D column j = row 16 s + j)
       if constexpr (RS) {
-        if (do_rs && (s >> 2) == wn) {
-          const u32x4 w = __builtin_bit_cast(u32x4, fa[H][s]);
-          float v = rsv[s & 3];
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            v += __builtin_bit_cast(float, w[q] << 16) + __builtin_bit_cast(float, w[q] & 0xFFFF0000u);
-          rsv[s & 3] = v;
-        }
+        if (do_rs && (s >> 2) == wn) mma16_vacc(rsacc[s & 3], ones, fa[H][s]);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
@@ -982,12 +986,9 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_waitcnt vmcnt(0)" ::: "memory");
   if (RS && do_rs) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {      // fold the 4 k-blocks (lane groups 16 apart), fixed order
-      float v = rsv[j];
-      v += __shfl_xor(v, 16, 64);
-      v += __shfl_xor(v, 32, 64);
+    for (int j = 0; j < 4; ++j) {      // lanes 0..15 hold rows 16 (4 wn + j) + lane (every i the same sum)
       const int m = m0 + wm * 128 + 16 * (4 * wn + j) + lane;
-      if (lane < 16 && m < g.M) g.rowsum_part[(long)split * g.M + m] = v;
+      if (lane < 16 && m < g.M) g.rowsum_part[(long)split * g.M + m] = rsacc[j][0];
     }
   }
   __syncthreads();

@@ -119,8 +119,8 @@ int eegf_gemm_colsum_tiles(int dtype, int out_dtype, int a_kcontig, int M, int N
 /* Weight gradient of an nn.Linear with its bias gradient fused (autograd of F.linear, the weight and
  * bias grads of every BERT projection, modeling_bert.py:139-351): dW [M][N] = dY^T X + beta dW over
  * K tokens, db [M] += dY.sum(0).  dY [K][M] (row stride ldd) and X [K][N] (ldx) bf16; dW, db fp32.
- * The row sums ride on the weight-gradient kernel (4 MFMAs per K-tile against a ones operand in the
- * workgroups of tile column 0) and are reduced in a fixed order.  workspace: fp32 split-K slabs
+ * The row sums ride on the weight-gradient kernel (summed on the VALU from the dY fragments the
+ * workgroups of tile column 0 already hold, in the MFMA shadows) and are reduced in a fixed order.  workspace: fp32 split-K slabs
  * (splits x (M*N + M) floats).  EEGF_ERR_ARG when the shape is not eligible (bf16, M, N >= 256,
  * K >= 4096, K % 64 == 0, 8-aligned dims, 16-B aligned dY / X, workspace too small): run eegf_gemm and
  * eegf_colsum instead. */

@@ -101,6 +101,21 @@ def test_lint_flags_an_accumulator_read_inside_the_mfma_latency():
     assert other == []
 
 
+def test_lint_flags_a_fresh_vgpr_source_of_an_mfma():
+    """hipcc rebuilt the ones operand of the weight-gradient row-sum MFMA (an asm statement) with v_mov
+    right before it: the MFMA read a half-written operand (NaN bias gradients)."""
+    bad = isa_lint.lint_mfma_src("k", _prog("v_mov_b32_e32 v153, v150",
+                                            "v_mfma_f32_16x16x32_bf16 v[78:81], v[150:153], v[34:37], v[78:81]"))
+    assert [x.kind for x in bad] == ["mfma_src_write"]
+    ok = isa_lint.lint_mfma_src("k", _prog("v_mov_b32_e32 v153, v150", "s_nop 2",
+                                           "v_mfma_f32_16x16x32_bf16 v[78:81], v[150:153], v[34:37], v[78:81]"))
+    assert ok == []
+    # a VGPR accumulator read by VALU inside the result latency
+    d = isa_lint.lint_mfma_d("k", _prog("v_mfma_f32_16x16x32_bf16 v[78:81], v[150:153], v[34:37], v[78:81]",
+                                        "v_mov_b32_e32 v0, v78"))
+    assert [x.kind for x in d] == ["mfma_d_read"]
+
+
 @pytest.mark.skipif(not LIB.exists(), reason="libeegfusion.so not built (run __graft_entry__.build())")
 def test_shipped_library_has_no_vmem_sgpr_hazards():
     findings, counts = isa_lint.lint(LIB)

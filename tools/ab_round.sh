@@ -23,6 +23,12 @@ if [ $# -gt 2 ]; then
     run "new gemm $rep" "" 200 python -u tools/gemm_bench.py "${@:3}" || exit 1
   done
 fi
+if [ -n "$WGRAD" ]; then
+  for rep in $(seq $REPS); do
+    run "base wgrad $rep" ab/libbase.so 200 python -u tools/wgrad_probe.py || exit 1
+    run "new wgrad $rep" "" 200 python -u tools/wgrad_probe.py || exit 1
+  done
+fi
 for rep in $(seq $REPS); do
   run "base bench $rep" ab/libbase.so 200 python -u bench.py --no-cpu-baseline --steps 20 --warmup 5 || exit 1
   run "new bench $rep" "" 200 python -u bench.py --no-cpu-baseline --steps 20 --warmup 5 || exit 1
@@ -35,7 +41,7 @@ for line in open(sys.argv[1]):
     if line.startswith("== "):
         cur = line[3:].split()[0]
         continue
-    if line.startswith(("fwd ", "dgrad ")):
+    if line.startswith(("fwd ", "dgrad ", "wgrad ")):
         bits[cur].append(line.strip())
     elif line.startswith("{"):
         try:
@@ -46,6 +52,10 @@ for line in open(sys.argv[1]):
         m = re.match(r"(\S+)\s+M=\s*\d+ N=\s*\d+ K=\s*\d+\s+eegf\s+([\d.]+) us", line)
         if m:
             gem[(cur, m.group(1))].append(float(m.group(2)))
+        m = re.match(r"(\S+_wgrad)\s+\S+\s+with bias grad\s+([\d.]+) us\s+plain\s+([\d.]+) us", line)
+        if m:
+            gem[(cur, m.group(1) + "+bias")].append(float(m.group(2)))
+            gem[(cur, m.group(1))].append(float(m.group(3)))
 print("bits identical:", bits["base"] == bits["new"] and len(bits["base"]) > 0)
 for a, b in zip(bits["base"], bits["new"]):
     if a != b:

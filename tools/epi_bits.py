@@ -47,6 +47,20 @@ def main():
         K.gemm(A, B, C, M=M, N=N, K=Kd, a_kc=1, b_kc=0, lda=Kd, ldb=N, ldc=N, epi=epi, aux=aux, ldaux=N, beta=beta)
         torch.cuda.synchronize()
         print(f"dgrad {N:5d}x{Kd:5d} {epi:8s} beta={beta:g} C {digest(C)}")
+    # weight gradients with the fused bias gradient (eegf_gemm_wgrad_bias): dW [Mo][N] += dY^T X, db += dY.sum(0)
+    from eegfusion import _lib
+    lib = _lib.lib()
+    ws = torch.empty(64 << 20, device=dev)
+    R = 4 * M
+    for Mo, N in ((2304, 768), (768, 3072)):
+        dy = rn(R, Mo).to(dt)
+        x = rn(R, N).to(dt)
+        dw = rn(Mo, N) * 0.01
+        db = rn(Mo) * 0.01
+        st = lib.eegf_gemm_wgrad_bias(_lib.BF16, Mo, N, R, dy.data_ptr(), Mo, x.data_ptr(), N, dw.data_ptr(), N, 1.0,
+                                      db.data_ptr(), ws.data_ptr(), ws.numel() * 4, 0)
+        torch.cuda.synchronize()
+        print(f"wgrad {Mo:5d}x{N:5d} K={R} st={st} dW {digest(dw)} db {digest(db)}")
 
 
 if __name__ == "__main__":

@@ -31,10 +31,14 @@ do", item 2).  This lint reads the shipped library, not the sources:
    that wait is walked and any instruction naming a destination register is reported (a copy placed
    there reads in-flight data: the first build of the split did exactly that on one side of a branch).
 
-5. ``mfma_d_read`` — a ``v_accvgpr_read`` / ``v_accvgpr_write`` of an AGPR that an MFMA wrote fewer than
-   12 wait states earlier (16 for the 32x32 shapes).  hipcc pads its own MFMAs, but the K-loops' MFMAs
+5. ``mfma_d_read`` — an instruction that reads or writes an MFMA's destination (AGPRs or VGPRs; an
+   MFMA taking it as srcC excepted) sooner after it than hipcc pads its own MFMAs (16x16x32 bf16: 8
+   wait states, 16x16x4 f32: 10).  hipcc pads its own MFMAs, but the K-loops' MFMAs
    are asm statements, and the register allocator may place an accumulator copy right after one (it
    did when a 32-VGPR value was kept live across the last K-tile: wrong epilogue values).
+
+6. ``mfma_src_write`` — a VALU write of a VGPR that an MFMA reads as srcA / srcB fewer than 2 wait states
+   before it (hipcc rebuilt a constant operand of an asm MFMA with ``v_mov`` right before it).
 
 usage: python tools/isa_lint.py [path/to/libeegfusion.so] [--all]
 Exit status 1 when any hazard is found.  ``tests/test_isa_lint_cpu.py`` runs it on the built library.
@@ -307,23 +311,58 @@ def aregs(op: str) -> set:
 
 
 def lint_mfma_d(name: str, insts: list[Inst]) -> list[Finding]:
-    """accvgpr read / write of an MFMA destination within its result latency (straight-line look-back)."""
+    """Any instruction but an MFMA taking it whole as srcC that reads or writes an MFMA's destination
+    (AGPRs or VGPRs) within its result latency (straight-line look-ahead)."""
     out = []
     for k, ins in enumerate(insts):
-        if not ins.mnem.startswith("v_accvgpr_") or len(ins.ops) < 2:
+        if not ins.mnem.startswith("v_mfma") or not ins.ops:
             continue
-        touched = aregs(ins.ops[1] if ins.mnem.startswith("v_accvgpr_read") else ins.ops[0])
-        if not touched:
+        d = ins.ops[0]
+        dst = ("a", aregs(d)) if d.startswith("a") else ("v", vregs(d))
+        if not dst[1]:
             continue
-        acc, j = 0, k - 1
-        while j >= 0 and acc < 16:
+        # the result latency in wait states, as hipcc pads its own MFMAs on gfx950 (16x16x32 bf16: 8,
+        # 16x16x4 f32: 10; 32x32 shapes taken as 16)
+        need = 16 if "32x32" in ins.mnem else 8 if "16x16x32" in ins.mnem else 10 if "16x16x4" in ins.mnem else 12
+        acc, j = 0, k + 1
+        while j < len(insts) and acc < need:
             p = insts[j]
             if p.mnem in ("s_branch", "s_endpgm", "s_setpc_b64") or p.mnem.startswith("s_cbranch"):
                 break
-            if p.mnem.startswith("v_mfma") and p.ops and aregs(p.ops[0]) & touched:
-                need = 16 if "32x32" in p.mnem else 12
-                if acc < need:
-                    out.append(Finding("mfma_d_read", name, ins.addr, ins.text, p.text, acc))
+            rd = aregs if dst[0] == "a" else vregs
+            if p.mnem.startswith("v_mfma"):
+                # MFMA -> MFMA through srcC is interlocked (the accumulate chains; hipcc pads its own
+                # other cases); through srcA / srcB it is a hazard
+                if len(p.ops) > 2 and (rd(p.ops[1]) | rd(p.ops[2])) & dst[1]:
+                    out.append(Finding("mfma_d_read", name, p.addr, p.text, ins.text, acc))
+                    break
+                acc += 1
+                j += 1
+                continue
+            regs = rd(p.text)
+            if regs & dst[1]:
+                out.append(Finding("mfma_d_read", name, p.addr, p.text, ins.text, acc))
+                break
+            acc += states(p)
+            j += 1
+    return out
+
+
+def lint_mfma_src(name: str, insts: list[Inst]) -> list[Finding]:
+    """A VALU / VMEM / LDS write of a VGPR that the next MFMA reads as srcA / srcB within 2 wait states
+    (hipcc pads its own MFMAs; an asm MFMA's operands it does not)."""
+    out = []
+    for k, ins in enumerate(insts):
+        if not ins.mnem.startswith("v_mfma") or len(ins.ops) < 3:
+            continue
+        src = vregs(ins.ops[1]) | vregs(ins.ops[2])
+        acc, j = 0, k - 1
+        while j >= 0 and acc < 2:
+            p = insts[j]
+            if p.mnem in ("s_branch", "s_endpgm", "s_setpc_b64") or p.mnem.startswith("s_cbranch"):
+                break
+            if p.mnem.startswith("v_") and not p.mnem.startswith("v_mfma") and p.ops and vregs(p.ops[0]) & src:
+                out.append(Finding("mfma_src_write", name, ins.addr, ins.text, p.text, acc))
                 break
             acc += states(p)
             j -= 1
@@ -337,6 +376,7 @@ def lint(so: Path) -> tuple[list[Finding], Counter]:
             findings += lint_function(name, insts)
             findings += lint_async(name, insts)
             findings += lint_mfma_d(name, insts)
+            findings += lint_mfma_src(name, insts)
             vmem["async_issue"] += len(async_issue_blocks(insts))
             vmem["lds_dma"] += sum(is_lds_dma(i) for i in insts)
             vmem["vmem"] += sum(bool(_VMEM.match(i.mnem)) for i in insts)
