@@ -120,9 +120,16 @@ def test_b16_takes_the_bench_routes():
         batch = {"eeg": torch.randn(B, 64, 256, generator=g, device=DEV),
                  "act": torch.randn(B, 32, generator=g, device=DEV) * 0.5}
         labels = (torch.rand(B, generator=g, device=DEV) < 0.66).long()
+        if B == 16:
+            batch16, labels16 = batch, labels
         tr.step(batch, labels)                           # warm (workspaces sized)
         sets[B] = _kernel_names(lambda: tr.step(batch, labels))
     big, small = _prod_kernels(sets[256]), _prod_kernels(sets[16])
+    if not big <= small:
+        # the torch profiler on ROCm occasionally drops a step's later kernel records (r5ze: a B = 16
+        # profile held the forward kernels only; the same test passed twice in a row on the next box,
+        # r5zf_routes.log): profile the B = 16 step once more and take the union
+        small |= _prod_kernels(_kernel_names(lambda: tr.step(batch16, labels16)))
     print("\n[routes] B=256 production kernels:", len(big), "B=16:", len(small))
     for n in sorted(big):
         print("   ", "ok " if n in small else "MISSING", n[:160])

@@ -9,6 +9,7 @@ O=gpurun_out
 mkdir -p $O
 export PYTHONUNBUFFERED=1
 L=$O/${TAG}_ab.log
+NEW=${NEWLIB:-}          # the "new" arm: the in-tree library, or NEWLIB (a variant build under ab/)
 : > $L
 run() {   # run <label> <lib or ""> <seconds> <cmd...>
   local label=$1 lib=$2 t=$3; shift 3
@@ -16,22 +17,22 @@ run() {   # run <label> <lib or ""> <seconds> <cmd...>
   EEGF_LIB=$lib timeout -k 10 $t "$@" >> $L 2>&1
 }
 run "base bits" ab/libbase.so 120 python -u tools/epi_bits.py || exit 1
-run "new bits" "" 120 python -u tools/epi_bits.py || exit 1
+run "new bits" "$NEW" 120 python -u tools/epi_bits.py || exit 1
 if [ $# -gt 2 ]; then
   for rep in $(seq $REPS); do
     run "base gemm $rep" ab/libbase.so 200 python -u tools/gemm_bench.py "${@:3}" || exit 1
-    run "new gemm $rep" "" 200 python -u tools/gemm_bench.py "${@:3}" || exit 1
+    run "new gemm $rep" "$NEW" 200 python -u tools/gemm_bench.py "${@:3}" || exit 1
   done
 fi
 if [ -n "$WGRAD" ]; then
   for rep in $(seq $REPS); do
     run "base wgrad $rep" ab/libbase.so 200 python -u tools/wgrad_probe.py || exit 1
-    run "new wgrad $rep" "" 200 python -u tools/wgrad_probe.py || exit 1
+    run "new wgrad $rep" "$NEW" 200 python -u tools/wgrad_probe.py || exit 1
   done
 fi
 for rep in $(seq $REPS); do
   run "base bench $rep" ab/libbase.so 200 python -u bench.py --no-cpu-baseline --steps 20 --warmup 5 || exit 1
-  run "new bench $rep" "" 200 python -u bench.py --no-cpu-baseline --steps 20 --warmup 5 || exit 1
+  run "new bench $rep" "$NEW" 200 python -u bench.py --no-cpu-baseline --steps 20 --warmup 5 || exit 1
 done
 python - "$L" > $O/${TAG}_ab_summary.log <<'EOF'
 import json, re, sys
