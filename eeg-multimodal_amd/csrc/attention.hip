@@ -459,9 +459,13 @@ int g_attn256_mode = [] {
 namespace {
 // the L = 256 kernels draw with 32-bit call numbers (keep01x8_c32 / keep_bits8_c32): every call of the
 // launch, < B H L 4 ceil(L / 32), must fit (B <= 43690 at H = 12); larger B runs the generic kernels
-bool l256_path(int dtype, int B, int H, int L, const float* key_bias, bool bwd) {
+// and they index in 32 bits (attention256.inc): every element offset (rows x the larger stride, the
+// keep-bit bytes) must stay below 2^31
+bool l256_path(int dtype, int B, int H, int L, const float* key_bias, bool bwd, long ld_qkv, long ld_out) {
   const bool c32 = (uint64_t)B * H * L * 4 * ((L + 31) / 32) <= (1ull << 32);
-  return (g_attn256_mode & (bwd ? 2 : 1)) && dtype == EEGF_BF16 && L == LF && !key_bias && c32;
+  const bool i32 = (uint64_t)B * L * (uint64_t)(ld_qkv > ld_out ? ld_qkv : ld_out) < (1ull << 31) &&
+                   (uint64_t)B * H * L * (L / 8) < (1ull << 31);
+  return (g_attn256_mode & (bwd ? 2 : 1)) && dtype == EEGF_BF16 && L == LF && H == 12 && !key_bias && c32 && i32;
 }
 
 }  // namespace
@@ -474,7 +478,7 @@ extern "C" int eegf_attn_fwd(int dtype, int B, int H, int L, const void* qkv, lo
   if (B > 65535 || drop_p < 0.f || drop_p >= 1.f) return EEGF_ERR_ARG;
   AttnArgs a{qkv, out, lse, key_bias, nullptr, nullptr, nullptr, nullptr, B, H, L, ld_qkv, ld_out, scale,
              drop_p, seed, offset, drop_p > 0.f ? drop_bits : nullptr};
-  if (l256_path(dtype, B, H, L, key_bias, false)) {
+  if (l256_path(dtype, B, H, L, key_bias, false, ld_qkv, ld_out)) {
     const dim3 g1(l256_grid(B * H));
     if (a.bits) hipLaunchKernelGGL((attn_fwd256_kernel<true, true>), g1, dim3(512), 0, stream, a);
     else if (drop_p > 0.f) hipLaunchKernelGGL(attn_fwd256_kernel<true>, g1, dim3(512), 0, stream, a);
@@ -500,7 +504,7 @@ extern "C" int eegf_attn_bwd(int dtype, int B, int H, int L, const void* qkv, lo
   if (L > 256) hipMemsetAsync(dq_workspace, 0, sizeof(float) * (size_t)B * L * 768, stream);
   AttnArgs a{qkv, nullptr, const_cast<float*>(lse), key_bias, out, dout, dqkv, dq_workspace, B, H, L, ld_qkv, ld_out,
              scale, drop_p, seed, offset, drop_p > 0.f ? const_cast<uint32_t*>(drop_bits) : nullptr};
-  if (l256_path(dtype, B, H, L, key_bias, true)) {
+  if (l256_path(dtype, B, H, L, key_bias, true, ld_qkv, ld_out)) {
     const dim3 g1(l256_grid(B * H));
     if (drop_p > 0.f) hipLaunchKernelGGL(attn_bwd256_kernel<true>, g1, dim3(512), 0, stream, a);
     else hipLaunchKernelGGL(attn_bwd256_kernel<false>, g1, dim3(512), 0, stream, a);

@@ -30,6 +30,12 @@ if [ -n "$WGRAD" ]; then
     run "new wgrad $rep" "$NEW" 200 python -u tools/wgrad_probe.py || exit 1
   done
 fi
+if [ -n "$ATTN" ]; then
+  for rep in $(seq $REPS); do
+    run "base attn $rep" ab/libbase.so 200 python -u tools/attn_bench.py --nobits || exit 1
+    run "new attn $rep" "$NEW" 200 python -u tools/attn_bench.py --nobits || exit 1
+  done
+fi
 for rep in $(seq $REPS); do
   run "base bench $rep" ab/libbase.so 200 python -u bench.py --no-cpu-baseline --steps 20 --warmup 5 || exit 1
   run "new bench $rep" "$NEW" 200 python -u bench.py --no-cpu-baseline --steps 20 --warmup 5 || exit 1
@@ -42,7 +48,7 @@ for line in open(sys.argv[1]):
     if line.startswith("== "):
         cur = line[3:].split()[0]
         continue
-    if line.startswith(("fwd ", "dgrad ", "wgrad ")):
+    if line.startswith(("fwd ", "dgrad ", "wgrad ", "attn ")):
         bits[cur].append(line.strip())
     elif line.startswith("{"):
         try:
@@ -53,6 +59,9 @@ for line in open(sys.argv[1]):
         m = re.match(r"(\S+)\s+M=\s*\d+ N=\s*\d+ K=\s*\d+\s+eegf\s+([\d.]+) us", line)
         if m:
             gem[(cur, m.group(1))].append(float(m.group(2)))
+        m = re.match(r"(attn_\w+) B=\d+ L=\d+ p=\S+ bits=(\d):\s+([\d.]+) us", line)
+        if m:
+            gem[(cur, m.group(1) + ("+bits" if m.group(2) == "1" else ""))].append(float(m.group(3)))
         m = re.match(r"(\S+_wgrad)\s+\S+\s+with bias grad\s+([\d.]+) us\s+plain\s+([\d.]+) us", line)
         if m:
             gem[(cur, m.group(1) + "+bias")].append(float(m.group(2)))

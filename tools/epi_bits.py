@@ -61,6 +61,24 @@ def main():
                                       db.data_ptr(), ws.data_ptr(), ws.numel() * 4, 0)
         torch.cuda.synchronize()
         print(f"wgrad {Mo:5d}x{N:5d} K={R} st={st} dW {digest(dw)} db {digest(db)}")
+    # the L = 256 attention kernels (dropout 0.1, regenerated masks and exported bits)
+    B, L = 64, 256
+    qkv = (rn(B, L, 2304) * 2).to(dt)
+    dout = rn(B, L, 768).to(dt)
+    s = torch.cuda.current_stream().cuda_stream
+    for use_bits in (False, True):
+        out = torch.empty(B, L, 768, device=dev, dtype=dt)
+        lse = torch.empty(B, 12, L, device=dev)
+        dqkv = torch.empty_like(qkv)
+        bits = torch.zeros(B * 12 * L * L // 32, device=dev, dtype=torch.int32) if use_bits else None
+        bp = bits.data_ptr() if use_bits else None
+        _lib.call("eegf_attn_fwd", _lib.BF16, B, 12, L, qkv.data_ptr(), 2304, None, 0.125, 0.1, 7, 3, out.data_ptr(), 768,
+                  lse.data_ptr(), bp, s)
+        _lib.call("eegf_attn_bwd", _lib.BF16, B, 12, L, qkv.data_ptr(), 2304, None, 0.125, 0.1, 7, 3, out.data_ptr(),
+                  dout.data_ptr(), 768, lse.data_ptr(), bp, dqkv.data_ptr(), None, s)
+        torch.cuda.synchronize()
+        print(f"attn  bits={int(use_bits)} out {digest(out)} lse {digest(lse)} dqkv {digest(dqkv)}"
+              + (f" keep {digest(bits)}" if use_bits else ""))
 
 
 if __name__ == "__main__":
