@@ -530,8 +530,12 @@ extern "C" int eegf_ln_fwd(int dtype, long rows, int width, const void* x, const
 }
 
 extern "C" long eegf_ln_bwd_partial_rows(long rows) {
-  // rows per block of eegf_ln_bwd: partial buffers hold ceil(rows / this) x width floats
-  return rows >= 65536 ? g_ln_bwd_rpb : 64;
+  // rows per block of eegf_ln_bwd: partial buffers hold ceil(rows / this) x width floats.  Below 65536
+  // rows about 256 blocks (a multiple of 4 rows, 4 .. 64): the decoder's 256-row LayerNorms ran 4 blocks
+  // of 64 rows, 16 waves on the whole chip (25.5 us each, 9 per step; profiles/r5zh_kernel_stats.md)
+  if (rows >= 65536) return g_ln_bwd_rpb;
+  const long r = (rows / 256 + 3) / 4 * 4;
+  return r < 4 ? 4 : r > 64 ? 64 : r;
 }
 
 extern "C" int eegf_ln_bwd(int dtype, long rows, int width, const void* dy, const void* s, const float* mean,

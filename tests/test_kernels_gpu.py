@@ -87,7 +87,8 @@ def test_layernorm_fwd_bwd(dt, mode):
         dy = torch.randn(R, W, device="cuda").to(dt)
         out.backward(dy.double())
         dx = torch.empty_like(x)
-        nb = (R + 63) // 64
+        rpb = L.lib().eegf_ln_bwd_partial_rows(R)          # the ABI's block size (include/eegfusion.h)
+        nb = (R + rpb - 1) // rpb
         part = torch.empty(2, nb, W, device="cuda")
         L.call("eegf_ln_bwd", _code(dt), R, W, dy.data_ptr(), s.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
                g.data_ptr(), 0.0, 0, 0, 0, dx.data_ptr(), None, part[0].data_ptr(), part[1].data_ptr(), _s())
