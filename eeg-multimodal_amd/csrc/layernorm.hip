@@ -396,18 +396,33 @@ __global__ void __launch_bounds__(256) colsum_scalar(const T* __restrict__ in, l
   ws[(long)blockIdx.y * width + c] = acc;
 }
 
-__global__ void __launch_bounds__(256) colsum_combine(const float* __restrict__ ws, int chunks, int width,
-                                                      float* __restrict__ out, float beta) {
-  __shared__ float red[4][64];
+// 16 waves per 64-column block, each summing chunks k = wave (mod 16) with 8 loads in flight (one
+// load per memory round trip before: the 1,024-chunk combine of a 65,536-row bias gradient took 65 us
+// for 3 MB on 12 workgroups); the 16 wave sums are added in a fixed order (deterministic)
+constexpr int CW = 16;
+__global__ void __launch_bounds__(64 * CW) colsum_combine(const float* __restrict__ ws, int chunks, int width,
+                                                          float* __restrict__ out, float beta) {
+  __shared__ float red[CW][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
   float acc = 0.f;
-  if (c < width)
-    for (int k = wave; k < chunks; k += 4) acc += ws[(long)k * width + c];
+  if (c < width) {
+    int k = wave;
+    for (; k + 7 * CW < chunks; k += 8 * CW) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = ws[(long)(k + u * CW) * width + c];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; k < chunks; k += CW) acc += ws[(long)k * width + c];
+  }
   red[wave][lane] = acc;
   __syncthreads();
   if (wave == 0 && c < width) {
-    const float v = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    float v = red[0][lane];
+#pragma unroll
+    for (int w = 1; w < CW; ++w) v += red[w][lane];
     out[c] = beta != 0.f ? v + beta * out[c] : v;
   }
 }
@@ -430,7 +445,7 @@ int colsum_t(const void* in, long ld, long rows, int width, int period, float* w
   chunks = (rows + rpc - 1) / rpc;
   if (vec) hipLaunchKernelGGL(colsum_chunks<T>, dim3(xblocks, (unsigned)chunks), dim3(256), 0, st, (const T*)in, ld, rows, width, rpc, ws);
   else hipLaunchKernelGGL(colsum_scalar<T>, dim3(xblocks, (unsigned)chunks), dim3(256), 0, st, (const T*)in, ld, rows, width, rpc, ws);
-  hipLaunchKernelGGL(colsum_combine, dim3((width + 63) / 64), dim3(256), 0, st, ws, (int)chunks, width, out, beta);
+  hipLaunchKernelGGL(colsum_combine, dim3((width + 63) / 64), dim3(64 * CW), 0, st, ws, (int)chunks, width, out, beta);
   return (int)hipGetLastError();
 }
 
