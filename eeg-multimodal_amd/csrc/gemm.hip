@@ -190,7 +190,8 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmArgs g) {
 
   // ---- epilogue ----
   if (g.ksplit > 0) {                    // split-K: raw fp32 partial slab, reduced by gemm_splitk_reduce
-    float* slab = (float*)g.C + (long)blockIdx.z * g.M * g.N;
+    // slabs [split][batch][M][N] (batched split-K: plain GEMMs only, gemm_splitk_reduce_batched)
+    float* slab = (float*)g.C + ((long)blockIdx.z * gridDim.y + z) * g.M * g.N;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const int m = m0 + wm * WT + i * 16 + (lane & 15);
@@ -375,6 +376,23 @@ __global__ void __launch_bounds__(256) gemm_splitk_reduce(const float* __restric
   *c = from_f32<TO>(v);
 }
 
+// the batched plain form: C[b] = sum_s slab[s][b] + beta C[b] (C[b] at C + b strideC, row stride ldc),
+// the same fixed summation order
+template <typename TO>
+__global__ void __launch_bounds__(256) gemm_splitk_reduce_batched(const float* __restrict__ slabs, int splits, int batch,
+                                                                  int M, int N, TO* C, long ldc, long strideC,
+                                                                  float beta) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  const long mn = (long)M * N, total = mn * batch;
+  if (e >= total) return;
+  float v = 0.f;
+  for (int s = 0; s < splits; ++s) v += slabs[(long)s * total + e];
+  const long b = e / mn, r = e % mn, m = r / N, n = r % N;
+  TO* c = C + b * strideC + m * ldc + n;
+  if (beta != 0.f) v += beta * to_f32(*c);
+  *c = from_f32<TO>(v);
+}
+
 template <typename TO>
 int splitk_reduce_t(int epi, const float* ws, int splits, int M, int N, void* C, long ldc, float beta,
                     const float* bias, void* aux, long ldaux, float scale, hipStream_t st) {
@@ -502,6 +520,35 @@ static int gemm_impl(int dtype, int out_dtype, int a_kcontig, int b_kcontig, int
   // batch-row GEMMs; the fixed-order slab reduction applies the epilogue.
   if (((M + BM - 1) / BM) * ((N + BN - 1) / BN) * batch < 192) a.bt = 64;
   const int tiles = ((M + a.bt - 1) / a.bt) * ((N + a.bt - 1) / a.bt);
+  if (batch > 1 && epi == EPI_NONE && workspace && tiles * batch <= 256 && K >= 512) {
+    // batched plain GEMMs on an under-filled grid (the decoder's per-head dq = dqp Wk_h, 48 workgroups
+    // over K = 768 took 28 us): split K as for the batch-row GEMMs, slabs [split][batch][M][N]
+    const int kt = dtype == EEGF_F32 ? 32 : 64;
+    const int min_slice = dtype == EEGF_F32 ? 128 : 256;
+    int splits = 1;
+    while (splits * tiles * batch < 512 && K / (splits * 2) >= min_slice) splits *= 2;
+    while (splits > 1 && (long)splits * batch * M * N * 4 > ws_bytes) splits /= 2;
+    if (splits > 1) {
+      int ks = (K + splits - 1) / splits;
+      ks = (ks + kt - 1) / kt * kt;
+      splits = (K + ks - 1) / ks;
+      GemmArgs b = a;
+      b.C = workspace; b.ksplit = ks; b.alpha = alpha;
+      int st;
+      if (dtype == EEGF_F32) {
+        if (out_dtype != EEGF_F32) return EEGF_ERR_ARG;
+        st = a_kcontig && b_kcontig ? launch<float, true, true, float, EPI_NONE>(b, batch, stream, splits)
+           : a_kcontig ? launch<float, true, false, float, EPI_NONE>(b, batch, stream, splits)
+           : b_kcontig ? launch<float, false, true, float, EPI_NONE>(b, batch, stream, splits)
+                       : launch<float, false, false, float, EPI_NONE>(b, batch, stream, splits);
+        if (st) return st;
+        const dim3 grid((unsigned)(((long)batch * M * N + 255) / 256));
+        hipLaunchKernelGGL(gemm_splitk_reduce_batched<float>, grid, dim3(256), 0, stream, (const float*)workspace,
+                           splits, batch, M, N, (float*)C, ldc, strideC, beta);
+        return (int)hipGetLastError();
+      }
+    }
+  }
   if (batch == 1 && workspace && tiles < 512 && (K >= 4096 || (tiles <= 256 && K >= 512))) {
     const int kt = dtype == EEGF_F32 ? 32 : 64;
     int splits = 1;

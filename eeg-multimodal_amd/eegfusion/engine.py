@@ -179,7 +179,8 @@ class FusionEngine:
 
     def gemm(self, A, B, C, M, N, K, a_kc, b_kc, lda, ldb, ldc, epi=_lib.EPI_NONE, bias=None, aux=None, ldaux=0,
              alpha=1.0, beta=0.0, scale=1.0, batch=1, sA=0, sB=0, sC=0, sAux=0, sBias=0):
-        ws = self.ws.get("splitk", SPLITK_WS, torch.float32) if batch == 1 else None
+        # batched plain GEMMs split K too (eegf_gemm: the decoder's per-head products on under-filled grids)
+        ws = self.ws.get("splitk", SPLITK_WS, torch.float32) if batch == 1 or epi == _lib.EPI_NONE else None
         call("eegf_gemm", _code(A), _code(C), a_kc, b_kc, epi, M, N, K, batch,
              P(A), lda, sA, P(B), ldb, sB, P(C), ldc, sC, P(bias), sBias, P(aux), ldaux, sAux,
              float(alpha), float(beta), float(scale), P(ws), (ws.numel() * 4 if ws is not None else 0), _stream())

@@ -139,6 +139,28 @@ def test_gemm_wgrad_beta_and_batch(dt):
     _check(C, A.double() @ B.double().transpose(1, 2), dt)
 
 
+@pytest.mark.parametrize("akc,bkc", [(1, 1), (1, 0), (0, 1), (0, 0)])
+@pytest.mark.parametrize("beta", [0.0, 1.0])
+def test_gemm_batched_splitk(akc, bkc, beta):
+    """Batched plain fp32 GEMMs on an under-filled grid split K (slabs [split][batch][M][N] and a batched
+    fixed-order reduction): the decoder's per-head dq[b, h 64 + i] = sum_c dqp[b, h, c] Wk[h 64 + i, c],
+    C batches as column blocks of one row-major matrix (strideC = 64, ldc = 768)."""
+    k = _k()
+    torch.manual_seed(9)
+    Z, M, N, K = 12, 256, 64, 768
+    A = torch.randn(Z, M, K, device="cuda") if akc else torch.randn(Z, K, M, device="cuda")
+    B = torch.randn(Z, N, K, device="cuda") if bkc else torch.randn(Z, K, N, device="cuda")
+    C = torch.randn(M, Z * N, device="cuda")
+    ref = (A.double() if akc else A.double().transpose(1, 2)) @ (B.double().transpose(1, 2) if bkc else B.double())
+    ref = ref.permute(1, 0, 2).reshape(M, Z * N) + beta * C.double()
+    ws = torch.empty(16 << 20, device="cuda")
+    k.gemm(A, B, C, M=M, N=N, K=K, a_kc=akc, b_kc=bkc, lda=K if akc else M, ldb=K if bkc else N, ldc=Z * N,
+           beta=beta, batch=Z, sA=M * K, sB=N * K, sC=N, workspace=ws)
+    torch.cuda.synchronize()
+    err = ((C.double() - ref).abs().max() / ref.abs().max()).item()
+    assert err <= 1e-5, err
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("M,N,K", [(768, 768, 16384), (2304, 768, 8192), (300, 200, 9000)])
 def test_gemm_wgrad_splitk(dt, M, N, K):
