@@ -20,6 +20,9 @@
 #include "common.h"
 #include "eegfusion_internal.h"
 
+// eegf_tune key 19: the bf16-memory backward on xbwd_mfma_kernel (1, default) or the VALU xbwd_cols_kernel (0)
+int g_xbwd_mfma = 1;
+
 namespace {
 
 constexpr int E = 768, NH = 12, SLAB = 256;
@@ -311,6 +314,121 @@ __global__ void __launch_bounds__(512) xbwd_cols_kernel(const T* __restrict__ me
   }
 }
 
+// The same backward on the fp32 MFMA for a bf16 memory (v_mfma_f32_16x16x4_f32: fp32 products, fp32
+// sums, as the VALU kernel above).  grid (E/256, B), 4 waves; wave w owns the 64 columns
+// cbase = 256 slab + 64 w of every memory row, as four interleaved 16-column tiles q (MFMA row m <->
+// column cbase + 4 m + q), so one 8-B load of M[j][cbase + 4 li ..] feeds all four tiles and the four
+// tiles' accumulators hold 16 consecutive columns of one row:
+//   dM^T[c][j] = sum_k B2[k][c] A2[j][k],  k < 24: A2 = [p~ | dsc] (LDS a2[j][k]), B2 = [dc ; q'] rows
+//   dq'^T[c][h] = sum_j M[j][c] dsc[h][j]
+// The softmax backward (the prologue) is the VALU kernel's.  Rows j >= S are zero in a2 (their M loads
+// clamp to row S - 1 and contribute 0).  VALU kernel at B = 256, S = 256: 130 us per launch, 2.4 TB/s.
+constexpr int A2LD = 25;     // a2 row stride (floats): 24 used
+template <typename TQ>
+__global__ void __launch_bounds__(256) xbwd_mfma_kernel(const bf16* __restrict__ mem, const TQ* __restrict__ qp,
+                                                        const float* __restrict__ probs, const float* __restrict__ raw,
+                                                        const float* __restrict__ dpsum, const TQ* __restrict__ dc, int S,
+                                                        float p_drop, uint64_t seed, uint64_t offset,
+                                                        bf16* __restrict__ dmem, float beta, TQ* __restrict__ dqp) {
+  extern __shared__ __attribute__((aligned(16))) float a2[];        // [Spad][A2LD]
+  const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, li = lane & 15;
+  const int Spad = (S + 15) & ~15;
+  for (int h = wave; h < NH; h += 4) {
+    const float* pr = probs + ((long)b * NH + h) * S;
+    const float* dr = raw + ((long)b * NH + h) * S;
+    const float dsh = dpsum ? dpsum[b * NH + h] : 0.f;
+    float dot = 0.f;
+    for (int j = lane; j < S; j += 64) {
+      const float mk = p_drop > 0.f ? drop_mask1(seed, offset, ((uint64_t)b * NH + h) * S + j, p_drop) : 1.f;
+      const float p = pr[j], dp = (dr[j] + dsh) * mk;
+      a2[j * A2LD + h] = p * mk;
+      a2[j * A2LD + NH + h] = dp;
+      dot += p * dp;
+    }
+    dot = wave_sum(dot);
+    for (int j = lane; j < S; j += 64) a2[j * A2LD + NH + h] = pr[j] * (a2[j * A2LD + NH + h] - dot);
+  }
+  for (int i = S * A2LD + tid; i < Spad * A2LD; i += 256) a2[i] = 0.f;
+  __syncthreads();
+  const int cbase = blockIdx.x * SLAB + 64 * wave;
+  // B2 rows k = g + 4 t (t < 6): columns cbase + 4 li + q -> bq[t][q]
+  float bq[6][4];
+#pragma unroll
+  for (int t = 0; t < 6; ++t) {
+    const int k = g + 4 * t;
+    const TQ* src = k < NH ? dc + ((long)b * NH + k) * E : qp + ((long)b * NH + k - NH) * E;
+    load4<TQ>(src + cbase + 4 * li, bq[t]);
+  }
+  const bf16* Mb = mem + (long)b * S * E + cbase + 4 * li;
+  bf16* dMb = dmem + (long)b * S * E + cbase + 16 * g;
+  f32x4 acc1[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) acc1[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // per 16-row tile: M rows jb + 4 t + g (t < 4) as 8-B loads; the old dM row jb + li as two 16-B loads
+  auto load_tile = [&](int jb, bf16x4 (&m)[4], bf16x8 (&o)[2]) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) m[t] = *(const bf16x4*)(Mb + (long)min(jb + 4 * t + g, S - 1) * E);
+    if (beta != 0.f) {
+      const bf16* src = dMb + (long)min(jb + li, S - 1) * E;
+      o[0] = *(const bf16x8*)src;
+      o[1] = *(const bf16x8*)(src + 8);
+    }
+  };
+  bf16x4 mc[4], mn[4];
+  bf16x8 oc[2], on[2];
+  load_tile(0, mc, oc);
+  for (int jb = 0; jb < Spad; jb += 16) {
+    if (jb + 16 < Spad) load_tile(jb + 16, mn, on);
+    // dq': k = rows jb + 4 t + g, n = head li
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float dv = li < NH ? a2[(jb + 4 * t + g) * A2LD + NH + li] : 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc1[q] = __builtin_amdgcn_mfma_f32_16x16x4f32((float)mc[t][q], dv, acc1[q], 0, 0, 0);
+    }
+    // dM: k = g + 4 t, n = row jb + li
+    f32x4 acc2[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc2[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 6; ++t) {
+      const float av = a2[(jb + li) * A2LD + g + 4 * t];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc2[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(bq[t][q], av, acc2[q], 0, 0, 0);
+    }
+    // acc2[q][r] = dM[jb + li][cbase + 16 g + 4 r + q]
+    if (jb + li < S) {
+      bf16x8 v[2];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float x = acc2[q][r];
+          if (beta != 0.f) x += beta * (float)oc[r >> 1][4 * (r & 1) + q];
+          v[r >> 1][4 * (r & 1) + q] = (bf16)x;
+        }
+      bf16* dst = dMb + (long)(jb + li) * E;
+      *(bf16x8*)dst = v[0];
+      *(bf16x8*)(dst + 8) = v[1];
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) mc[t] = mn[t];
+    oc[0] = on[0];
+    oc[1] = on[1];
+  }
+  // acc1[q][r] = dq'[h = li][cbase + 16 g + 4 r + q]
+  if (li < NH) {
+    TQ* dst = dqp + ((long)b * NH + li) * E + cbase + 16 * g;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = acc1[q][r];
+      store4<TQ>(dst + 4 * r, v);
+    }
+  }
+}
+
 // x[b, c] += bias[c] * s[b, c / group]   (the s_h bv_h term of the dropped-out context)
 __global__ void __launch_bounds__(256) head_bias_fwd_kernel(int B, int W, int group, float* __restrict__ x,
                                                             const float* __restrict__ bias, const float* __restrict__ s) {
@@ -361,6 +479,15 @@ template <typename T, typename TQ>
 int xbwd(int B, int S, const void* mem, const void* qp, const float* probs, const float* dpsum, const void* dctx,
          float p, uint64_t seed, uint64_t off, float* ws, void* dmem, float beta, void* dqp, hipStream_t st) {
   launch_xrow_dot<T, TQ>((const T*)mem, (const TQ*)dctx, (const float*)nullptr, B, S, ws, st);
+  if constexpr (sizeof(T) == 2) {
+    if (g_xbwd_mfma) {
+      const size_t lds = sizeof(float) * (size_t)((S + 15) & ~15) * A2LD;
+      hipFuncSetAttribute((const void*)xbwd_mfma_kernel<TQ>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL((xbwd_mfma_kernel<TQ>), dim3(E / SLAB, B), dim3(256), lds, st, (const bf16*)mem,
+                         (const TQ*)qp, probs, ws, dpsum, (const TQ*)dctx, S, p, seed, off, (bf16*)dmem, beta, (TQ*)dqp);
+      return (int)hipGetLastError();
+    }
+  }
   const size_t lds = sizeof(float) * ((size_t)2 * S * NH + 4 * NH * SLAB);
   hipFuncSetAttribute((const void*)xbwd_cols_kernel<T, TQ>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL((xbwd_cols_kernel<T, TQ>), dim3(E / SLAB, B), dim3(512), lds, st, (const T*)mem, (const TQ*)qp,

@@ -2424,7 +2424,9 @@ extern "C" int eegf_gemm_big_timestamps(long long* buf) {
   return 0;
 }
 
+extern int g_xbwd_mfma;   // decoder.hip
 extern "C" int eegf_tune(int key, int value) {
+  if (key == 19) { const int o = g_xbwd_mfma; if (value < 0 || value > 1) return EEGF_ERR_ARG; g_xbwd_mfma = value; return o; }
   if (key == 1) {
     if (value != -1 && value != 0 && value != 4 && value != 6) return EEGF_ERR_ARG;
     const int o = g_gemm8;

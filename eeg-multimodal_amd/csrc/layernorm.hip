@@ -477,11 +477,33 @@ int ln_bwd_t(int nch, const LnBwdArgs& a, hipStream_t st) {
 
 // ---- batched column sums: many small independent reductions in one launch ----
 // Descriptor (6 x int64): src, dst, ld, rows, width | dtype << 32, float_bits(beta) | first_block << 32.
-// Block b serves the descriptor whose block range holds b: 64 columns, 4 waves over contiguous row
-// quarters, combined in a fixed order (bitwise reproducible); dst[c] = sum + beta * dst[c].
+// Block b serves the descriptor whose block range holds b: 64 columns.  Thread t sums the 4 columns
+// 4 (t & 15) .. of the rows r = t >> 4 (mod 16) with one 16-B (fp32) / 8-B (bf16) load per row, 4 rows in
+// flight; the 16 row-group partials are combined in a fixed order (bitwise reproducible); dst[c] = sum +
+// beta * dst[c].  Descriptors whose base, row stride or width are not 4-element aligned take the
+// one-column-per-lane form.  (The 1-column form held ~2.3 TB/s on the 1,165-block batch of the bench
+// step's LayerNorm / bias partials: 130 us, profiles/r5zh_kernel_stats.md.)
+template <typename T>
+DEV void colsum_rows4(const T* p, long ld, long rows, int rg, float (&acc)[4]) {
+  long r = rg;
+  for (; r + 48 < rows; r += 64) {
+    f32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = V4<T>::load(p + (r + 16 * u) * ld);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[e] += v[u][e];
+  }
+  for (; r < rows; r += 16) {
+    const f32x4 v = V4<T>::load(p + r * ld);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc[e] += v[e];
+  }
+}
 __global__ void __launch_bounds__(256) colsum_batch_kernel(const long long* __restrict__ desc, int n) {
-  __shared__ float red[4][64];
-  const int blk = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __shared__ float red[16][65];
+  const int blk = blockIdx.x, tid = threadIdx.x;
   int d = 0;
   for (int i = 1; i < n; ++i) {
     if ((int)(desc[6 * i + 5] >> 32) <= blk) d = i;
@@ -491,23 +513,39 @@ __global__ void __launch_bounds__(256) colsum_batch_kernel(const long long* __re
   const long ld = D[2], rows = D[3];
   const int width = (int)(D[4] & 0xffffffffLL), dtype = (int)(D[4] >> 32);
   const float beta = __int_as_float((int)(D[5] & 0xffffffffLL));
-  const int c = (blk - (int)(D[5] >> 32)) * 64 + lane;
-  const long r0 = rows * wave / 4, r1 = rows * (wave + 1) / 4;
-  float acc = 0.f;
-  if (c < width) {
-    if (dtype == EEGF_BF16) {
-      const bf16* p = (const bf16*)D[0] + c;
-      for (long r = r0; r < r1; ++r) acc += (float)p[r * ld];
-    } else {
-      const float* p = (const float*)D[0] + c;
-      for (long r = r0; r < r1; ++r) acc += p[r * ld];
+  const int c0 = (blk - (int)(D[5] >> 32)) * 64;
+  const int esz = dtype == EEGF_BF16 ? 2 : 4;
+  const bool vec = ((D[0] | (ld * esz)) & (4L * esz - 1)) == 0 && (width & 3) == 0;
+  if (vec) {
+    const int cq = tid & 15, rg = tid >> 4, c = c0 + 4 * cq;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    if (c < width) {
+      if (dtype == EEGF_BF16) colsum_rows4((const bf16*)D[0] + c, ld, rows, rg, acc);
+      else colsum_rows4((const float*)D[0] + c, ld, rows, rg, acc);
     }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) red[rg][4 * cq + e] = acc[e];
+  } else {
+    const int lane = tid & 63, wave = tid >> 6, c = c0 + lane;
+    const long r0 = rows * wave / 4, r1 = rows * (wave + 1) / 4;
+    float acc = 0.f;
+    if (c < width) {
+      if (dtype == EEGF_BF16) {
+        const bf16* p = (const bf16*)D[0] + c;
+        for (long r = r0; r < r1; ++r) acc += (float)p[r * ld];
+      } else {
+        const float* p = (const float*)D[0] + c;
+        for (long r = r0; r < r1; ++r) acc += p[r * ld];
+      }
+    }
+    red[wave][lane] = acc;
   }
-  red[wave][lane] = acc;
   __syncthreads();
-  if (wave == 0 && c < width) {
+  if (tid < 64 && c0 + tid < width) {
+    const int c = c0 + tid, ng = vec ? 16 : 4;
+    float v = 0.f;
+    for (int i = 0; i < ng; ++i) v += red[i][tid];
     float* dst = (float*)D[1];
-    const float v = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
     dst[c] = beta != 0.f ? v + beta * dst[c] : v;
   }
 }

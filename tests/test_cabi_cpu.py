@@ -41,17 +41,18 @@ def test_argument_errors_return_status_without_gpu():
 
 def test_tune_routing_keys_validate_and_restore_without_gpu():
     """eegf_tune is host state only: the GEMM routing keys report the production defaults (key 11 = 1
-    persistent GEMM, key 14 = 2 gemm4q for every eligible shape), refuse out-of-range values with
+    persistent GEMM, key 14 = 2 gemm4q for every eligible shape, key 19 = 1 the MFMA cross-attention
+    backward), refuse out-of-range values with
     EEGF_ERR_ARG and return the previous value when set."""
     import os
 
     from eegfusion import _lib
     lib = _lib.lib()
     lib.eegf_tune.argtypes = [_lib.i32, _lib.i32]
-    for key, default, hi in ((11, 1, 3), (14, 2, 2)):
-        env = {11: "EEGF_GEMM4P", 14: "EEGF_GEMM4Q"}[key]
+    for key, default, hi in ((11, 1, 3), (14, 2, 2), (19, 1, 1)):
+        env = {11: "EEGF_GEMM4P", 14: "EEGF_GEMM4Q"}.get(key, "")
         old = lib.eegf_tune(key, default)
-        if env not in os.environ:
+        if not env or env not in os.environ:
             assert old == default, (key, old)
         assert lib.eegf_tune(key, hi + 1) == _lib.ERR_ARG
         assert lib.eegf_tune(key, -1) == _lib.ERR_ARG

@@ -334,6 +334,59 @@ def test_xattn_fwd_bwd(dt, S, pdrop, masked):
     assert _rel(dqp, q.grad) < _tol(dt) * 3
 
 
+@pytest.mark.parametrize("S,pdrop,beta", [(256, 0.1, 1.0), (256, 0.0, 0.0), (100, 0.2, 1.0), (300, 0.0, 1.0), (7, 0.3, 0.0)])
+def test_xattn_bwd_mixed_mfma(S, pdrop, beta):
+    """The engine's cross-attention backward (bf16 memory, fp32 query / context gradient) on the fp32-MFMA
+    kernel (eegf_tune key 19 = 1) vs float64 autograd with the replayed Philox mask, and vs the VALU kernel
+    (key 19 = 0): the same fp32 products summed in another order."""
+    from philox_ref import drop_mask
+    lib = _lib()
+    torch.manual_seed(5)
+    B, seed, off = 3, 77, 5
+    mem = torch.randn(B, S, 768, device="cuda").to(torch.bfloat16)
+    qp = 0.05 * torch.randn(B, 12, 768, device="cuda")
+    probs = torch.empty(B, 12, S, device="cuda")
+    psum = torch.empty(B, 12, device="cuda")
+    cc = torch.empty(B, 12, 768, device="cuda")
+    ws = torch.empty(B * 12 * S, device="cuda")
+    lib.call("eegf_xattn_fwd", 1, 0, B, S, mem.data_ptr(), qp.data_ptr(), None, pdrop, seed, off, ws.data_ptr(),
+             probs.data_ptr(), psum.data_ptr(), cc.data_ptr(), _s())
+    torch.cuda.synchronize()
+    m = mem.double().clone().requires_grad_()
+    q = qp.double().clone().requires_grad_()
+    p = torch.einsum("bhc,bjc->bhj", q, m).softmax(-1)
+    z = torch.ones_like(p)
+    if pdrop > 0:
+        z = torch.from_numpy(drop_mask(seed, off, torch.arange(B * 12 * S).numpy(), pdrop)).view(B, 12, S).cuda()
+    pt = p * z
+    c = torch.einsum("bhj,bjc->bhc", pt, m)
+    dc = torch.randn(B, 12, 768, device="cuda")
+    dps = torch.randn(B, 12, device="cuda")
+    (c * dc.double()).sum().add((pt.sum(-1) * dps.double()).sum() if pdrop > 0 else 0.0).backward()
+    dmem0 = torch.randn_like(mem)
+    out = {}
+    for key in (1, 0):
+        tune = lib.lib().eegf_tune
+        tune.argtypes = [lib.i32, lib.i32]
+        old = tune(19, key)
+        try:
+            dmem = dmem0.clone()
+            dqp = torch.empty_like(qp)
+            lib.call("eegf_xattn_bwd", 1, 0, B, S, mem.data_ptr(), qp.data_ptr(), probs.data_ptr(),
+                     dps.data_ptr() if pdrop > 0 else None, dc.data_ptr(), pdrop, seed, off, ws.data_ptr(),
+                     dmem.data_ptr(), beta, dqp.data_ptr(), _s())
+            torch.cuda.synchronize()
+        finally:
+            tune(19, old)
+        out[key] = (dmem, dqp)
+    for key, (dmem, dqp) in out.items():
+        ref_m = m.grad + beta * dmem0.double()
+        assert _rel(dmem, ref_m) < 1e-2, key                 # bf16 output: one rounding
+        assert _rel(dqp, q.grad) < 1e-5, key                 # fp32 output
+    assert _rel(out[1][1], out[0][1]) < 1e-5
+    assert (out[1][0].double() - out[0][0].double()).abs().max() <= 2 * 2.0 ** -8 * out[0][0].double().abs().max()
+
+
 def test_head_bias_fwd_bwd():
     lib = _lib()
     torch.manual_seed(4)
@@ -551,7 +604,10 @@ def test_colsum_batch():
     lib = _lib()
     torch.manual_seed(21)
     specs = [(torch.float32, 1024, 768, 768), (torch.bfloat16, 256, 2304, 2304), (torch.float32, 37, 100, 130),
-             (torch.bfloat16, 5, 1, 8), (torch.float32, 256, 2, 2)]
+             (torch.bfloat16, 5, 1, 8), (torch.float32, 256, 2, 2),
+             # 4-column vector form: ragged row counts (tails of the 64-row unroll), partial last block
+             (torch.float32, 37, 100, 128), (torch.float32, 8192, 72, 72), (torch.bfloat16, 1000, 300, 304),
+             (torch.bfloat16, 70, 6, 8)]
     srcs, dsts, refs, rows_d, blk = [], [], [], [], 0
     one = struct.unpack("<i", struct.pack("<f", 1.0))[0]
     for dt, rows, width, ld in specs:
