@@ -16,11 +16,13 @@
 //              scores), dropout, then c[h, cols] = sum_j p~[h][j] M[j][cols]; 4 waves split j
 //   xbwd_cols  per (b, 256-column slab): softmax backward, then in one pass over M:
 //              dq'[h, cols] = sum_j dsc[h][j] M[j][cols],  dM[j][cols] = sum_h p~ dc + dsc q'
+//   xctx_mfma / xbwd_mfma  the same two for a bf16 memory on v_mfma_f32_16x16x4_f32 (the bench path)
 // The q'/Wv/out-proj GEMMs are eegf_gemm; the s_h bv_h term is eegf_head_bias_fwd/bwd.
 #include "common.h"
 #include "eegfusion_internal.h"
 
-// eegf_tune key 19: the bf16-memory backward on xbwd_mfma_kernel (1, default) or the VALU xbwd_cols_kernel (0)
+// eegf_tune key 19: the bf16-memory context and backward on xctx_mfma_kernel / xbwd_mfma_kernel (1,
+// default) or the VALU xctx_kernel / xbwd_cols_kernel (0)
 int g_xbwd_mfma = 1;
 
 namespace {
@@ -108,12 +110,34 @@ __global__ void __launch_bounds__(64 * XW) xrow_dot_mfma_kernel(const bf16* __re
   constexpr int LDV = E + 8;
   __shared__ __attribute__((aligned(16))) bf16 vt[2][16 * LDV];
   const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, li = lane & 15;
-  for (int i = tid; i < 16 * E; i += 64 * XW) {
-    const int h = i / E, c = i % E;
-    const float x = h < NH ? to_f32(vec[((long)b * NH + h) * E + c]) : 0.f;
-    const bf16 hi = (bf16)x;
-    vt[0][h * LDV + c] = hi;
-    vt[1][h * LDV + c] = (bf16)(x - (float)hi);
+  // 4 consecutive elements per thread and every load of the loop issued before the first LDS store (one
+  // load latency: the element-per-thread loop waited for each of its 24 loads in turn)
+  constexpr int NV = 16 * E / 4 / (64 * XW);
+  static_assert(NV * 4 * 64 * XW == 16 * E, "v staging covers 16 x 768");
+  float4 xv[NV];
+#pragma unroll
+  for (int u = 0; u < NV; ++u) {
+    const int i = 4 * (tid + u * 64 * XW), h = i / E, c = i % E;
+    if (h < NH) {
+      float t[4];
+      load4<TV>(vec + ((long)b * NH + h) * E + c, t);
+      xv[u] = float4{t[0], t[1], t[2], t[3]};
+    } else {
+      xv[u] = float4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < NV; ++u) {
+    const int i = 4 * (tid + u * 64 * XW), h = i / E, c = i % E;
+    const float x[4] = {xv[u].x, xv[u].y, xv[u].z, xv[u].w};
+    bf16x4 hi, lo;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      hi[e] = (bf16)x[e];
+      lo[e] = (bf16)(x[e] - (float)hi[e]);
+    }
+    *(bf16x4*)(vt[0] + h * LDV + c) = hi;
+    *(bf16x4*)(vt[1] + h * LDV + c) = lo;
   }
   __syncthreads();
   const bf16* vh = vt[0] + li * LDV + 8 * g;
@@ -155,13 +179,18 @@ DEV void softmax_rows(const float* __restrict__ raw, int S, int b, float p_drop,
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   for (int h = wave; h < NH; h += nw) {
     const float* r = raw + ((long)b * NH + h) * S;
+    // loops unrolled by 4: their independent loads issue together (the 1-by-1 loops waited for every
+    // load in turn: ~24 dependent L2 round trips per workgroup before the first memory row)
     float mx = -3.0e38f;
+#pragma unroll 4
     for (int j = lane; j < S; j += 64) mx = fmaxf(mx, r[j]);
     mx = wave_max(mx);
     float sum = 0.f;
+#pragma unroll 4
     for (int j = lane; j < S; j += 64) { const float e = __expf(r[j] - mx); pt[j * NH + h] = e; sum += e; }
     const float inv = 1.0f / wave_sum(sum);
     float ds = 0.f;
+#pragma unroll 4
     for (int j = lane; j < S; j += 64) {
       const float p = pt[j * NH + h] * inv;
       if (write) probs[((long)b * NH + h) * S + j] = p;
@@ -241,6 +270,56 @@ __global__ void __launch_bounds__(512) xctx_kernel(const T* __restrict__ mem, co
   for (int i = tid; i < NH * SLAB; i += 512) {
     const int h = i / SLAB, c = i % SLAB;
     ctx[((long)b * NH + h) * E + blockIdx.x * SLAB + c] = from_f32<TQ>(red4(red, h, c));
+  }
+}
+
+// The context on the fp32 MFMA for a bf16 memory: grid (E/256, B), 4 waves, the column layout of
+// xbwd_mfma_kernel below (wave w: columns 256 slab + 64 w as four interleaved 16-column tiles):
+// ctx^T[c][h] = sum_j M[j][c] p~[h][j] as v_mfma_f32_16x16x4_f32 (fp32 products and sums, as xctx_kernel).
+// xctx_kernel at B = 256, S = 256: 37.9 us per launch, 2.6 TB/s (profiles/r5zm_kernel_stats.md).
+template <typename TQ>
+__global__ void __launch_bounds__(256) xctx_mfma_kernel(const bf16* __restrict__ mem, const float* __restrict__ raw, int S,
+                                                        float p_drop, uint64_t seed, uint64_t offset,
+                                                        float* __restrict__ probs, float* __restrict__ psum,
+                                                        TQ* __restrict__ ctx) {
+  extern __shared__ __attribute__((aligned(16))) float pt[];       // [Spad][12]
+  const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, li = lane & 15;
+  const int Spad = (S + 15) & ~15;
+  softmax_rows(raw, S, b, p_drop, seed, offset, blockIdx.x == 0, probs, psum, pt);
+  for (int i = S * NH + tid; i < Spad * NH; i += 256) pt[i] = 0.f;
+  __syncthreads();
+  const int cbase = blockIdx.x * SLAB + 64 * wave;
+  const bf16* Mb = mem + (long)b * S * E + cbase + 4 * li;
+  f32x4 acc[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x4 mc[4], mn[4];
+  auto load_tile = [&](int jb, bf16x4 (&m)[4]) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) m[t] = *(const bf16x4*)(Mb + (long)min(jb + 4 * t + g, S - 1) * E);
+  };
+  load_tile(0, mc);
+  for (int jb = 0; jb < Spad; jb += 16) {
+    if (jb + 16 < Spad) load_tile(jb + 16, mn);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float pv = li < NH ? pt[(jb + 4 * t + g) * NH + li] : 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32((float)mc[t][q], pv, acc[q], 0, 0, 0);
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) mc[t] = mn[t];
+  }
+  // acc[q][r] = ctx[h = li][cbase + 16 g + 4 r + q]
+  if (li < NH) {
+    TQ* dst = ctx + ((long)b * NH + li) * E + cbase + 16 * g;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = acc[q][r];
+      store4<TQ>(dst + 4 * r, v);
+    }
   }
 }
 
@@ -338,6 +417,7 @@ __global__ void __launch_bounds__(256) xbwd_mfma_kernel(const bf16* __restrict__
     const float* dr = raw + ((long)b * NH + h) * S;
     const float dsh = dpsum ? dpsum[b * NH + h] : 0.f;
     float dot = 0.f;
+#pragma unroll 4
     for (int j = lane; j < S; j += 64) {
       const float mk = p_drop > 0.f ? drop_mask1(seed, offset, ((uint64_t)b * NH + h) * S + j, p_drop) : 1.f;
       const float p = pr[j], dp = (dr[j] + dsh) * mk;
@@ -346,6 +426,7 @@ __global__ void __launch_bounds__(256) xbwd_mfma_kernel(const bf16* __restrict__
       dot += p * dp;
     }
     dot = wave_sum(dot);
+#pragma unroll 4
     for (int j = lane; j < S; j += 64) a2[j * A2LD + NH + h] = pr[j] * (a2[j * A2LD + NH + h] - dot);
   }
   for (int i = S * A2LD + tid; i < Spad * A2LD; i += 256) a2[i] = 0.f;
@@ -469,6 +550,15 @@ template <typename T, typename TQ>
 int xfwd(int B, int S, const void* mem, const void* qp, const float* kb, float p, uint64_t seed, uint64_t off,
          float* ws, float* probs, float* psum, void* ctx, hipStream_t st) {
   launch_xrow_dot<T, TQ>((const T*)mem, (const TQ*)qp, kb, B, S, ws, st);
+  if constexpr (sizeof(T) == 2) {
+    if (g_xbwd_mfma) {
+      const size_t lds = sizeof(float) * (size_t)((S + 15) & ~15) * NH;
+      hipFuncSetAttribute((const void*)xctx_mfma_kernel<TQ>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL((xctx_mfma_kernel<TQ>), dim3(E / SLAB, B), dim3(256), lds, st, (const bf16*)mem, ws, S, p,
+                         seed, off, probs, psum, (TQ*)ctx);
+      return (int)hipGetLastError();
+    }
+  }
   const size_t lds = sizeof(float) * ((size_t)S * NH + 4 * NH * SLAB);
   hipFuncSetAttribute((const void*)xctx_kernel<T, TQ>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL((xctx_kernel<T, TQ>), dim3(E / SLAB, B), dim3(512), lds, st, (const T*)mem, ws, S, p, seed, off,

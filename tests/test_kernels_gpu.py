@@ -334,6 +334,42 @@ def test_xattn_fwd_bwd(dt, S, pdrop, masked):
     assert _rel(dqp, q.grad) < _tol(dt) * 3
 
 
+@pytest.mark.parametrize("S,pdrop", [(256, 0.1), (256, 0.0), (100, 0.2), (300, 0.0), (7, 0.3)])
+def test_xattn_fwd_mixed_mfma(S, pdrop):
+    """The engine's cross-attention context (bf16 memory, fp32 query / context) on the fp32-MFMA kernel
+    (eegf_tune key 19 = 1) vs float64 with the replayed Philox mask, and vs the VALU kernel (key 19 = 0):
+    identical probabilities and s = sum p~ (same softmax code), the context within fp32 summation order."""
+    from philox_ref import drop_mask
+    lib = _lib()
+    torch.manual_seed(6)
+    B, seed, off = 3, 31, 2
+    mem = torch.randn(B, S, 768, device="cuda").to(torch.bfloat16)
+    qp = 0.05 * torch.randn(B, 12, 768, device="cuda")
+    tune = lib.lib().eegf_tune
+    tune.argtypes = [lib.i32, lib.i32]
+    out = {}
+    for key in (1, 0):
+        probs = torch.empty(B, 12, S, device="cuda")
+        psum = torch.empty(B, 12, device="cuda")
+        cc = torch.empty(B, 12, 768, device="cuda")
+        ws = torch.empty(B * 12 * S, device="cuda")
+        old = tune(19, key)
+        try:
+            lib.call("eegf_xattn_fwd", 1, 0, B, S, mem.data_ptr(), qp.data_ptr(), None, pdrop, seed, off,
+                     ws.data_ptr(), probs.data_ptr(), psum.data_ptr(), cc.data_ptr(), _s())
+            torch.cuda.synchronize()
+        finally:
+            tune(19, old)
+        out[key] = (probs, psum, cc)
+    p = torch.einsum("bhc,bjc->bhj", qp.double(), mem.double()).softmax(-1)
+    z = torch.ones_like(p)
+    if pdrop > 0:
+        z = torch.from_numpy(drop_mask(seed, off, torch.arange(B * 12 * S).numpy(), pdrop)).view(B, 12, S).cuda()
+    c = torch.einsum("bhj,bjc->bhc", p * z, mem.double())
+    assert torch.equal(out[1][0], out[0][0]) and torch.equal(out[1][1], out[0][1])
+    assert _rel(out[1][2], c) < 1e-5 and _rel(out[1][2], out[0][2]) < 1e-5
+
+
 @pytest.mark.parametrize("S,pdrop,beta", [(256, 0.1, 1.0), (256, 0.0, 0.0), (100, 0.2, 1.0), (300, 0.0, 1.0), (7, 0.3, 0.0)])
 def test_xattn_bwd_mixed_mfma(S, pdrop, beta):
     """The engine's cross-attention backward (bf16 memory, fp32 query / context gradient) on the fp32-MFMA
