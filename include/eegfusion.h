@@ -100,7 +100,10 @@ int eegf_tune(int key, int value);
  *          late; env EEGF_TILE_ORDER.
  *   key 16: the start delay of the key-15 + 32 probe.
  *   key 18: the gemm4q-eligible GEMMs on gemm4r (rolling A fragments, A / B images in 3 + 2 ring slots,
- *          bitwise the same results): 1 (default) on, 0 gemm4q; env EEGF_GEMM4R. */
+ *          bitwise the same results): 1 (default) on, 0 gemm4q; env EEGF_GEMM4R.
+ *   key 19: eegf_xattn_fwd / eegf_xattn_bwd with a bf16 memory: 1 (default) the context and the backward
+ *          on the fp32 MFMA (xctx_mfma / xbwd_mfma), 0 the VALU kernels; fp32 products and sums either
+ *          way, results equal up to summation order (tests/test_kernels_gpu.py). */
 /* Diagnostics (no reference counterpart): every following 256-row GEMM launch of the 8-wave / 4-wave
  * kernels writes 4 s_memrealtime stamps per workgroup (start, prologue done, K-loop done, epilogue
  * issued, slot 4 the CU id) into buf = int64 [grid.y][grid.x][8]; nullptr switches it off.  tools/gemm_phases.py. */
