@@ -57,7 +57,17 @@ KERNEL_GROUPS = {
     "dgrad_out": "input gradient through the attention output projection, 65536x768x768",
     "dgrad_ffn2": "input gradient through BertOutput with the GELU' product, 65536x3072x768",
     "wgrad": "weight gradients (split-K over 65536 tokens) with the bias gradients fused (row sums)",
+    # HBM-bound kernels, reported in GB/s (the gate / min-max / CE / LN /
+    # Adam kernels separately): engine.probe records their algorithmic bytes per launch
+    "fusion_fwd": "concat + row min-max + PriGumbel gate (Laplace, Gumbel-softmax, eps_hat), fp32 [B, 2304]",
+    "fusion_bwd": "its backward: min-max / gate gradients to the three encoders (+ the DP gradient rows, pass 1)",
+    "cross_entropy": "F.cross_entropy(mean) + argmax count + logit gradients, [B, 2]",
+    "ln_fwd768": "BERT hidden dropout + residual + LayerNorm forward, [65536, 768] bf16",
+    "adam": "fused Adam (+ bf16 shadow) over the used arena ranges",
 }
+HBM_TAGS = ("fusion_fwd", "fusion_bwd", "cross_entropy", "ln_fwd768", "adam")
+PEAK_HBM = 8000.0                 # GB/s HBM3E (MI355X_MICROARCH.md)
+T_ORIGIN = time.perf_counter()    # process start: the CPU-baseline budget guard counts from here
 # The kernel (rocprof symbol) each probed group runs on: the roofline object reports the SYMBOL with the
 # most time per step, combining the groups that share it, with the PMC traffic of that symbol
 # (profiles/PMC_FILE key).  Algorithmic bytes per launch: A + W + C (+ aux) of each shape, bf16.
@@ -102,12 +112,16 @@ def parse_args(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true",
                     help="no HIP-event probes in the timed loop (no per-kernel roofline; A/B of the probes' cost)")
-    ap.add_argument("--cpu-batch", type=int, default=16,
-                    help="CPU-baseline batch of the live sample (bounded: ~10-30 s of CPU work)")
+    ap.add_argument("--cpu-batch", type=int, default=256,
+                    help="CPU-baseline batch (BASELINE.md section 3: the bench's batch, 256; ~107 s per iteration "
+                         "on a GPU box's 16-CPU share)")
     ap.add_argument("--cpu-iters", type=int, default=3, help="CPU-baseline timed iterations after one warm-up")
-    ap.add_argument("--cpu-warm-batch", type=int, default=0,
+    ap.add_argument("--cpu-warm-batch", type=int, default=16,
                     help="batch of the CPU-baseline warm-up iteration (0 = --cpu-batch; the batch-256 sample "
                          "warms up at 16: thread pool and allocator, not another 2-4 minutes of page faults)")
+    ap.add_argument("--cpu-budget", type=float, default=450.0,
+                    help="seconds since process start the run may reach: the CPU leg stops after the last "
+                         "iteration whose successor would end past it (the count is stated in the line)")
     ap.add_argument("--cpu-baseline-only", action="store_true",
                     help="time only the CPU baseline (e.g. --cpu-batch 256 --cpu-iters 3, BASELINE.md §3) and print "
                          "its JSON; profiles/" + "cpu_baseline_b256.json holds that run for the bench line")
@@ -166,13 +180,15 @@ def cpu_share() -> dict:
     return {"threads": threads, "affinity": avail, "cgroup_quota": quota, "omp_num_threads": omp}
 
 
-def cpu_baseline(variant: str, batch: int, iters: int, warm_batch: int = 0) -> dict:
+def cpu_baseline(variant: str, batch: int, iters: int, warm_batch: int = 0, budget_s: float = 0.0) -> dict:
     """The CPU oracle (torch fp32 restatement, oracle/fusion_oracle.py; pinned against the reference's
     own outputs by tests/test_oracle_golden.py) timed on the host cores on a bounded sample of the
     same iteration: the bench's batch (256), dropout 0.1 at every reference site as on the GPU leg,
     PriConcat with the honoured feature_all_lap mechanism, one warm-up iteration then `iters` timed.
     Threads = the CPUs this process may run on (sched_getaffinity), capped by the cgroup quota and
-    OMP_NUM_THREADS (the GPU box's CPU share): cpu_share()."""
+    OMP_NUM_THREADS (the GPU box's CPU share): cpu_share().  budget_s > 0: stop after the last timed
+    iteration whose successor, at the mean iteration time so far, would end more than budget_s after
+    process start (at least one iteration always runs); the line states how many ran."""
     import torch
     import torch.nn.functional as F
     from oracle import fusion_oracle as O
@@ -252,21 +268,31 @@ def cpu_baseline(variant: str, batch: int, iters: int, warm_batch: int = 0) -> d
         warm = time.perf_counter() - t0
         del warm_d, warm_l
         t0 = time.perf_counter()
+        done_iters = 0
         for i in range(iters):
             iteration(batch_d, labels)
-            progress(f"iteration {i + 1}/{iters}: {time.perf_counter() - t0:.1f} s")
+            done_iters += 1
+            now = time.perf_counter()
+            progress(f"iteration {i + 1}/{iters}: {now - t0:.1f} s")
+            if budget_s > 0 and done_iters < iters and (now - T_ORIGIN) + (now - t0) / done_iters > budget_s:
+                progress(f"budget: stopping after {done_iters} iteration(s), {now - T_ORIGIN:.0f} s since start")
+                break
         dt = time.perf_counter() - t0
     finally:
         done.set()
         O.set_dropout_replay(None)
-    return {"value": round(batch * iters / dt, 4), "unit": "samples/s", "cores": threads, "kind": "port",
-            "cpu_model": cpu_model(), "cpus_available": avail, "cpu_share": share,
-            "seconds_per_iteration": round(dt / iters, 2),
-            "warmup_seconds": round(warm, 2),
-            "sample": f"oracle/fusion_oracle.py {variant} iteration (torch CPU fp32, dropout 0.1"
-                      f"{', feature_all_lap honoured' if variant != 'prigumbel' else ''}), batch {batch}, "
-                      f"64x256 EEG + 32-d action, {iters} timed iteration(s) after 1 warm-up"
-                      f"{f' at batch {warm_batch}' if warm_batch != batch else ''}, {dt:.1f} s timed"}
+    out = {"value": round(batch * done_iters / dt, 4), "unit": "samples/s", "cores": threads, "kind": "port",
+           "cpu_model": cpu_model(), "cpus_available": avail, "cpu_share": share, "batch": batch,
+           "timed_iterations": done_iters, "seconds_per_iteration": round(dt / done_iters, 2),
+           "warmup_seconds": round(warm, 2),
+           "sample": f"oracle/fusion_oracle.py {variant} iteration (torch CPU fp32, dropout 0.1"
+                     f"{', feature_all_lap honoured' if variant != 'prigumbel' else ''}), batch {batch}, "
+                     f"64x256 EEG + 32-d action, {done_iters} timed iteration(s) after 1 warm-up"
+                     f"{f' at batch {warm_batch}' if warm_batch != batch else ''}, {dt:.1f} s timed"}
+    if done_iters < iters:
+        out["deviation"] = (f"{done_iters} of {iters} timed iterations: the next one would have ended past the "
+                            f"{budget_s:.0f} s run budget (bench.py --cpu-budget)")
+    return out
 
 
 def load_profile_json(name: str, tag: str):
@@ -284,10 +310,13 @@ def probe_stats(probe: dict) -> dict:
     for tag, v in probe.items():
         if not v:
             continue
-        ms = [s.elapsed_time(e) for s, e, _ in v]
-        fl = sum(f for _, _, f in v)
+        ms = [s.elapsed_time(e) for s, e, _, _ in v]
+        fl = sum(x[2] for x in v)
+        by = sum(x[3] for x in v)
         out[tag] = {"launches": len(v), "avg_ms": sum(ms) / len(ms), "tflops": fl / (sum(ms) * 1e-3) / 1e12,
                     "flops_per_launch": fl / len(v)}
+        if by > 0:
+            out[tag].update(bytes_per_launch=by / len(v), gbps=by / (sum(ms) * 1e-3) / 1e9)
     return out
 
 
@@ -496,6 +525,20 @@ def main():
             ms1 = sum(p["avg_ms"] * p["launches"] for p in f1p)
             f1 = {"avg_ms": ms1 / n1, "tflops": sum(p["flops_per_launch"] * p["launches"] for p in f1p) / (ms1 * 1e-3) / 1e12}
         ffn1 = load_profile_json(PMC_FILE, "ffn1_fwd") or {}
+        hbm = {t: {"launches_per_step": round(ks[t]["launches"] / probed_steps, 2),
+                   "avg_us": round(ks[t]["avg_ms"] * 1e3, 2),
+                   "alg_bytes_per_launch": int(ks[t]["bytes_per_launch"]),
+                   "achieved": round(ks[t]["gbps"], 1), "peak": PEAK_HBM, "unit": "GB/s",
+                   "frac": round(ks[t]["gbps"] / PEAK_HBM, 4), "what": KERNEL_GROUPS[t],
+                   **({"traffic": p.get("hbm_bytes_per_launch"), "pmc_round": p.get("round")}
+                      if (p := load_profile_json(PMC_FILE, t)) else {})}
+               for t in HBM_TAGS if t in ks and "gbps" in ks[t]}
+        # non-default routing switches: the symbol names above assume the default routes
+        routing_env = {k: v for k, v in os.environ.items()
+                       if k.startswith("EEGF_") and k not in ("EEGF_LIB", "EEGF_BERT_WEIGHTS")}
+        if routing_env:
+            roofline["routing"] = ("assumed default routing; EEGF_* switches set: " +
+                                   ", ".join(f"{k}={v}" for k, v in sorted(routing_env.items())))
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "samples/s", "n_gpus": world, "steps": steps,
             "warmup": args.warmup, "ms_per_step": round(total_dt / steps * 1e3, 3), "higher_is_better": True,
@@ -518,6 +561,7 @@ def main():
             "kernels": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                         for k, v in ks.items()},
             "kernels_by_symbol": kernels_by_symbol,
+            "hbm_kernels": hbm,
             "loss": float(loss[-1].item()),
         }
         if len(sweep) > 1 or feawei is not None:
@@ -526,18 +570,17 @@ def main():
         if replicas is not None:
             out["replicas"] = replicas
         if world == 1 and not args.no_cpu_baseline:
-            cb = cpu_baseline(args.variant, args.cpu_batch, args.cpu_iters, args.cpu_warm_batch)
-            # the BASELINE.md §3 sample (batch 256, 1 warm-up + 3 timed) measured on a GPU box's host by
-            # `bench.py --cpu-baseline-only --cpu-batch 256 --cpu-iters 3`: too long for the default run
-            ref = load_profile_json("cpu_baseline_b256.json", args.variant)
+            # batch 256 (the GPU leg's batch), 1 warm-up + 3 timed iterations, in this run;
+            # the stderr heartbeat every 30 s keeps the ~5.5 min leg visibly alive
+            cb = cpu_baseline(args.variant, args.cpu_batch, args.cpu_iters, args.cpu_warm_batch, args.cpu_budget)
             if args.cpu_batch != B:
-                cb["deviation"] = (f"live sample at batch {args.cpu_batch} (BASELINE.md section 3 asks for batch {B}, "
-                                   f"1 warm-up + >= 3 timed iterations in the same run: about 107 s per batch-256 "
-                                   f"iteration on a GPU box's 16-CPU share, minutes more than the default run may "
-                                   f"take); the batch-256 sample, measured by bench.py --cpu-baseline-only "
-                                   f"--cpu-batch 256 --cpu-iters 3 on a GPU box, is batch256_measured")
+                cb["deviation"] = (cb.get("deviation", "") + "; " if "deviation" in cb else "") + (
+                    f"sample at batch {args.cpu_batch}, the GPU leg runs batch {B} (--cpu-batch)")
+            # an earlier separate run of the same sample on a GPU box (bench.py --cpu-baseline-only): a cross-check
+            ref = load_profile_json("cpu_baseline_b256.json", args.variant)
             if ref:
-                cb["batch256_measured"] = ref
+                cb["crosscheck_b256_separate_run"] = {k: ref[k] for k in ("value", "seconds_per_iteration", "sample")
+                                                      if k in ref}
             out["cpu_baseline"] = cb
         print(json.dumps(out), flush=True)
     if world > 1:

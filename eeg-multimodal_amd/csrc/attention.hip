@@ -480,14 +480,14 @@ extern "C" int eegf_attn_fwd(int dtype, int B, int H, int L, const void* qkv, lo
              drop_p, seed, offset, drop_p > 0.f ? drop_bits : nullptr};
   if (l256_path(dtype, B, H, L, key_bias, false, ld_qkv, ld_out)) {
     const dim3 g1(l256_grid(B * H));
-    if (a.bits) hipLaunchKernelGGL((attn_fwd256_kernel<true, true>), g1, dim3(512), 0, stream, a);
-    else if (drop_p > 0.f) hipLaunchKernelGGL(attn_fwd256_kernel<true>, g1, dim3(512), 0, stream, a);
-    else hipLaunchKernelGGL(attn_fwd256_kernel<false>, g1, dim3(512), 0, stream, a);
+    if (a.bits) EEGF_LAUNCH((attn_fwd256_kernel<true, true>), g1, dim3(512), 0, stream, a);
+    else if (drop_p > 0.f) EEGF_LAUNCH(attn_fwd256_kernel<true>, g1, dim3(512), 0, stream, a);
+    else EEGF_LAUNCH(attn_fwd256_kernel<false>, g1, dim3(512), 0, stream, a);
     return (int)hipGetLastError();
   }
   const dim3 grid(L / 128, H, B);
-  if (dtype == EEGF_F32) hipLaunchKernelGGL(attn_fwd_kernel<float>, grid, dim3(512), 0, stream, a);
-  else if (dtype == EEGF_BF16) hipLaunchKernelGGL(attn_fwd_kernel<bf16>, grid, dim3(512), 0, stream, a);
+  if (dtype == EEGF_F32) EEGF_LAUNCH(attn_fwd_kernel<float>, grid, dim3(512), 0, stream, a);
+  else if (dtype == EEGF_BF16) EEGF_LAUNCH(attn_fwd_kernel<bf16>, grid, dim3(512), 0, stream, a);
   else return EEGF_ERR_ARG;
   return (int)hipGetLastError();
 }
@@ -506,17 +506,17 @@ extern "C" int eegf_attn_bwd(int dtype, int B, int H, int L, const void* qkv, lo
              scale, drop_p, seed, offset, drop_p > 0.f ? const_cast<uint32_t*>(drop_bits) : nullptr};
   if (l256_path(dtype, B, H, L, key_bias, true, ld_qkv, ld_out)) {
     const dim3 g1(l256_grid(B * H));
-    if (drop_p > 0.f) hipLaunchKernelGGL(attn_bwd256_kernel<true>, g1, dim3(512), 0, stream, a);
-    else hipLaunchKernelGGL(attn_bwd256_kernel<false>, g1, dim3(512), 0, stream, a);
+    if (drop_p > 0.f) EEGF_LAUNCH(attn_bwd256_kernel<true>, g1, dim3(512), 0, stream, a);
+    else EEGF_LAUNCH(attn_bwd256_kernel<false>, g1, dim3(512), 0, stream, a);
     return (int)hipGetLastError();
   }
   const dim3 grid(L / 256, H, B);
-  if (dtype == EEGF_F32) hipLaunchKernelGGL(attn_bwd_kernel<float>, grid, dim3(512), 0, stream, a);
-  else if (dtype == EEGF_BF16) hipLaunchKernelGGL(attn_bwd_kernel<bf16>, grid, dim3(512), 0, stream, a);
+  if (dtype == EEGF_F32) EEGF_LAUNCH(attn_bwd_kernel<float>, grid, dim3(512), 0, stream, a);
+  else if (dtype == EEGF_BF16) EEGF_LAUNCH(attn_bwd_kernel<bf16>, grid, dim3(512), 0, stream, a);
   else return EEGF_ERR_ARG;
   if (L > 256) {
     const long n = (long)B * L * 768;
-    hipLaunchKernelGGL(dq_convert_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, dq_workspace, dqkv,
+    EEGF_LAUNCH(dq_convert_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, dq_workspace, dqkv,
                        dtype == EEGF_BF16, (long)B * L, ld_qkv);
   }
   return (int)hipGetLastError();
@@ -541,8 +541,8 @@ extern "C" int eegf_attn_varlen_fwd(int dtype, int B, int H, int max_len, const 
   AttnArgs a{qkv, out, lse, key_bias, nullptr, nullptr, nullptr, nullptr, B, H, max_len, ld_qkv, ld_out, scale,
              drop_p, seed, offset, nullptr, cu_seqlens};
   const dim3 grid((max_len + 127) / 128, H, B);
-  if (dtype == EEGF_F32) hipLaunchKernelGGL((attn_fwd_kernel<float, true>), grid, dim3(512), 0, stream, a);
-  else hipLaunchKernelGGL((attn_fwd_kernel<bf16, true>), grid, dim3(512), 0, stream, a);
+  if (dtype == EEGF_F32) EEGF_LAUNCH((attn_fwd_kernel<float, true>), grid, dim3(512), 0, stream, a);
+  else EEGF_LAUNCH((attn_fwd_kernel<bf16, true>), grid, dim3(512), 0, stream, a);
   return (int)hipGetLastError();
 }
 
@@ -569,11 +569,11 @@ extern "C" int eegf_attn_varlen_bwd(int dtype, int B, int H, int max_len, const 
   AttnArgs a{qkv, nullptr, const_cast<float*>(lse), key_bias, out, dout, dqkv, dq_workspace, B, H, max_len, ld_qkv,
              ld_out, scale, drop_p, seed, offset, nullptr, cu_seqlens};
   const dim3 grid((max_len + 255) / 256, H, B);
-  if (dtype == EEGF_F32) hipLaunchKernelGGL((attn_bwd_kernel<float, true>), grid, dim3(512), 0, stream, a);
-  else hipLaunchKernelGGL((attn_bwd_kernel<bf16, true>), grid, dim3(512), 0, stream, a);
+  if (dtype == EEGF_F32) EEGF_LAUNCH((attn_bwd_kernel<float, true>), grid, dim3(512), 0, stream, a);
+  else EEGF_LAUNCH((attn_bwd_kernel<bf16, true>), grid, dim3(512), 0, stream, a);
   if (max_len > 256) {
     const long n = total_rows * 768;
-    hipLaunchKernelGGL(dq_convert_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, dq_workspace, dqkv,
+    EEGF_LAUNCH(dq_convert_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, dq_workspace, dqkv,
                        dtype == EEGF_BF16, total_rows, ld_qkv);
   }
   return (int)hipGetLastError();
@@ -674,10 +674,10 @@ extern "C" int eegf_attn_small_fwd(int dtype, int N, int S, const void* qkv, lon
     return EEGF_ERR_ARG;
   const dim3 grid(N, 12);
   if (dtype == EEGF_F32)
-    hipLaunchKernelGGL(attn_small_fwd_kernel<float>, grid, dim3(64), 0, stream, S, (const float*)qkv, ld_qkv, scale,
+    EEGF_LAUNCH(attn_small_fwd_kernel<float>, grid, dim3(64), 0, stream, S, (const float*)qkv, ld_qkv, scale,
                        drop_p, seed, offset, (float*)out, ld_out, probs);
   else if (dtype == EEGF_BF16)
-    hipLaunchKernelGGL(attn_small_fwd_kernel<bf16>, grid, dim3(64), 0, stream, S, (const bf16*)qkv, ld_qkv, scale,
+    EEGF_LAUNCH(attn_small_fwd_kernel<bf16>, grid, dim3(64), 0, stream, S, (const bf16*)qkv, ld_qkv, scale,
                        drop_p, seed, offset, (bf16*)out, ld_out, probs);
   else return EEGF_ERR_ARG;
   return (int)hipGetLastError();
@@ -691,10 +691,10 @@ extern "C" int eegf_attn_small_bwd(int dtype, int N, int S, const void* qkv, lon
     return EEGF_ERR_ARG;
   const dim3 grid(N, 12);
   if (dtype == EEGF_F32)
-    hipLaunchKernelGGL(attn_small_bwd_kernel<float>, grid, dim3(64), 0, stream, S, (const float*)qkv, ld_qkv, probs,
+    EEGF_LAUNCH(attn_small_bwd_kernel<float>, grid, dim3(64), 0, stream, S, (const float*)qkv, ld_qkv, probs,
                        (const float*)dout, ld_out, scale, drop_p, seed, offset, (float*)dqkv, ld_dqkv);
   else if (dtype == EEGF_BF16)
-    hipLaunchKernelGGL(attn_small_bwd_kernel<bf16>, grid, dim3(64), 0, stream, S, (const bf16*)qkv, ld_qkv, probs,
+    EEGF_LAUNCH(attn_small_bwd_kernel<bf16>, grid, dim3(64), 0, stream, S, (const bf16*)qkv, ld_qkv, probs,
                        (const bf16*)dout, ld_out, scale, drop_p, seed, offset, (bf16*)dqkv, ld_dqkv);
   else return EEGF_ERR_ARG;
   return (int)hipGetLastError();

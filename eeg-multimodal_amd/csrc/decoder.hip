@@ -166,10 +166,10 @@ __global__ void __launch_bounds__(64 * XW) xrow_dot_mfma_kernel(const bf16* __re
 template <typename T, typename TV>
 void launch_xrow_dot(const T* mem, const TV* vec, const float* kbias, int B, int S, float* out, hipStream_t st) {
   if constexpr (sizeof(T) == 2)
-    hipLaunchKernelGGL((xrow_dot_mfma_kernel<TV>), dim3((S + 64 * XR - 1) / (64 * XR), B), dim3(64 * XW), 0, st, mem, vec,
+    EEGF_LAUNCH((xrow_dot_mfma_kernel<TV>), dim3((S + 64 * XR - 1) / (64 * XR), B), dim3(64 * XW), 0, st, mem, vec,
                        kbias, S, out);
   else
-    hipLaunchKernelGGL((xrow_dot_kernel<T, TV>), dim3((S + 63) / 64, B), dim3(256), 0, st, mem, vec, kbias, S, out);
+    EEGF_LAUNCH((xrow_dot_kernel<T, TV>), dim3((S + 63) / 64, B), dim3(256), 0, st, mem, vec, kbias, S, out);
 }
 
 // Softmax (+dropout) of the 12 raw score rows of batch row b into LDS pt[S][12] (p~);
@@ -554,14 +554,14 @@ int xfwd(int B, int S, const void* mem, const void* qp, const float* kb, float p
     if (g_xbwd_mfma) {
       const size_t lds = sizeof(float) * (size_t)((S + 15) & ~15) * NH;
       hipFuncSetAttribute((const void*)xctx_mfma_kernel<TQ>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      hipLaunchKernelGGL((xctx_mfma_kernel<TQ>), dim3(E / SLAB, B), dim3(256), lds, st, (const bf16*)mem, ws, S, p,
+      EEGF_LAUNCH((xctx_mfma_kernel<TQ>), dim3(E / SLAB, B), dim3(256), lds, st, (const bf16*)mem, ws, S, p,
                          seed, off, probs, psum, (TQ*)ctx);
       return (int)hipGetLastError();
     }
   }
   const size_t lds = sizeof(float) * ((size_t)S * NH + 4 * NH * SLAB);
   hipFuncSetAttribute((const void*)xctx_kernel<T, TQ>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((xctx_kernel<T, TQ>), dim3(E / SLAB, B), dim3(512), lds, st, (const T*)mem, ws, S, p, seed, off,
+  EEGF_LAUNCH((xctx_kernel<T, TQ>), dim3(E / SLAB, B), dim3(512), lds, st, (const T*)mem, ws, S, p, seed, off,
                      probs, psum, (TQ*)ctx);
   return (int)hipGetLastError();
 }
@@ -573,14 +573,14 @@ int xbwd(int B, int S, const void* mem, const void* qp, const float* probs, cons
     if (g_xbwd_mfma) {
       const size_t lds = sizeof(float) * (size_t)((S + 15) & ~15) * A2LD;
       hipFuncSetAttribute((const void*)xbwd_mfma_kernel<TQ>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      hipLaunchKernelGGL((xbwd_mfma_kernel<TQ>), dim3(E / SLAB, B), dim3(256), lds, st, (const bf16*)mem,
+      EEGF_LAUNCH((xbwd_mfma_kernel<TQ>), dim3(E / SLAB, B), dim3(256), lds, st, (const bf16*)mem,
                          (const TQ*)qp, probs, ws, dpsum, (const TQ*)dctx, S, p, seed, off, (bf16*)dmem, beta, (TQ*)dqp);
       return (int)hipGetLastError();
     }
   }
   const size_t lds = sizeof(float) * ((size_t)2 * S * NH + 4 * NH * SLAB);
   hipFuncSetAttribute((const void*)xbwd_cols_kernel<T, TQ>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((xbwd_cols_kernel<T, TQ>), dim3(E / SLAB, B), dim3(512), lds, st, (const T*)mem, (const TQ*)qp,
+  EEGF_LAUNCH((xbwd_cols_kernel<T, TQ>), dim3(E / SLAB, B), dim3(512), lds, st, (const T*)mem, (const TQ*)qp,
                      probs, ws, dpsum, (const TQ*)dctx, S, p, seed, off, (T*)dmem, beta, (TQ*)dqp);
   return (int)hipGetLastError();
 }
@@ -621,7 +621,7 @@ extern "C" int eegf_head_bias_fwd(int B, int W, int group, float* x, const float
                                   hipStream_t stream) {
   if (B <= 0 || W <= 0 || group <= 0 || W % group != 0 || !x || !bias || !s) return EEGF_ERR_ARG;
   const long n = (long)B * W;
-  hipLaunchKernelGGL(head_bias_fwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, B, W, group, x,
+  EEGF_LAUNCH(head_bias_fwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, B, W, group, x,
                      bias, s);
   return (int)hipGetLastError();
 }
@@ -629,7 +629,7 @@ extern "C" int eegf_head_bias_fwd(int B, int W, int group, float* x, const float
 extern "C" int eegf_head_bias_bwd(int B, int W, int group, const float* dx, const float* bias, const float* s,
                                   float* ds, float* dbias, float beta, hipStream_t stream) {
   if (B <= 0 || W <= 0 || group != 64 || W % 256 != 0 || !dx || !bias || !s || !ds) return EEGF_ERR_ARG;
-  hipLaunchKernelGGL(head_bias_ds_kernel, dim3(B), dim3(256), 0, stream, W, dx, bias, ds);
-  if (dbias) hipLaunchKernelGGL(head_bias_db_kernel, dim3(W / 64), dim3(256), 0, stream, B, W, dx, s, dbias, beta);
+  EEGF_LAUNCH(head_bias_ds_kernel, dim3(B), dim3(256), 0, stream, W, dx, bias, ds);
+  if (dbias) EEGF_LAUNCH(head_bias_db_kernel, dim3(W / 64), dim3(256), 0, stream, B, W, dx, s, dbias, beta);
   return (int)hipGetLastError();
 }

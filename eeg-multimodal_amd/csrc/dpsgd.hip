@@ -179,13 +179,13 @@ extern "C" int eegf_ghost_norm(int dtype, int S, int T, int Dx, int Dy, const vo
   if (ws_elems < (long)S * ntiles) return EEGF_ERR_ARG;
   const dim3 grid((unsigned)S, (unsigned)ntiles);
   if (dtype == EEGF_F32)
-    hipLaunchKernelGGL(ghost_norm_kernel<float>, grid, dim3(256), 0, stream, T, Dx, Dy, (const float*)X, ldx,
+    EEGF_LAUNCH(ghost_norm_kernel<float>, grid, dim3(256), 0, stream, T, Dx, Dy, (const float*)X, ldx,
                        (const float*)DY, ldy, ws);
   else if (dtype == EEGF_BF16)
-    hipLaunchKernelGGL(ghost_norm_kernel<bf16>, grid, dim3(256), 0, stream, T, Dx, Dy, (const bf16*)X, ldx,
+    EEGF_LAUNCH(ghost_norm_kernel<bf16>, grid, dim3(256), 0, stream, T, Dx, Dy, (const bf16*)X, ldx,
                        (const bf16*)DY, ldy, ws);
   else return EEGF_ERR_ARG;
-  hipLaunchKernelGGL(rowsum_kernel, dim3((S + 255) / 256), dim3(256), 0, stream, S, ntiles, (const float*)ws, beta, out);
+  EEGF_LAUNCH(rowsum_kernel, dim3((S + 255) / 256), dim3(256), 0, stream, S, ntiles, (const float*)ws, beta, out);
   return (int)hipGetLastError();
 }
 
@@ -196,10 +196,10 @@ extern "C" int eegf_seg_sqnorm(int dtype, int S, int T, int W, const void* dy, l
   if (xs && (!mean || !rstd)) return EEGF_ERR_ARG;
   if (!xs && !bias_term) return EEGF_ERR_ARG;
   if (dtype == EEGF_F32)
-    hipLaunchKernelGGL(seg_sqnorm_kernel<float>, dim3(S), dim3(256), 0, stream, T, W, (const float*)dy, ldd,
+    EEGF_LAUNCH(seg_sqnorm_kernel<float>, dim3(S), dim3(256), 0, stream, T, W, (const float*)dy, ldd,
                        (const float*)xs, ldx, mean, rstd, bias_term, beta, out);
   else if (dtype == EEGF_BF16)
-    hipLaunchKernelGGL(seg_sqnorm_kernel<bf16>, dim3(S), dim3(256), 0, stream, T, W, (const bf16*)dy, ldd,
+    EEGF_LAUNCH(seg_sqnorm_kernel<bf16>, dim3(S), dim3(256), 0, stream, T, W, (const bf16*)dy, ldd,
                        (const bf16*)xs, ldx, mean, rstd, bias_term, beta, out);
   else return EEGF_ERR_ARG;
   return (int)hipGetLastError();
@@ -210,10 +210,10 @@ extern "C" int eegf_row_sqnorm(int dtype, int S, int Wa, const void* a, long lda
   if (S <= 0 || Wa <= 0 || !a || !out || (b && Wb <= 0)) return EEGF_ERR_ARG;
   const dim3 grid((unsigned)((S + 3) / 4));
   if (dtype == EEGF_F32)
-    hipLaunchKernelGGL(row_sqnorm_kernel<float>, grid, dim3(256), 0, stream, S, Wa, (const float*)a, lda, Wb,
+    EEGF_LAUNCH(row_sqnorm_kernel<float>, grid, dim3(256), 0, stream, S, Wa, (const float*)a, lda, Wb,
                        (const float*)b, ldb, out);
   else if (dtype == EEGF_BF16)
-    hipLaunchKernelGGL(row_sqnorm_kernel<bf16>, grid, dim3(256), 0, stream, S, Wa, (const bf16*)a, lda, Wb,
+    EEGF_LAUNCH(row_sqnorm_kernel<bf16>, grid, dim3(256), 0, stream, S, Wa, (const bf16*)a, lda, Wb,
                        (const bf16*)b, ldb, out);
   else return EEGF_ERR_ARG;
   return (int)hipGetLastError();
@@ -222,7 +222,7 @@ extern "C" int eegf_row_sqnorm(int dtype, int S, int Wa, const void* a, long lda
 extern "C" int eegf_dp_clip_rows(int S, int ncls, const float* psn, float max_norm, float* dlogits, float* clip,
                                  hipStream_t stream) {
   if (S <= 0 || ncls <= 0 || !psn || !dlogits || !(max_norm > 0.f)) return EEGF_ERR_ARG;
-  hipLaunchKernelGGL(clip_rows_kernel, dim3((S + 255) / 256), dim3(256), 0, stream, S, ncls, psn, max_norm, dlogits, clip);
+  EEGF_LAUNCH(clip_rows_kernel, dim3((S + 255) / 256), dim3(256), 0, stream, S, ncls, psn, max_norm, dlogits, clip);
   return (int)hipGetLastError();
 }
 
@@ -230,7 +230,7 @@ extern "C" int eegf_dp_noise(long n, float* grad, float std, float scale, unsign
                              unsigned long long offset, hipStream_t stream) {
   if (n <= 0 || !grad || std < 0.f) return EEGF_ERR_ARG;
   const long calls = (n + 3) / 4;
-  hipLaunchKernelGGL(dp_noise_kernel, dim3((unsigned)((calls + 255) / 256)), dim3(256), 0, stream, n, grad, std, scale,
+  EEGF_LAUNCH(dp_noise_kernel, dim3((unsigned)((calls + 255) / 256)), dim3(256), 0, stream, n, grad, std, scale,
                      seed, offset);
   return (int)hipGetLastError();
 }

@@ -33,8 +33,8 @@ __global__ void __launch_bounds__(256) dropout_kernel(long n, int group, float p
 extern "C" int eegf_axpby(int dtype, long n, float alpha, const void* x, float beta, void* y, hipStream_t stream) {
   if (n <= 0 || !x || !y) return EEGF_ERR_ARG;
   const dim3 grid((unsigned)((n + 255) / 256));
-  if (dtype == EEGF_F32) hipLaunchKernelGGL(axpby_kernel<float>, grid, dim3(256), 0, stream, n, alpha, (const float*)x, beta, (float*)y);
-  else if (dtype == EEGF_BF16) hipLaunchKernelGGL(axpby_kernel<bf16>, grid, dim3(256), 0, stream, n, alpha, (const bf16*)x, beta, (bf16*)y);
+  if (dtype == EEGF_F32) EEGF_LAUNCH(axpby_kernel<float>, grid, dim3(256), 0, stream, n, alpha, (const float*)x, beta, (float*)y);
+  else if (dtype == EEGF_BF16) EEGF_LAUNCH(axpby_kernel<bf16>, grid, dim3(256), 0, stream, n, alpha, (const bf16*)x, beta, (bf16*)y);
   else return EEGF_ERR_ARG;
   return (int)hipGetLastError();
 }
@@ -42,8 +42,8 @@ extern "C" int eegf_axpby(int dtype, long n, float alpha, const void* x, float b
 extern "C" int eegf_tanh_bwd(int dtype, long n, const void* dy, const void* y, void* dx, hipStream_t stream) {
   if (n <= 0 || !dy || !y || !dx) return EEGF_ERR_ARG;
   const dim3 grid((unsigned)((n + 255) / 256));
-  if (dtype == EEGF_F32) hipLaunchKernelGGL(tanh_bwd_kernel<float>, grid, dim3(256), 0, stream, n, (const float*)dy, (const float*)y, (float*)dx);
-  else if (dtype == EEGF_BF16) hipLaunchKernelGGL(tanh_bwd_kernel<bf16>, grid, dim3(256), 0, stream, n, (const bf16*)dy, (const bf16*)y, (bf16*)dx);
+  if (dtype == EEGF_F32) EEGF_LAUNCH(tanh_bwd_kernel<float>, grid, dim3(256), 0, stream, n, (const float*)dy, (const float*)y, (float*)dx);
+  else if (dtype == EEGF_BF16) EEGF_LAUNCH(tanh_bwd_kernel<bf16>, grid, dim3(256), 0, stream, n, (const bf16*)dy, (const bf16*)y, (bf16*)dx);
   else return EEGF_ERR_ARG;
   return (int)hipGetLastError();
 }
@@ -53,8 +53,8 @@ extern "C" int eegf_dropout(int dtype, long n, int group, float p, unsigned long
   if (n <= 0 || group <= 0 || p < 0.f || p >= 1.f || !x) return EEGF_ERR_ARG;
   if (p == 0.f) return 0;
   const dim3 grid((unsigned)((n + 255) / 256));
-  if (dtype == EEGF_F32) hipLaunchKernelGGL(dropout_kernel<float>, grid, dim3(256), 0, stream, n, group, p, seed, offset, (float*)x);
-  else if (dtype == EEGF_BF16) hipLaunchKernelGGL(dropout_kernel<bf16>, grid, dim3(256), 0, stream, n, group, p, seed, offset, (bf16*)x);
+  if (dtype == EEGF_F32) EEGF_LAUNCH(dropout_kernel<float>, grid, dim3(256), 0, stream, n, group, p, seed, offset, (float*)x);
+  else if (dtype == EEGF_BF16) EEGF_LAUNCH(dropout_kernel<bf16>, grid, dim3(256), 0, stream, n, group, p, seed, offset, (bf16*)x);
   else return EEGF_ERR_ARG;
   return (int)hipGetLastError();
 }
@@ -92,9 +92,9 @@ extern "C" int eegf_seq_mean(int dtype, int B, int L, int width, const void* x, 
   if (B <= 0 || B > 65535 || L <= 0 || width <= 0 || !x || !out || ld_x < width || ld_out < width) return EEGF_ERR_ARG;
   const dim3 grid(B, (width + 255) / 256);
   if (dtype == EEGF_F32)
-    hipLaunchKernelGGL(seq_mean_kernel<float>, grid, dim3(256), 0, stream, L, width, (const float*)x, ld_x, out, ld_out);
+    EEGF_LAUNCH(seq_mean_kernel<float>, grid, dim3(256), 0, stream, L, width, (const float*)x, ld_x, out, ld_out);
   else if (dtype == EEGF_BF16)
-    hipLaunchKernelGGL(seq_mean_kernel<bf16>, grid, dim3(256), 0, stream, L, width, (const bf16*)x, ld_x, out, ld_out);
+    EEGF_LAUNCH(seq_mean_kernel<bf16>, grid, dim3(256), 0, stream, L, width, (const bf16*)x, ld_x, out, ld_out);
   else return EEGF_ERR_ARG;
   return (int)hipGetLastError();
 }
@@ -105,10 +105,10 @@ extern "C" int eegf_seq_mean_bwd(int dtype, int B, int L, int width, const float
     return EEGF_ERR_ARG;
   const dim3 grid(B, (width + 255) / 256);
   if (dtype == EEGF_F32)
-    hipLaunchKernelGGL(seq_mean_bwd_kernel<float>, grid, dim3(256), 0, stream, L, width, dmean, ld_dmean, (float*)dx,
+    EEGF_LAUNCH(seq_mean_bwd_kernel<float>, grid, dim3(256), 0, stream, L, width, dmean, ld_dmean, (float*)dx,
                        ld_dx, beta);
   else if (dtype == EEGF_BF16)
-    hipLaunchKernelGGL(seq_mean_bwd_kernel<bf16>, grid, dim3(256), 0, stream, L, width, dmean, ld_dmean, (bf16*)dx,
+    EEGF_LAUNCH(seq_mean_bwd_kernel<bf16>, grid, dim3(256), 0, stream, L, width, dmean, ld_dmean, (bf16*)dx,
                        ld_dx, beta);
   else return EEGF_ERR_ARG;
   return (int)hipGetLastError();
@@ -136,6 +136,6 @@ __global__ void __launch_bounds__(256) ring_proxy_kernel(long n4, int passes, fl
 
 extern "C" int eegf_ring_proxy(long n, int passes, int wgs, float* x, hipStream_t stream) {
   if (n <= 0 || n % 4 || passes <= 0 || wgs <= 0 || wgs > 4096 || !x || (((uintptr_t)x) & 15)) return EEGF_ERR_ARG;
-  hipLaunchKernelGGL(ring_proxy_kernel, dim3(wgs), dim3(256), 0, stream, n / 4, passes, x);
+  EEGF_LAUNCH(ring_proxy_kernel, dim3(wgs), dim3(256), 0, stream, n / 4, passes, x);
   return (int)hipGetLastError();
 }

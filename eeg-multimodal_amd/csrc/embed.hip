@@ -108,7 +108,7 @@ __global__ void __launch_bounds__(256) varlen_rows_kernel(const int* __restrict_
 extern "C" int eegf_seq_lengths(int B, int L, const long long* mask, int* lens, int* nonprefix, hipStream_t stream) {
   if (B <= 0 || L <= 0 || !mask || !lens || !nonprefix) return EEGF_ERR_ARG;
   hipMemsetAsync(nonprefix, 0, sizeof(int), stream);
-  hipLaunchKernelGGL(seq_lengths_kernel, dim3(B), dim3(64), 0, stream, mask, L, lens, nonprefix);
+  EEGF_LAUNCH(seq_lengths_kernel, dim3(B), dim3(64), 0, stream, mask, L, lens, nonprefix);
   return (int)hipGetLastError();
 }
 
@@ -126,10 +126,10 @@ extern "C" int eegf_varlen_embed(int dtype, int B, int L, int width, const int* 
   }
   const dim3 grid((L + 3) / 4, B);
   if (dtype == EEGF_F32)
-    hipLaunchKernelGGL(varlen_embed_kernel<float>, grid, dim3(256), 0, stream, cu_seqlens, ids, L, width, word, pos,
+    EEGF_LAUNCH(varlen_embed_kernel<float>, grid, dim3(256), 0, stream, cu_seqlens, ids, L, width, word, pos,
                        (float*)out, ids_packed);
   else
-    hipLaunchKernelGGL(varlen_embed_kernel<bf16>, grid, dim3(256), 0, stream, cu_seqlens, ids, L, width, word, pos,
+    EEGF_LAUNCH(varlen_embed_kernel<bf16>, grid, dim3(256), 0, stream, cu_seqlens, ids, L, width, word, pos,
                        (bf16*)out, ids_packed);
   return (int)hipGetLastError();
 }
@@ -145,7 +145,7 @@ extern "C" int eegf_varlen_rows(int dtype, int B, int S, int width, const int* c
     hipMemset2DAsync((char*)dst + packed_rows * ld_dst * es, ld_dst * es, 0, width * es, total_rows - packed_rows,
                      stream);
   const dim3 grid((S + 3) / 4, B);
-  hipLaunchKernelGGL(varlen_rows_kernel, grid, dim3(256), 0, stream, cu_seqlens, S, (int)(width * es / 16),
+  EEGF_LAUNCH(varlen_rows_kernel, grid, dim3(256), 0, stream, cu_seqlens, S, (int)(width * es / 16),
                      (const char*)src, (long)(ld_src * es), (char*)dst, (long)(ld_dst * es), to_padded);
   return (int)hipGetLastError();
 }
@@ -153,8 +153,8 @@ extern "C" int eegf_varlen_rows(int dtype, int B, int S, int width, const int* c
 extern "C" int eegf_window_tokens(int dtype, int B, int C, int T, const float* eeg, void* tokens, hipStream_t stream) {
   if (B <= 0 || C <= 0 || C > 128 || T <= 0 || !eeg || !tokens || B > 65535) return EEGF_ERR_ARG;
   const dim3 grid((T + 63) / 64, B);
-  if (dtype == EEGF_F32) hipLaunchKernelGGL(window_tokens_kernel<float>, grid, dim3(256), 0, stream, eeg, C, T, (float*)tokens);
-  else if (dtype == EEGF_BF16) hipLaunchKernelGGL(window_tokens_kernel<bf16>, grid, dim3(256), 0, stream, eeg, C, T, (bf16*)tokens);
+  if (dtype == EEGF_F32) EEGF_LAUNCH(window_tokens_kernel<float>, grid, dim3(256), 0, stream, eeg, C, T, (float*)tokens);
+  else if (dtype == EEGF_BF16) EEGF_LAUNCH(window_tokens_kernel<bf16>, grid, dim3(256), 0, stream, eeg, C, T, (bf16*)tokens);
   else return EEGF_ERR_ARG;
   return (int)hipGetLastError();
 }
@@ -163,8 +163,8 @@ extern "C" int eegf_embed_gather(int dtype, long rows, int width, const long lon
                                  hipStream_t stream) {
   if (rows <= 0 || width <= 0 || !ids || !table || !out) return EEGF_ERR_ARG;
   const dim3 grid((unsigned)((rows + 3) / 4));
-  if (dtype == EEGF_F32) hipLaunchKernelGGL(gather_kernel<float>, grid, dim3(256), 0, stream, ids, table, width, rows, (float*)out);
-  else if (dtype == EEGF_BF16) hipLaunchKernelGGL(gather_kernel<bf16>, grid, dim3(256), 0, stream, ids, table, width, rows, (bf16*)out);
+  if (dtype == EEGF_F32) EEGF_LAUNCH(gather_kernel<float>, grid, dim3(256), 0, stream, ids, table, width, rows, (float*)out);
+  else if (dtype == EEGF_BF16) EEGF_LAUNCH(gather_kernel<bf16>, grid, dim3(256), 0, stream, ids, table, width, rows, (bf16*)out);
   else return EEGF_ERR_ARG;
   return (int)hipGetLastError();
 }
@@ -174,9 +174,9 @@ extern "C" int eegf_embed_scatter_add(int dtype, long rows, int width, const lon
   if (rows <= 0 || width <= 0 || !ids || !d || !table_grad) return EEGF_ERR_ARG;
   const dim3 grid((unsigned)((rows + 3) / 4));
   if (dtype == EEGF_F32)
-    hipLaunchKernelGGL(scatter_add_kernel<float>, grid, dim3(256), 0, stream, ids, (const float*)d, width, rows, table_grad);
+    EEGF_LAUNCH(scatter_add_kernel<float>, grid, dim3(256), 0, stream, ids, (const float*)d, width, rows, table_grad);
   else if (dtype == EEGF_BF16)
-    hipLaunchKernelGGL(scatter_add_kernel<bf16>, grid, dim3(256), 0, stream, ids, (const bf16*)d, width, rows, table_grad);
+    EEGF_LAUNCH(scatter_add_kernel<bf16>, grid, dim3(256), 0, stream, ids, (const bf16*)d, width, rows, table_grad);
   else return EEGF_ERR_ARG;
   return (int)hipGetLastError();
 }

@@ -9,14 +9,18 @@
 //              out = y*m0 + y*m1                                                   past_acc.py:130-136
 //   PriConcat: DP_guarantee(f, eps, dp_mode) — identity as ConcatModel.forward calls it
 //              (main_0430.py:118), or 'feature_all_lap': minmax + one Laplace(0,1/eps) per row.
-// One 256-thread workgroup per sample row; the Laplace/Gumbel draws come from Philox(seed,
-// offset, element) unless injected (parity mode), and are regenerated in the backward.
+// One 768-thread workgroup (12 waves) per sample row, thread t owning features t, 768 + t and 1536 + t
+// (one element of each encoder's row: three coalesced row reads, no branch); the Laplace/Gumbel draws
+// come from Philox(seed, offset, element) unless injected (parity mode), and are regenerated in the
+// backward.  Round 5 ran 256 threads x 9 elements: one wave per SIMD with nine serial Philox + log
+// chains per lane, 19-20 us per launch at B = 256 (latency-bound, ~0.35 TB/s).
 #include "common.h"
 #include "eegfusion_internal.h"
 
 namespace {
 
-constexpr int D3 = 2304, D1 = 768, PER = D3 / 256;  // 9 features per thread
+constexpr int D3 = 2304, D1 = 768;
+constexpr int FT = 768, FW = FT / 64, PER = D3 / FT;  // fusion kernels: 768 threads, 12 waves, 3 features each
 
 struct FusionArgs {
   const void* pooled; const void* img; const void* cross; long ld_pooled, ld_img, ld_cross;
@@ -95,10 +99,12 @@ DEV GateVals gate(const FusionArgs& a, int b, int j) {
   return v;
 }
 
-// block argmin/argmax (first index on ties)
+// block argmin/argmax (first index on ties: the (value, index) order is total, so the result does
+// not depend on the reduction order); NW waves
+template <int NW = 4>
 DEV void block_minmax(float& vmin, int& imin, float& vmax, int& imax) {
-  __shared__ float smin[4], smax[4];
-  __shared__ int simin[4], simax[4];
+  __shared__ float smin[NW], smax[NW];
+  __shared__ int simin[NW], simax[NW];
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const float om = __shfl_xor(vmin, o, 64), oM = __shfl_xor(vmax, o, 64);
@@ -110,29 +116,33 @@ DEV void block_minmax(float& vmin, int& imin, float& vmax, int& imax) {
   if ((threadIdx.x & 63) == 0) { smin[wave] = vmin; simin[wave] = imin; smax[wave] = vmax; simax[wave] = imax; }
   __syncthreads();
   vmin = smin[0]; imin = simin[0]; vmax = smax[0]; imax = simax[0];
-  for (int w = 1; w < 4; ++w) {
+  for (int w = 1; w < NW; ++w) {
     if (smin[w] < vmin || (smin[w] == vmin && simin[w] < imin)) { vmin = smin[w]; imin = simin[w]; }
     if (smax[w] > vmax || (smax[w] == vmax && simax[w] < imax)) { vmax = smax[w]; imax = simax[w]; }
   }
 }
 
+template <int NW = 4>
 DEV float block_sum(float v, float* red) {
   v = wave_sum(v);
   __syncthreads();
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
-  return red[0] + red[1] + red[2] + red[3];
+  float s = red[0];
+#pragma unroll
+  for (int w = 1; w < NW; ++w) s += red[w];
+  return s;
 }
 
 template <typename T>
-__global__ void __launch_bounds__(256) fusion_fwd_kernel(FusionArgs a) {
+__global__ void __launch_bounds__(FT) fusion_fwd_kernel(FusionArgs a) {
   const int b = blockIdx.x, tid = threadIdx.x;
   float x[PER];
   float vmin = 3.4e38f, vmax = -3.4e38f;
   int imin = 0x7fffffff, imax = 0x7fffffff;
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
-    const int j = tid + 256 * k;
+    const int j = tid + FT * k;
     x[k] = feat<T>(a, b, j);
     if (x[k] < vmin) { vmin = x[k]; imin = j; }
     if (x[k] > vmax) { vmax = x[k]; imax = j; }
@@ -140,16 +150,16 @@ __global__ void __launch_bounds__(256) fusion_fwd_kernel(FusionArgs a) {
   T* out = (T*)a.out + (long)b * D3;
   if (a.variant == FUSE_PRICONCAT) {                      // DP_guarantee(dp_mode=None): identity
 #pragma unroll
-    for (int k = 0; k < PER; ++k) out[tid + 256 * k] = from_f32<T>(x[k]);
+    for (int k = 0; k < PER; ++k) out[tid + FT * k] = from_f32<T>(x[k]);
     return;
   }
-  block_minmax(vmin, imin, vmax, imax);
+  block_minmax<FW>(vmin, imin, vmax, imax);
   const float R = vmax - vmin;
   if (tid == 0 && a.amin) { a.amin[b] = imin; a.amax[b] = imax; a.range[b] = R; }
   const float rn = a.variant == FUSE_PRICONCAT_LAP ? row_laplace(a, b) : 0.f;
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
-    const int j = tid + 256 * k;
+    const int j = tid + FT * k;
     const float xn = (x[k] - vmin) / R;
     if (a.xn) a.xn[(long)b * D3 + j] = xn;
     float o;
@@ -167,15 +177,15 @@ __global__ void __launch_bounds__(256) fusion_fwd_kernel(FusionArgs a) {
 }
 
 template <typename T>
-__global__ void __launch_bounds__(256) fusion_bwd_kernel(FusionArgs a) {
-  __shared__ float red[4];
+__global__ void __launch_bounds__(FT) fusion_bwd_kernel(FusionArgs a) {
+  __shared__ float red[FW];
   const int b = blockIdx.x, tid = threadIdx.x;
   const T* dout = (const T*)a.dout + (long)b * D3;
   float dxn[PER], xn[PER];
   float s1 = 0.f, s2 = 0.f;
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
-    const int j = tid + 256 * k;
+    const int j = tid + FT * k;
     const float d = to_f32(dout[j]);
     if (a.variant == FUSE_PRIGUMBEL) {
       const GateVals g = gate(a, b, j);
@@ -206,15 +216,15 @@ __global__ void __launch_bounds__(256) fusion_bwd_kernel(FusionArgs a) {
   float R = 1.f;
   int imin = -1, imax = -1;
   if (a.variant != FUSE_PRICONCAT) {
-    s1 = block_sum(s1, red);
-    s2 = block_sum(s2, red);
+    s1 = block_sum<FW>(s1, red);
+    s2 = block_sum<FW>(s2, red);
     R = a.range[b];
     imin = a.amin[b];
     imax = a.amax[b];
   }
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
-    const int j = tid + 256 * k;
+    const int j = tid + FT * k;
     float dx = dxn[k] / R;
     if (j == imin) dx += s1 / R;
     if (j == imax) dx -= s2 / R;
@@ -424,8 +434,8 @@ extern "C" int eegf_fusion_fwd(int dtype, int B, int variant, const void* pooled
   a.hard = hard; a.eps_mode = eps_mode; a.eps_a = eps_a; a.lap_scale = lap_scale; a.tau = 1.0f;
   a.seed = seed; a.offset = offset; a.out = out; a.xn = xn; a.amin = amin; a.amax = amax; a.range = range;
   if (variant != FUSE_PRICONCAT && (!amin || !amax || !range)) return EEGF_ERR_ARG;
-  if (dtype == EEGF_F32) hipLaunchKernelGGL(fusion_fwd_kernel<float>, dim3(B), dim3(256), 0, stream, a);
-  else if (dtype == EEGF_BF16) hipLaunchKernelGGL(fusion_fwd_kernel<bf16>, dim3(B), dim3(256), 0, stream, a);
+  if (dtype == EEGF_F32) EEGF_LAUNCH(fusion_fwd_kernel<float>, dim3(B), dim3(FT), 0, stream, a);
+  else if (dtype == EEGF_BF16) EEGF_LAUNCH(fusion_fwd_kernel<bf16>, dim3(B), dim3(FT), 0, stream, a);
   else return EEGF_ERR_ARG;
   return (int)hipGetLastError();
 }
@@ -445,8 +455,8 @@ extern "C" int eegf_fusion_bwd(int dtype, int B, int variant, const void* dout, 
   a.variant = variant; a.hard = hard; a.eps_mode = eps_mode; a.eps_a = eps_a; a.tau = 1.0f; a.seed = seed;
   a.offset = offset; a.d_pooled = d_pooled; a.ld_pooled = ld_pooled; a.d_img = d_img; a.ld_img = ld_img;
   a.d_cross = d_cross; a.ld_cross = ld_cross; a.ddp_rows = ddp_rows;
-  if (dtype == EEGF_F32) hipLaunchKernelGGL(fusion_bwd_kernel<float>, dim3(B), dim3(256), 0, stream, a);
-  else if (dtype == EEGF_BF16) hipLaunchKernelGGL(fusion_bwd_kernel<bf16>, dim3(B), dim3(256), 0, stream, a);
+  if (dtype == EEGF_F32) EEGF_LAUNCH(fusion_bwd_kernel<float>, dim3(B), dim3(FT), 0, stream, a);
+  else if (dtype == EEGF_BF16) EEGF_LAUNCH(fusion_bwd_kernel<bf16>, dim3(B), dim3(FT), 0, stream, a);
   else return EEGF_ERR_ARG;
   return (int)hipGetLastError();
 }
@@ -456,10 +466,10 @@ extern "C" int eegf_cross_entropy(int dtype, int B, int C, const void* logits, c
                                   hipStream_t stream) {
   if (B <= 0 || C <= 0 || C > 64 || !logits || !labels) return EEGF_ERR_ARG;
   if (dtype == EEGF_F32)
-    hipLaunchKernelGGL(ce_kernel<float>, dim3(1), dim3(256), 0, stream, (const float*)logits, labels, B, C, reduction,
+    EEGF_LAUNCH(ce_kernel<float>, dim3(1), dim3(256), 0, stream, (const float*)logits, labels, B, C, reduction,
                        dscale, loss, correct, (float*)dlogits);
   else if (dtype == EEGF_BF16)
-    hipLaunchKernelGGL(ce_kernel<bf16>, dim3(1), dim3(256), 0, stream, (const bf16*)logits, labels, B, C, reduction,
+    EEGF_LAUNCH(ce_kernel<bf16>, dim3(1), dim3(256), 0, stream, (const bf16*)logits, labels, B, C, reduction,
                        dscale, loss, correct, (bf16*)dlogits);
   else return EEGF_ERR_ARG;
   return (int)hipGetLastError();
@@ -474,7 +484,7 @@ extern "C" int eegf_v1_gate_fwd(int B, const float* x, long ldx, const float* w,
   a.pooled = x; a.ld_pooled = ldx; a.DP = w; a.gumbels = gumbels; a.row_noise = row_noise; a.B = B; a.hard = hard;
   a.tau = tau; a.lap_scale = lap_scale; a.seed = seed; a.offset = offset; a.out = out; a.xn = xn; a.amin = amin;
   a.amax = amax; a.range = range;
-  hipLaunchKernelGGL(v1_fwd_kernel, dim3(B), dim3(256), 0, stream, a);
+  EEGF_LAUNCH(v1_fwd_kernel, dim3(B), dim3(256), 0, stream, a);
   return (int)hipGetLastError();
 }
 
@@ -488,21 +498,21 @@ extern "C" int eegf_v1_gate_bwd(int B, const float* dout, const float* x, long l
   a.dout = dout; a.pooled = x; a.ld_pooled = ldx; a.DP = w; a.gumbels = gumbels; a.xn = const_cast<float*>(xn);
   a.amin = const_cast<int*>(amin); a.amax = const_cast<int*>(amax); a.range = const_cast<float*>(range); a.B = B;
   a.hard = hard; a.tau = tau; a.seed = seed; a.offset = offset; a.d_pooled = dx; a.ddp_rows = dw_rows;
-  hipLaunchKernelGGL(v1_bwd_kernel, dim3(B), dim3(256), 0, stream, a);
+  EEGF_LAUNCH(v1_bwd_kernel, dim3(B), dim3(256), 0, stream, a);
   return (int)hipGetLastError();
 }
 
 extern "C" int eegf_v1_wloss(int D, const float* w, float eps_a, float dscale, float* loss, float* dw,
                              hipStream_t stream) {
   if (D <= 0 || !w) return EEGF_ERR_ARG;
-  hipLaunchKernelGGL(v1_wloss_kernel, dim3(1), dim3(256), 0, stream, D, w, eps_a, dscale, loss, dw);
+  EEGF_LAUNCH(v1_wloss_kernel, dim3(1), dim3(256), 0, stream, D, w, eps_a, dscale, loss, dw);
   return (int)hipGetLastError();
 }
 
 extern "C" int eegf_feawei_init(int D, const float* colsum, long count, float k, int zscore, const float* base,
                                 float* dp, hipStream_t stream) {
   if (D <= 0 || count <= 0 || !colsum || !base || !dp) return EEGF_ERR_ARG;
-  hipLaunchKernelGGL(feawei_kernel, dim3(1), dim3(256), 0, stream, D, colsum, 1.0 / (double)count, k, zscore,
+  EEGF_LAUNCH(feawei_kernel, dim3(1), dim3(256), 0, stream, D, colsum, 1.0 / (double)count, k, zscore,
                      base, dp);
   return (int)hipGetLastError();
 }

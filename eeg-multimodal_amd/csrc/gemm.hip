@@ -66,8 +66,15 @@ struct TileCfg {
   static constexpr int RS_KC = KT + VE;
   // k-major LDS tile: [KT rows][BT] + 32 B pad per row
   static constexpr int RS_KM = BT + 2 * VE;
+  // fp32 k-major tiles: rows 8 apart (the four 16-lane groups of an fp32 ld_col8) would sit a multiple
+  // of 64 banks apart (8 x 72 / 8 x 136 words: 4-way conflicts, 0.33-0.44 of LDS cycles in the round-5
+  // counters), so every block of 8 rows is shifted by 16 more words: the four groups land on disjoint
+  // 16-bank quarters.  The shift keeps every 16-B row chunk aligned.  bf16 tiles read through
+  // ds_read_b64_tr_b16 and keep the plain layout.
+  static constexpr int SKEW = sizeof(T) == 4 ? 16 : 0;
+  static DEV int skew(int krow) { return SKEW * ((krow >> 3) & 3); }
   static constexpr int SZ_KC = BT * RS_KC;
-  static constexpr int SZ_KM = KT * RS_KM;
+  static constexpr int SZ_KM = KT * RS_KM + 3 * SKEW;
   static constexpr int CHUNKS = BT * 8 / NT;             // 16-B chunks per thread per operand tile
 };
 
@@ -112,7 +119,7 @@ DEV void store_tile(T* lds, const u32x4* reg, int tid) {
     int r, col;
     if (KC) { r = c >> 3; col = (c & 7) * C::VE; }
     else    { constexpr int CPR = BT / C::VE; r = c / CPR; col = (c % CPR) * C::VE; }
-    st16(lds + r * (KC ? C::RS_KC : C::RS_KM) + col, reg[i]);
+    st16(lds + (KC ? r * C::RS_KC : r * C::RS_KM + C::skew(r)) + col, reg[i]);
   }
 }
 
@@ -173,13 +180,13 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmArgs g) {
       for (int i = 0; i < NI; ++i) {
         const int r = wm * WT + i * 16;
         if (AKC) a[i] = ld_row8(As + (r + (lane & 15)) * C::RS_KC + kk);
-        else     a[i] = ld_col8(As, C::RS_KM, kk, r, lane);
+        else     a[i] = ld_col8(As + C::skew(kk), C::RS_KM, kk, r, lane);
       }
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
         const int c = wn * WT + j * 16;
         if (BKC) b[j] = ld_row8(Bs + (c + (lane & 15)) * C::RS_KC + kk);
-        else     b[j] = ld_col8(Bs, C::RS_KM, kk, c, lane);
+        else     b[j] = ld_col8(Bs + C::skew(kk), C::RS_KM, kk, c, lane);
       }
 #pragma unroll
       for (int i = 0; i < NI; ++i)
@@ -397,7 +404,7 @@ template <typename TO>
 int splitk_reduce_t(int epi, const float* ws, int splits, int M, int N, void* C, long ldc, float beta,
                     const float* bias, void* aux, long ldaux, float scale, hipStream_t st) {
   const dim3 grid((unsigned)(((long)M * N + 255) / 256));
-#define RED(E) hipLaunchKernelGGL((gemm_splitk_reduce<TO, E>), grid, dim3(256), 0, st, ws, splits, M, N, (TO*)C, ldc, \
+#define RED(E) EEGF_LAUNCH((gemm_splitk_reduce<TO, E>), grid, dim3(256), 0, st, ws, splits, M, N, (TO*)C, ldc, \
                                   beta, bias, (TO*)aux, ldaux, scale)
   switch (epi) {
     case EPI_NONE: RED(EPI_NONE); break;
@@ -428,10 +435,10 @@ template <typename T, bool AKC, bool BKC, typename TO, int EPI>
 int launch(const GemmArgs& a, int batch, hipStream_t s, int splits = 1) {
   if (a.bt == 64) {
     const int tiles = ((a.M + 63) / 64) * ((a.N + 63) / 64);
-    hipLaunchKernelGGL((gemm_kernel<T, AKC, BKC, TO, EPI, 64>), dim3(tiles, batch, splits), dim3(NT), 0, s, a);
+    EEGF_LAUNCH((gemm_kernel<T, AKC, BKC, TO, EPI, 64>), dim3(tiles, batch, splits), dim3(NT), 0, s, a);
   } else {
     const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-    hipLaunchKernelGGL((gemm_kernel<T, AKC, BKC, TO, EPI>), dim3(tiles, batch, splits), dim3(NT), 0, s, a);
+    EEGF_LAUNCH((gemm_kernel<T, AKC, BKC, TO, EPI>), dim3(tiles, batch, splits), dim3(NT), 0, s, a);
   }
   return (int)hipGetLastError();
 }
@@ -543,7 +550,7 @@ static int gemm_impl(int dtype, int out_dtype, int a_kcontig, int b_kcontig, int
                        : launch<float, false, false, float, EPI_NONE>(b, batch, stream, splits);
         if (st) return st;
         const dim3 grid((unsigned)(((long)batch * M * N + 255) / 256));
-        hipLaunchKernelGGL(gemm_splitk_reduce_batched<float>, grid, dim3(256), 0, stream, (const float*)workspace,
+        EEGF_LAUNCH(gemm_splitk_reduce_batched<float>, grid, dim3(256), 0, stream, (const float*)workspace,
                            splits, batch, M, N, (float*)C, ldc, strideC, beta);
         return (int)hipGetLastError();
       }

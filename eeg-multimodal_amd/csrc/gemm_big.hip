@@ -2193,16 +2193,16 @@ int launch_big(const BigArgs& a, int splits, hipStream_t s) {
       const bool r = q && g_gemm4r;
       if (acc) {
         if constexpr (EPI == EPI_NONE) {
-          if (r) hipLaunchKernelGGL((gemm4r_kernel<BKC, EPI, true>), grid, dim3(NT4), 0, s, ap);
-          else if (q) hipLaunchKernelGGL((gemm4q_kernel<BKC, EPI, true>), grid, dim3(NT4), 0, s, ap);
-          else hipLaunchKernelGGL((gemm4p_kernel<BKC, EPI, true>), grid, dim3(NT4), 0, s, ap);
+          if (r) EEGF_LAUNCH((gemm4r_kernel<BKC, EPI, true>), grid, dim3(NT4), 0, s, ap);
+          else if (q) EEGF_LAUNCH((gemm4q_kernel<BKC, EPI, true>), grid, dim3(NT4), 0, s, ap);
+          else EEGF_LAUNCH((gemm4p_kernel<BKC, EPI, true>), grid, dim3(NT4), 0, s, ap);
         }
       } else if (r) {
-        hipLaunchKernelGGL((gemm4r_kernel<BKC, EPI>), grid, dim3(NT4), 0, s, ap);
+        EEGF_LAUNCH((gemm4r_kernel<BKC, EPI>), grid, dim3(NT4), 0, s, ap);
       } else if (q) {
-        hipLaunchKernelGGL((gemm4q_kernel<BKC, EPI>), grid, dim3(NT4), 0, s, ap);
+        EEGF_LAUNCH((gemm4q_kernel<BKC, EPI>), grid, dim3(NT4), 0, s, ap);
       } else {
-        hipLaunchKernelGGL((gemm4p_kernel<BKC, EPI>), grid, dim3(NT4), 0, s, ap);
+        EEGF_LAUNCH((gemm4p_kernel<BKC, EPI>), grid, dim3(NT4), 0, s, ap);
       }
       return (int)hipGetLastError();
     }
@@ -2216,7 +2216,7 @@ int launch_big(const BigArgs& a, int splits, hipStream_t s) {
     // weight gradients and on K >= 2048 (K-loop-bound; at K = 768 its unoverlapped epilogue loses)
     if (sizeof(TO) == 4 ? (!AKC && !BKC) : a.K >= 2048) {
       if (!a.colsum_part) {
-        hipLaunchKernelGGL((gemm4w_kernel<AKC, BKC, EPI, TO>), dim3(tiles, splits), dim3(NT4), 0, s, a);
+        EEGF_LAUNCH((gemm4w_kernel<AKC, BKC, EPI, TO>), dim3(tiles, splits), dim3(NT4), 0, s, a);
         return (int)hipGetLastError();
       }
     }
@@ -2227,36 +2227,36 @@ int launch_big(const BigArgs& a, int splits, hipStream_t s) {
       const bool h_ok = g_gemm4h == 1 || (g_gemm4h == 2 && a.N <= 768);
       if (h_ok && splits == 1 && !a.colsum_part && a.K < 2048 && a.K % BK4 == 0 && a.N >= 128) {
         const int tiles_h = ((a.M + TM - 1) / TM) * ((a.N + TNH - 1) / TNH);
-        hipLaunchKernelGGL((gemm4h_kernel<BKC, EPI>), dim3(tiles_h), dim3(NT4), 0, s, a);
+        EEGF_LAUNCH((gemm4h_kernel<BKC, EPI>), dim3(tiles_h), dim3(NT4), 0, s, a);
         return (int)hipGetLastError();
       }
     }
     if (use8) {
       if constexpr (AKC && !BKC && sizeof(TO) == 2) {
         if (a.colsum_part) {
-          hipLaunchKernelGGL((gemm8_kernel<AKC, BKC, EPI, TO, true>), dim3(tiles, splits), dim3(NT), 0, s, a);
+          EEGF_LAUNCH((gemm8_kernel<AKC, BKC, EPI, TO, true>), dim3(tiles, splits), dim3(NT), 0, s, a);
           return (int)hipGetLastError();
         }
       }
       if (!a.colsum_part) {
-        hipLaunchKernelGGL((gemm8_kernel<AKC, BKC, EPI, TO>), dim3(tiles, splits), dim3(NT), 0, s, a);
+        EEGF_LAUNCH((gemm8_kernel<AKC, BKC, EPI, TO>), dim3(tiles, splits), dim3(NT), 0, s, a);
         return (int)hipGetLastError();
       }
     }
   } else if ((g_gemm8 == 4 || g_gemm8 == 6) && !a.colsum_part) {
     const dim3 grid(tiles, splits);
-    if (g_gemm8 == 4) hipLaunchKernelGGL((gemm8_kernel<AKC, BKC, EPI, TO>), grid, dim3(NT), 0, s, a);
-    else hipLaunchKernelGGL((gemm4w_kernel<AKC, BKC, EPI, TO>), grid, dim3(NT4), 0, s, a);
+    if (g_gemm8 == 4) EEGF_LAUNCH((gemm8_kernel<AKC, BKC, EPI, TO>), grid, dim3(NT), 0, s, a);
+    else EEGF_LAUNCH((gemm4w_kernel<AKC, BKC, EPI, TO>), grid, dim3(NT4), 0, s, a);
     return (int)hipGetLastError();
   }
   if constexpr (AKC && !BKC && sizeof(TO) == 2) {
     if (a.colsum_part) {
-      hipLaunchKernelGGL((gemm_big_kernel<AKC, BKC, EPI, TO, true>), dim3(tiles, splits), dim3(NT), 0, s, a);
+      EEGF_LAUNCH((gemm_big_kernel<AKC, BKC, EPI, TO, true>), dim3(tiles, splits), dim3(NT), 0, s, a);
       return (int)hipGetLastError();
     }
   }
   if (a.colsum_part) return EEGF_ERR_ARG;
-  hipLaunchKernelGGL((gemm_big_kernel<AKC, BKC, EPI, TO>), dim3(tiles, splits), dim3(NT), 0, s, a);
+  EEGF_LAUNCH((gemm_big_kernel<AKC, BKC, EPI, TO>), dim3(tiles, splits), dim3(NT), 0, s, a);
   return (int)hipGetLastError();
 }
 
@@ -2338,16 +2338,16 @@ int eegf_gemm_big_wgrad_bias(int M, int N, int K, const void* A, long lda, const
   BigArgs a{(const bf16*)A, (const bf16*)B, splits > 1 ? (void*)slabs : (void*)C, nullptr, nullptr, lda, ldb, ldc, 0,
             M, N, K, 1.0f, beta, 1.0f, splits > 1 ? ks : 0, nullptr, part, g_ts_buf, group_for(N)};
   const int tiles = ((M + TM - 1) / TM) * ((N + TN - 1) / TN);
-  hipLaunchKernelGGL((gemm4w_kernel<false, false, EPI_NONE, float, true>), dim3(tiles, splits), dim3(NT4), 0,
+  EEGF_LAUNCH((gemm4w_kernel<false, false, EPI_NONE, float, true>), dim3(tiles, splits), dim3(NT4), 0,
                      stream, a);
   const int nrow = (M + 255) / 256;
   if (splits > 1) {
     const long MN = (long)M * N;
     const int nslab = (int)((MN / 4 + 255) / 256);
-    hipLaunchKernelGGL(splitk_rowsum_reduce, dim3((unsigned)(nslab + nrow)), dim3(256), 0, stream, (const float*)slabs,
+    EEGF_LAUNCH(splitk_rowsum_reduce, dim3((unsigned)(nslab + nrow)), dim3(256), 0, stream, (const float*)slabs,
                        splits, MN, N, C, ldc, beta, nslab, (const float*)part, M, db);
   } else {
-    hipLaunchKernelGGL(rowsum_reduce, dim3((unsigned)nrow), dim3(256), 0, stream, (const float*)part, splits, M, db);
+    EEGF_LAUNCH(rowsum_reduce, dim3((unsigned)nrow), dim3(256), 0, stream, (const float*)part, splits, M, db);
   }
   return (int)hipGetLastError();
 }
@@ -2376,7 +2376,7 @@ int eegf_gemm_big(int a_kc, int b_kc, int epi, int out_f32, int M, int N, int K,
     const int st = launch_big<false, false, EPI_NONE, float>(a, splits, stream);
     if (st) return st;
     const long MN = (long)M * N;
-    hipLaunchKernelGGL(big_splitk_reduce, dim3((unsigned)((MN / 4 + 255) / 256)), dim3(256), 0, stream,
+    EEGF_LAUNCH(big_splitk_reduce, dim3((unsigned)((MN / 4 + 255) / 256)), dim3(256), 0, stream,
                        (const float*)workspace, splits, MN, N, (float*)C, ldc, beta);
     return (int)hipGetLastError();
   }

@@ -443,9 +443,9 @@ int colsum_t(const void* in, long ld, long rows, int width, int period, float* w
   if (chunks * width > ws_elems) return EEGF_ERR_ARG;
   const long rpc = (rows + chunks - 1) / chunks;
   chunks = (rows + rpc - 1) / rpc;
-  if (vec) hipLaunchKernelGGL(colsum_chunks<T>, dim3(xblocks, (unsigned)chunks), dim3(256), 0, st, (const T*)in, ld, rows, width, rpc, ws);
-  else hipLaunchKernelGGL(colsum_scalar<T>, dim3(xblocks, (unsigned)chunks), dim3(256), 0, st, (const T*)in, ld, rows, width, rpc, ws);
-  hipLaunchKernelGGL(colsum_combine, dim3((width + 63) / 64), dim3(64 * CW), 0, st, ws, (int)chunks, width, out, beta);
+  if (vec) EEGF_LAUNCH(colsum_chunks<T>, dim3(xblocks, (unsigned)chunks), dim3(256), 0, st, (const T*)in, ld, rows, width, rpc, ws);
+  else EEGF_LAUNCH(colsum_scalar<T>, dim3(xblocks, (unsigned)chunks), dim3(256), 0, st, (const T*)in, ld, rows, width, rpc, ws);
+  EEGF_LAUNCH(colsum_combine, dim3((width + 63) / 64), dim3(64 * CW), 0, st, ws, (int)chunks, width, out, beta);
   return (int)hipGetLastError();
 }
 
@@ -453,10 +453,10 @@ template <typename T>
 int ln_fwd_t(int nch, const LnFwdArgs& a, hipStream_t st) {
   const dim3 grid((unsigned)((a.rows + 4L * a.rpw - 1) / (4L * a.rpw)));
   switch (nch) {
-    case 1: hipLaunchKernelGGL((ln_fwd_kernel<T, 1>), grid, dim3(256), 0, st, a); break;
-    case 2: hipLaunchKernelGGL((ln_fwd_kernel<T, 2>), grid, dim3(256), 0, st, a); break;
-    case 3: hipLaunchKernelGGL((ln_fwd_kernel<T, 3>), grid, dim3(256), 0, st, a); break;
-    case 4: hipLaunchKernelGGL((ln_fwd_kernel<T, 4>), grid, dim3(256), 0, st, a); break;
+    case 1: EEGF_LAUNCH((ln_fwd_kernel<T, 1>), grid, dim3(256), 0, st, a); break;
+    case 2: EEGF_LAUNCH((ln_fwd_kernel<T, 2>), grid, dim3(256), 0, st, a); break;
+    case 3: EEGF_LAUNCH((ln_fwd_kernel<T, 3>), grid, dim3(256), 0, st, a); break;
+    case 4: EEGF_LAUNCH((ln_fwd_kernel<T, 4>), grid, dim3(256), 0, st, a); break;
     default: return EEGF_ERR_ARG;
   }
   return (int)hipGetLastError();
@@ -466,10 +466,10 @@ template <typename T>
 int ln_bwd_t(int nch, const LnBwdArgs& a, hipStream_t st) {
   const dim3 grid((unsigned)((a.rows + a.rows_per_block - 1) / a.rows_per_block));
   switch (nch) {
-    case 1: hipLaunchKernelGGL((ln_bwd_kernel<T, 1>), grid, dim3(256), 0, st, a); break;
-    case 2: hipLaunchKernelGGL((ln_bwd_kernel<T, 2>), grid, dim3(256), 0, st, a); break;
-    case 3: hipLaunchKernelGGL((ln_bwd_kernel<T, 3>), grid, dim3(256), 0, st, a); break;
-    case 4: hipLaunchKernelGGL((ln_bwd_kernel<T, 4>), grid, dim3(256), 0, st, a); break;
+    case 1: EEGF_LAUNCH((ln_bwd_kernel<T, 1>), grid, dim3(256), 0, st, a); break;
+    case 2: EEGF_LAUNCH((ln_bwd_kernel<T, 2>), grid, dim3(256), 0, st, a); break;
+    case 3: EEGF_LAUNCH((ln_bwd_kernel<T, 3>), grid, dim3(256), 0, st, a); break;
+    case 4: EEGF_LAUNCH((ln_bwd_kernel<T, 4>), grid, dim3(256), 0, st, a); break;
     default: return EEGF_ERR_ARG;
   }
   return (int)hipGetLastError();
@@ -554,7 +554,7 @@ __global__ void __launch_bounds__(256) colsum_batch_kernel(const long long* __re
 
 extern "C" int eegf_colsum_batch(int n, const long long* desc, int blocks, hipStream_t stream) {
   if (n <= 0 || !desc || blocks <= 0) return EEGF_ERR_ARG;
-  hipLaunchKernelGGL(colsum_batch_kernel, dim3(blocks), dim3(256), 0, stream, desc, n);
+  EEGF_LAUNCH(colsum_batch_kernel, dim3(blocks), dim3(256), 0, stream, desc, n);
   return (int)hipGetLastError();
 }
 
@@ -575,7 +575,7 @@ extern "C" int eegf_ln_fwd(int dtype, long rows, int width, const void* x, const
       ((((uintptr_t)x | (uintptr_t)r | (uintptr_t)y | (uintptr_t)s_out | (uintptr_t)table | (uintptr_t)table2 |
          (uintptr_t)gamma | (uintptr_t)beta) & 15) == 0)) {
     const dim3 grid((unsigned)((a.rows + 4L * a.rpw - 1) / (4L * a.rpw)));
-    hipLaunchKernelGGL(ln_fwd768_kernel, grid, dim3(256), 0, stream, a);
+    EEGF_LAUNCH(ln_fwd768_kernel, grid, dim3(256), 0, stream, a);
     return (int)hipGetLastError();
   }
   if (dtype == EEGF_BF16) return ln_fwd_t<bf16>(width / 256, a, stream);

@@ -79,7 +79,7 @@ extern "C" int eegf_adam(long n, float* p, const float* g, float* m, float* v, v
   const double bc1 = 1.0 - pow((double)beta1, step), bc2 = 1.0 - pow((double)beta2, step);
   const float step_size = (float)(lr / bc1), sqrt_bc2 = (float)sqrt(bc2);
   const long blocks = (n + 1023) / 1024;
-  hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, n, p, g, m, v, (bf16*)bf16_shadow,
+  EEGF_LAUNCH(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, n, p, g, m, v, (bf16*)bf16_shadow,
                      beta1, beta2, eps, weight_decay, grad_scale, step_size, sqrt_bc2);
   return (int)hipGetLastError();
 }
@@ -87,12 +87,12 @@ extern "C" int eegf_adam(long n, float* p, const float* g, float* m, float* v, v
 extern "C" int eegf_cast_f32_bf16(long n, const float* src, void* dst, hipStream_t stream) {
   if (n <= 0 || !src || !dst) return EEGF_ERR_ARG;
   if ((((uintptr_t)src) & 15) != 0 || (((uintptr_t)dst) & 7) != 0) return EEGF_ERR_ARG;
-  hipLaunchKernelGGL(cast_kernel, dim3((unsigned)((n + 1023) / 1024)), dim3(256), 0, stream, n, src, (bf16*)dst);
+  EEGF_LAUNCH(cast_kernel, dim3((unsigned)((n + 1023) / 1024)), dim3(256), 0, stream, n, src, (bf16*)dst);
   return (int)hipGetLastError();
 }
 
 extern "C" int eegf_key_bias(long n, const long long* mask, float* bias, hipStream_t stream) {
   if (n <= 0 || !mask || !bias) return EEGF_ERR_ARG;
-  hipLaunchKernelGGL(key_bias_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, n, mask, bias);
+  EEGF_LAUNCH(key_bias_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, n, mask, bias);
   return (int)hipGetLastError();
 }

@@ -45,6 +45,8 @@ SIGNATURES: dict[str, list] = {
     "eegf_tune": [i32, i32],
     "eegf_gemm_big_timestamps": [vp],
     "eegf_ring_proxy": [i64, i32, i32, vp, vp],
+    "eegf_launch_log_reset": [],
+    "eegf_launch_log_read": [vp, i64],
     "eegf_ln_fwd": [i32, i64, i32, vp, vp, vp, i32, vp, vp, vp, f32, f32, i32, u64, u64, vp, vp, vp, vp, vp],
     "eegf_ln_bwd_partial_rows": [i64],
     "eegf_ln_bwd": [i32, i64, i32, vp, vp, vp, vp, vp, f32, i32, u64, u64, vp, vp, vp, vp, vp],
@@ -84,7 +86,7 @@ SIGNATURES: dict[str, list] = {
     "eegf_dp_noise": [i64, vp, f32, f32, u64, u64, vp],
 }
 RESTYPE_LONG = {"eegf_ln_bwd_partial_rows", "eegf_attn_bwd_workspace", "eegf_ghost_norm_workspace",
-                "eegf_attn_varlen_bwd_workspace"}
+                "eegf_attn_varlen_bwd_workspace", "eegf_launch_log_read"}
 
 
 def register(name: str, argtypes: list) -> None:
@@ -111,6 +113,18 @@ def call(name: str, *args) -> None:
     if st != 0:
         raise RuntimeError(f"{name} failed with status {st}"
                            + (" (argument error)" if st == ERR_ARG else " (hipError)"))
+
+
+def launch_counts() -> dict[str, int]:
+    """kernel name -> launches since load or the last eegf_launch_log_reset (the library's own counters)"""
+    n = lib().eegf_launch_log_read(None, 0)
+    buf = C.create_string_buffer(int(n))
+    lib().eegf_launch_log_read(buf, n)
+    out = {}
+    for line in buf.value.decode().splitlines():
+        cnt, name = line.split("\t", 1)
+        out[name] = out.get(name, 0) + int(cnt)
+    return out
 
 
 def exported_symbols() -> list[str]:

@@ -57,13 +57,23 @@ def build(verbose: bool = False, jobs: int | None = None) -> Path:
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         objs = list(ex.map(lambda s: _compile(s, hdrs, verbose), srcs))
     if _needs(LIB_PATH, objs):
-        cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", str(LIB_PATH), *map(str, objs)]
+        # link to a temporary name; only a library that passed the lint is renamed into place, so a
+        # lint that fails or cannot run (missing llvm tools) never leaves an unchecked, up-to-date-looking
+        # LIB_PATH behind
+        tmp = LIB_PATH.with_name(LIB_PATH.name + ".tmp")
+        cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", str(tmp), *map(str, objs)]
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
+            tmp.unlink(missing_ok=True)
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
-        _lint(LIB_PATH)
+        try:
+            _lint(tmp)
+        except BaseException:
+            tmp.unlink(missing_ok=True)
+            raise
+        tmp.replace(LIB_PATH)
     return LIB_PATH
 
 
@@ -82,7 +92,7 @@ def _lint(lib: Path) -> None:
     spec.loader.exec_module(mod)
     findings, _ = mod.lint(lib)
     if findings:
-        bad = lib.with_name(lib.name + ".hazards")
+        bad = LIB_PATH.with_name(LIB_PATH.name + ".hazards")
         lib.replace(bad)
         head = "\n".join(f"  {f.kind}: {f.func} @0x{f.addr:x}: '{f.inst}' {f.states} state(s) after '{f.writer}'"
                           for f in findings[:10])

@@ -203,13 +203,14 @@ class FusionEngine:
         ev.record()
         return ev
 
-    def _ev_end(self, tag, ev, flops=0.0):
-        """probe[tag] gets (start, end, algorithmic FLOPs) of the launch just enqueued: HIP events on
-        the launch stream (torch's current stream, where every eegf_* call is enqueued)"""
+    def _ev_end(self, tag, ev, flops=0.0, nbytes=0.0):
+        """probe[tag] gets (start, end, algorithmic FLOPs, algorithmic HBM bytes) of the launch just
+        enqueued: HIP events on the launch stream (torch's current stream, where every eegf_* call is
+        enqueued)"""
         if ev is not None:
             e2 = torch.cuda.Event(enable_timing=True)
             e2.record()
-            self.probe[tag].append((ev, e2, flops))
+            self.probe[tag].append((ev, e2, flops, nbytes))
 
     def dgrad(self, dy, w, out, M, ldd=None, ldo=None, epi=_lib.EPI_NONE, aux=None, scale=1.0, beta=0.0,
               bias_grad=None, tag=None):
@@ -387,6 +388,13 @@ class FusionEngine:
         call("eegf_ln_fwd", _code(x), rows, HID, P(x), P(r), P(table), period, P(table2), P(self.F(pre + ".weight")),
              P(self.F(pre + ".bias")), float(eps), float(p), int(mode if p > 0 else 0), self.cfg.seed, rng, P(out),
              P(s), P(mean), P(rstd), _stream())
+
+    def _ln_bytes(self, rows, save):
+        """algorithmic bytes of a BERT-layer LayerNorm forward (dropout + residual + LN): the sublayer
+        output and the residual in, the normalised row out, and when saving for the backward the pre-LN
+        sum and the row mean / rstd; gamma / beta once"""
+        e = torch.empty((), dtype=self.dt).element_size()
+        return rows * HID * e * (3 + (1 if save else 0)) + (rows * 8 if save else 0) + 2 * HID * 4
 
     def ln_bwd(self, dy, s, mean, rstd, pre, rows, dx, dr, p=0.0, mode=0, rng=0):
         rpb = _lib.lib().eegf_ln_bwd_partial_rows(rows)
@@ -773,8 +781,10 @@ class FusionEngine:
                         ao, R, tag="ao_fwd")
             a1 = self.empty(R, HID)
             s1, m1, r1 = (self.empty(R, HID), self._f32(R), self._f32(R)) if save else (None, None, None)
+            ev = self._ev_start("ln_fwd768")
             self.ln_fwd(ao, h, pre + "attention.output.LayerNorm", R, a1, s1, m1, r1, 1e-12, pdrop, 1,
                         sv.rng + 10 + 3 * i)
+            self._ev_end("ln_fwd768", ev, 0.0, self._ln_bytes(R, save))
             # saved for the backward: gelu'(pre) (the DGELU epilogue becomes a multiply)
             ffgd = self.empty(R, FFN) if save else None
             ffact = self.empty(R, FFN) if save else self.ws.get("ffact", R * FFN, self.dt).view(R, FFN)
@@ -786,7 +796,9 @@ class FusionEngine:
                         tag="ffn2_fwd")
             h2 = self.empty(R, HID)
             s2, m2, r2 = (self.empty(R, HID), self._f32(R), self._f32(R)) if save else (None, None, None)
+            ev = self._ev_start("ln_fwd768")
             self.ln_fwd(fo, a1, pre + "output.LayerNorm", R, h2, s2, m2, r2, 1e-12, pdrop, 1, sv.rng + 11 + 3 * i)
+            self._ev_end("ln_fwd768", ev, 0.0, self._ln_bytes(R, save))
             if save:
                 layers.append(dict(h=h, qkv=qkv, ctx=ctx, lse=lse, bits=bits, a1=a1, ln1=(s1, m1, r1), ffgd=ffgd, ffact=ffact,
                                    ln2=(s2, m2, r2)))
@@ -877,11 +889,14 @@ class FusionEngine:
         rng_ = self._f32(B)
         inj = self.injected or {}
         eps_a = math.exp(cfg.eps)
+        ev = self._ev_start("fusion_fwd")
         call("eegf_fusion_fwd", F32, B, self.variant, P(pooled), pooled.stride(0), P(vis), vis.stride(0), P(cross),
              cross.stride(0),
              P(self.F("DP")) if "DP" in self.a.offsets else None, P(inj.get("noise")), P(inj.get("gumbels")),
              P(inj.get("row_noise")), int(hard), EPS_MODES.index(cfg.eps_mode), eps_a, 1.0 / cfg.eps,
              self.cfg.seed, rng + 200, P(g), P(xn), P(amin), P(amax), P(rng_), _stream())
+        # algorithmic bytes: the three fp32 feature rows in; xn and the gated row out; arg-min / max / range
+        self._ev_end("fusion_fwd", ev, 0.0, B * (3 * FUSED * 4 + 12) + FUSED * 4)
         z1 = self.eh(B, FUSED)
         self.linear(g, self.F("fc_layers.0.weight"), self.F("fc_layers.0.bias"), z1, B, epi=_lib.EPI_BIAS_RELU)
         z2 = self.eh(B, HID)
@@ -1168,10 +1183,13 @@ class FusionEngine:
         has_dp = "DP" in self.a.offsets and self.variant == _lib.FUSE_PRIGUMBEL and self.need("DP")
         ddp = self._f32(B, FUSED) if has_dp else None
         inj = fz["inj"]
+        ev = self._ev_start("fusion_bwd")
         call("eegf_fusion_bwd", F32, B, self.variant, P(dg), P(fz["xn"]), P(fz["amin"]), P(fz["amax"]),
              P(fz["range"]), P(self.F("DP")) if "DP" in self.a.offsets else None, P(inj.get("noise")),
              P(inj.get("gumbels")), int(hard), EPS_MODES.index(cfg.eps_mode), math.exp(cfg.eps),
              self.cfg.seed, rng + 200, P(dpooled), HID, P(dvis), HID, P(dcross), HID, P(ddp), _stream())
+        # dout and xn in, the three input-gradient rows out (+ the per-row DP gradient rows in pass 1)
+        self._ev_end("fusion_bwd", ev, 0.0, B * ((3 + (1 if has_dp else 0)) * FUSED * 4 + 12) + FUSED * 4)
         if has_dp:
             self.bgrad(ddp, "DP", B, FUSED)
         return dpooled, dvis, dcross

@@ -62,10 +62,13 @@ class FlatAdam:
             sh = a.shadow[self.lo:self.hi].data_ptr()
         for lo, hi in self.sub:
             o = lo - self.lo
+            ev = self.e._ev_start("adam")
             call("eegf_adam", hi - lo, a.master[lo:].data_ptr(), a.grad[lo:].data_ptr(), self.m[o:].data_ptr(),
                  self.v[o:].data_ptr(), None if sh is None else a.shadow[lo:].data_ptr(), float(self.lr),
                  float(self.betas[0]), float(self.betas[1]), float(self.eps), float(self.wd), float(grad_scale),
                  self.t, _s())
+            # master, gradient, m, v in; master, m, v out (+ the bf16 shadow): 28 (30) B per parameter
+            self.e._ev_end("adam", ev, 0.0, (hi - lo) * (28 + (2 if sh is not None else 0)))
 
 
 class GradReducer:
@@ -236,8 +239,11 @@ class PriGumbelTrainer:
     def _ce(self, logits, labels, i):
         B = logits.shape[0]
         dl = torch.empty_like(logits)
+        ev = self.e._ev_start("cross_entropy")
         call("eegf_cross_entropy", _lib.F32 if logits.dtype == torch.float32 else _lib.BF16, B, 2, logits.data_ptr(), labels.data_ptr(), 0, 1.0,
              self.loss[i:].data_ptr(), self.correct[i:].data_ptr(), dl.data_ptr(), _s())
+        # logits and int64 labels in, the logit gradients + loss / correct count out
+        self.e._ev_end("cross_entropy", ev, 0.0, 2 * logits.numel() * logits.element_size() + B * 8 + 8)
         return dl
 
     def step(self, batch: dict, labels: torch.Tensor):

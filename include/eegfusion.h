@@ -112,6 +112,14 @@ int eegf_gemm_big_timestamps(long long* buf);
  * the one-GPU overlap proxy of the gradient all-reduces (tools/overlap_proxy.py): `wgs`
  * workgroups read and rewrite x[0, n) unchanged `passes` times (n % 4 == 0, x 16-B aligned). */
 int eegf_ring_proxy(long n, int passes, int wgs, float* x, hipStream_t stream);
+/* Diagnostics (no reference counterpart): per-kernel launch counters.  Every kernel launch of the
+ * library is counted on the host (one entry per kernel template instantiation) from load time or the
+ * last reset.  eegf_launch_log_read writes "count<TAB>demangled kernel name\n" lines into buf (at most
+ * cap bytes, NUL-terminated; buf may be NULL) and returns the bytes the whole text needs, NUL
+ * included.  Process-global, like eegf_tune; the route-coverage test reads it
+ * (tests/test_production_gpu.py). */
+int eegf_launch_log_reset(void);
+long eegf_launch_log_read(char* buf, long cap);
 /* Rows of the a_colsum partial buffer eegf_gemm_acs writes for this shape (ceil(M/256)), or 0 when
  * the fused column sums are unavailable (needs bf16 in/out, K-contiguous A, M >= 2048, N >= 256,
  * K % 64 == 0, 8-aligned dims). */
@@ -122,8 +130,10 @@ int eegf_gemm_colsum_tiles(int dtype, int out_dtype, int a_kcontig, int M, int N
 /* Weight gradient of an nn.Linear with its bias gradient fused (autograd of F.linear, the weight and
  * bias grads of every BERT projection, modeling_bert.py:139-351): dW [M][N] = dY^T X + beta dW over
  * K tokens, db [M] += dY.sum(0).  dY [K][M] (row stride ldd) and X [K][N] (ldx) bf16; dW, db fp32.
- * The row sums ride on the weight-gradient kernel (summed on the VALU from the dY fragments the
- * workgroups of tile column 0 already hold, in the MFMA shadows) and are reduced in a fixed order.  workspace: fp32 split-K slabs
+ * The row sums ride on the weight-gradient kernel: the workgroups of tile column 0 run one
+ * v_mfma_f32_16x16x32_bf16 per 16-row block and K-tile against a ones operand (a column of the result
+ * holds the K-tile's sum of one row), into a VGPR accumulator; deterministic, in the MFMA's summation
+ * order (not bitwise the earlier VALU order), and reduced over the splits in a fixed order.  workspace: fp32 split-K slabs
  * (splits x (M*N + M) floats).  EEGF_ERR_ARG when the shape is not eligible (bf16, M, N >= 256,
  * K >= 4096, K % 64 == 0, 8-aligned dims, 16-B aligned dY / X, workspace too small): run eegf_gemm and
  * eegf_colsum instead. */

@@ -58,3 +58,13 @@ def test_tune_routing_keys_validate_and_restore_without_gpu():
         assert lib.eegf_tune(key, -1) == _lib.ERR_ARG
         assert lib.eegf_tune(key, 0) == default
         assert lib.eegf_tune(key, old) == 0
+
+
+def test_launch_log_reads_empty_without_gpu():
+    """The launch counters (eegf_launch_log_*) are host state: after a reset, with nothing launched, the
+    log is the empty string (1 byte with the NUL) and _lib.launch_counts() an empty dict."""
+    from eegfusion import _lib
+    lib = _lib.lib()
+    assert lib.eegf_launch_log_reset() == 0
+    assert lib.eegf_launch_log_read(None, 0) == 1
+    assert _lib.launch_counts() == {}
