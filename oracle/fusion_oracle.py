@@ -1,7 +1,10 @@
 """CPU oracle for the EEG+action fusion training path — TEST INFRASTRUCTURE ONLY.
 
-A plain torch-CPU fp32 restatement (no `transformers`, no HIP) of the reference computation,
+A plain torch fp32 restatement (no `transformers`, no HIP) of the reference computation,
 used by tests/, `__graft_entry__.smoke()` and the `cpu_baseline` leg of bench.py as the checker.
+Device-agnostic: on CPU tensors it is the golden-pinned oracle; on GPU tensors (plain ATen fp32
+ops, TF32 off) the same functions check the production step at full size
+(tests/test_fullsize_oracle_gpu.py).
 The product path (eeg-multimodal_amd/eegfusion) never imports this module.
 
 Pinned against golden vectors produced by running the reference itself in the survey container
@@ -111,7 +114,7 @@ def bert_layer(p, i, h, key_bias):
 
 def bert(p, emb, attention_mask):
     """BertModel.forward (modeling_bert.py:623-686) → (sequence_output, pooled_output)."""
-    key_bias = torch.zeros(attention_mask.shape, dtype=emb.dtype)
+    key_bias = torch.zeros(attention_mask.shape, dtype=emb.dtype, device=emb.device)
     key_bias = key_bias.masked_fill(attention_mask == 0, torch.finfo(emb.dtype).min)
     h = emb
     for i in range(NLAYER):
@@ -327,9 +330,9 @@ def encoders(p, batch, cfg: PathConfig):
         eeg, act = batch["eeg"], batch["act"]                      # [B,C,T], [B,A]
         tokens = eeg.transpose(1, 2)                               # time-major [B,T,C]
         emb = bert_embeddings(p, inputs_embeds=_lin(tokens, p, "eeg_encoder"))
-        mask = batch.get("eeg_mask", torch.ones(eeg.shape[0], eeg.shape[2], dtype=torch.long))
+        mask = batch.get("eeg_mask", torch.ones(eeg.shape[0], eeg.shape[2], dtype=torch.long, device=eeg.device))
         vis = _lin(act.unsqueeze(1), p, "visual_encoder")          # [B,1,768]
-        vmask = torch.ones(eeg.shape[0], 1, dtype=torch.long)
+        vmask = torch.ones(eeg.shape[0], 1, dtype=torch.long, device=eeg.device)
     else:
         emb = bert_embeddings(p, input_ids=batch["title_input"])
         mask = batch["text_mask"]

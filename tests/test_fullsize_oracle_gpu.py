@@ -1,0 +1,121 @@
+"""The bf16 production step at the bench size (B = 256, 64ch x 256 EEG + 32-d action, PriGumbel pass 2:
+hard gate, dropout 0.1 at every reference site) against an implementation that is not this engine: the
+oracle (oracle/fusion_oracle.py, pinned bit-exactly to the reference's own outputs) run as the checker
+on GPU tensors in fp32 ATen ops (TF32 off), with every dropout site replayed from the engine's Philox
+streams (tests/philox_torch.py, the device form of philox_ref) and the same injected Laplace / Gumbel
+draws.  Reference: the iteration body of past_acc.py:194-212 over ConcatModel.forward (:108-139).
+
+Compared: logits, and every parameter gradient the step produces (about 200 tensors).  Bounds are bf16
+precision bounds, set at the measured values minus a margin (profiles/r6_fullsize_oracle.log):
+  logits relative error (max |diff| / max |ref|) <= LOGIT_REL, cosine >= LOGIT_COS;
+  per-gradient cosine: worst >= GRAD_COS_WORST, median >= GRAD_COS_MEDIAN;
+structurally ~0 gradients (attention key biases: softmax is shift-invariant) are bounded against their
+sibling query-bias gradient instead.
+"""
+import pytest
+import torch
+
+from goldens import det_params, w_values_dp
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+B, P_DROP = 256, 0.1
+LOGIT_REL, LOGIT_COS = 2e-2, 0.9995
+GRAD_COS_WORST, GRAD_COS_MEDIAN = 0.99, 0.9999
+
+
+def _cos(a, b):
+    a, b = a.double().reshape(-1), b.double().reshape(-1)
+    return float(a @ b / (a.norm() * b.norm()).clamp_min(1e-300))
+
+
+def _replay(seed: int, R: int, p: float):
+    import philox_torch as PT
+
+    def fn(site, x):
+        kind = site[0]
+        i = site[1] if len(site) > 1 else 0
+        off, stream = {
+            "emb": (R + 1, PT.attn_mask), "attn_out": (R + 10 + 3 * i, PT.attn_mask),
+            "ffn_out": (R + 11 + 3 * i, PT.attn_mask), "attn_probs": (R + 12 + 3 * i, "probs"),
+            "dec_sa": (R + 100 + 8 * i, PT.attn_mask), "dec_ca": (R + 101 + 8 * i, PT.attn_mask),
+            "dec_ff": (R + 102 + 8 * i, PT.attn_mask), "dec_sa_w": (R + 103 + 8 * i, PT.drop_mask),
+            "dec_ca_probs": (R + 104 + 8 * i, PT.drop_mask), "dec_ff_inner": (R + 105 + 8 * i, PT.drop_mask),
+        }[kind]
+        e = torch.arange(x.numel(), device=x.device, dtype=torch.int64)
+        m = PT.attn_probs_mask(seed, off, e, p, x.shape[-1]) if stream == "probs" else stream(seed, off, e, p)
+        del e
+        return x * m.view(x.shape).to(x.dtype)
+    return fn
+
+
+@pytest.mark.parametrize("rng0", [1 << 20, 5 << 20])
+def test_b256_bf16_production_step_vs_gpu_oracle(rng0):
+    from eegfusion.modules import PriGumbelModel
+    from oracle import fusion_oracle as O
+    torch.backends.cuda.matmul.allow_tf32 = False
+    torch.backends.cudnn.allow_tf32 = False
+    g = torch.Generator().manual_seed(rng0 >> 20)
+    eeg = torch.randn(B, 64, 256, generator=g)
+    act = torch.randn(B, 32, generator=g) * 0.5
+    labels = (torch.rand(B, generator=g) < 0.66).long()
+    noise = O.laplace_from_uniform(torch.rand(B, 2304, generator=g) * 2 - 1)
+    gumbels = -torch.log(-torch.log(torch.rand(2, B, 2304, generator=g).clamp(1e-6, 1 - 1e-6)))
+    dp = w_values_dp()
+
+    # the production engine: bf16 BERT, the bench's kernels (persistent GEMMs, L = 256 attention, split-K
+    # weight gradients), dropout drawn by the kernels
+    torch.manual_seed(0)
+    m = PriGumbelModel(1.0, contract="W", eps_mode="newfrac", dropout=P_DROP, seed=980616)
+    m.load_state_dict(det_params("W", "prigumbel", dp, requires_grad=False), strict=False)
+    m = m.to(DEV).train().set_compute_dtype(torch.bfloat16)
+    m.engine.injected = dict(noise=noise.to(DEV), gumbels=gumbels.to(DEV).contiguous())
+    m.engine.rng_counter = rng0
+    logits = m.forward_window(eeg.to(DEV), act.to(DEV), True)
+    torch.nn.functional.cross_entropy(logits, labels.to(DEV)).backward()
+    torch.cuda.synchronize()
+    got = {n: q.grad.detach().float() for n, q in m.named_parameters() if q.grad is not None}
+    lg = logits.detach().float()
+    seed = m.engine.cfg.seed
+    del m
+    torch.cuda.empty_cache()
+
+    # the checker: the oracle on GPU tensors, fp32, the engine's dropout masks replayed
+    pr = {k: v.to(DEV).requires_grad_() for k, v in det_params("W", "prigumbel", dp, requires_grad=False).items()}
+    O.set_dropout_replay(_replay(seed, rng0, P_DROP))
+    try:
+        ref = O.forward(pr, dict(eeg=eeg.to(DEV), act=act.to(DEV)),
+                        O.PathConfig(contract="W", variant="prigumbel", eps=1.0, hard=True),
+                        noise=noise.to(DEV), gumbels=gumbels.to(DEV))
+        torch.nn.functional.cross_entropy(ref, labels.to(DEV)).backward()
+    finally:
+        O.set_dropout_replay(None)
+    torch.cuda.synchronize()
+
+    lrel = float((lg - ref.detach()).abs().max() / ref.detach().abs().max())
+    lcos = _cos(lg, ref.detach())
+    rows, skipped = [], []
+    for n, t in pr.items():
+        if t.grad is None or n not in got:
+            continue
+        gref = t.grad.detach()
+        if n.endswith("attention.self.key.bias"):
+            scale = float(pr[n.replace(".key.", ".query.")].grad.abs().max())
+            assert float(got[n].abs().max()) < 1e-2 * scale and float(gref.abs().max()) < 1e-3 * scale, n
+            skipped.append(n)
+            continue
+        if float(gref.abs().max()) == 0.0:
+            assert float(got[n].abs().max()) < 1e-12, n
+            skipped.append(n)
+            continue
+        rows.append((_cos(got[n], gref), float((got[n] - gref).abs().max() / gref.abs().max()), n))
+    rows.sort()
+    cos = [r[0] for r in rows]
+    med = cos[len(cos) // 2]
+    print(f"\n[B=256 rng0={rng0}] logits rel {lrel:.3e} cos {lcos:.7f}; {len(rows)} gradients (+{len(skipped)} "
+          f"structurally ~0): worst cos {rows[:5]}; median cos {med:.7f}; worst rel "
+          f"{sorted(rows, key=lambda r: -r[1])[:3]}")
+    assert len(rows) > 150
+    assert lrel <= LOGIT_REL and lcos >= LOGIT_COS, (lrel, lcos)
+    assert rows[0][0] >= GRAD_COS_WORST, rows[:5]
+    assert med >= GRAD_COS_MEDIAN, med

@@ -44,3 +44,21 @@ def test_attn_probs_numbering_is_a_bijection():
         assert np.unique(draw).size == rows * L
     m = attn_probs_mask(7, 3, np.arange(64 * 256 * 256, dtype=np.uint64), 0.1, 256)
     assert abs((m > 0).mean() - 0.9) < 2e-3
+
+
+def test_torch_philox_matches_numpy_replay():
+    """tests/philox_torch.py (the device form used at full size) draws exactly philox_ref's masks:
+    the known answers, and every dropout stream on 2^16 elements at offsets past 2^32."""
+    import torch
+    import philox_torch as PT
+    from philox_ref import attn_probs_mask
+    for ctr, key, want in KAT:
+        got = tuple(int(w) for w in PT.philox4x32(*(torch.tensor([c]) for c in ctr), *key))
+        assert got == want
+    e = np.arange(1 << 16, dtype=np.uint64) + np.uint64(12345)
+    et = torch.from_numpy(e.astype(np.int64))
+    for seed, off in ((980616, 7), (3, (5 << 32) + 11)):
+        assert np.array_equal(PT.drop_mask(seed, off, et, 0.1).numpy(), drop_mask(seed, off, e, 0.1).astype(np.float32))
+        assert np.array_equal(PT.attn_mask(seed, off, et, 0.1).numpy(), attn_mask(seed, off, e, 0.1).astype(np.float32))
+        assert np.array_equal(PT.attn_probs_mask(seed, off, et, 0.1, 256).numpy(),
+                              attn_probs_mask(seed, off, e, 0.1, 256).astype(np.float32))
