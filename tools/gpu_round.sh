@@ -20,7 +20,7 @@ for s in "${@:2}"; do
     attn) step attn timeout -k 10 120 python -u tools/attn_bench.py > $O/${TAG}_attn.log 2>&1 && EEGF_ATTN256=0 step attn0 timeout -k 10 120 python -u tools/attn_bench.py >> $O/${TAG}_attn.log 2>&1 || exit 1 ;;
     attntests) step attntests timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread -k "attention" > $O/${TAG}_attn_tests.log 2>&1 || exit 1 ;;
     gemm) step gemm timeout -k 10 300 python -u tools/gemm_bench.py > $O/${TAG}_gemm.log 2>&1 || exit 1 ;;
-    bench) step bench timeout -k 10 400 python -u bench.py > $O/${TAG}_bench.json 2> $O/${TAG}_bench.err || exit 1 ;;
+    bench) step bench timeout -k 10 580 python -u bench.py > $O/${TAG}_bench.json 2> $O/${TAG}_bench.err || exit 1 ;;
     prof) (cd /tmp && export TMPDIR=/tmp && step prof timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$O/${TAG}_prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 4 --warmup 2 --no-cpu-baseline > $GRAFT_REPO_ROOT/$O/${TAG}_prof.log 2>&1) || exit 1 ;;
     c5) step c5 timeout -k 10 600 python -u bench.py --batch 512 --eps-sweep 0.1,1,3,5,10 --feawei 2048 --steps 4 --warmup 2 --no-cpu-baseline > $O/${TAG}_c5.json 2> $O/${TAG}_c5.err || exit 1 ;;
     priconcat) step priconcat timeout -k 10 300 python -u bench.py --variant priconcat --no-cpu-baseline > $O/${TAG}_priconcat.json 2> $O/${TAG}_priconcat.err || exit 1 ;;
