@@ -153,10 +153,17 @@ __global__ void __launch_bounds__(FT) fusion_fwd_kernel(FusionArgs a) {
     for (int k = 0; k < PER; ++k) out[tid + FT * k] = from_f32<T>(x[k]);
     return;
   }
+  // the gate (DP load, Philox, Laplace / Gumbel logs, softmax) does not depend on the row's min / max:
+  // computed before the block reduction, so its latency overlaps the feature loads and the barriers
+  GateVals gv[PER];
+  if (a.variant == FUSE_PRIGUMBEL) {
+#pragma unroll
+    for (int k = 0; k < PER; ++k) gv[k] = gate(a, b, tid + FT * k);
+  }
+  const float rn = a.variant == FUSE_PRICONCAT_LAP ? row_laplace(a, b) : 0.f;
   block_minmax<FW>(vmin, imin, vmax, imax);
   const float R = vmax - vmin;
   if (tid == 0 && a.amin) { a.amin[b] = imin; a.amax[b] = imax; a.range[b] = R; }
-  const float rn = a.variant == FUSE_PRICONCAT_LAP ? row_laplace(a, b) : 0.f;
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     const int j = tid + FT * k;
@@ -164,7 +171,7 @@ __global__ void __launch_bounds__(FT) fusion_fwd_kernel(FusionArgs a) {
     if (a.xn) a.xn[(long)b * D3 + j] = xn;
     float o;
     if (a.variant == FUSE_PRIGUMBEL) {
-      const GateVals g = gate(a, b, j);
+      const GateVals& g = gv[k];
       const float y = xn + g.n * g.eh;
       o = y * g.r0 + y * g.r1;
     } else if (a.variant == FUSE_PRICONCAT_LAP) {

@@ -480,26 +480,14 @@ int dispatch_epi(int epi, int akc, int bkc, const GemmArgs& a, int batch, hipStr
 
 int eegf_gemm_big(int a_kc, int b_kc, int epi, int out_f32, int M, int N, int K, const void* A, long lda,
                   const void* B, long ldb, void* C, long ldc, const float* bias, void* aux, long ldaux, float alpha,
-                  float beta, float epi_scale, void* workspace, long ws_bytes, float* a_colsum, hipStream_t stream);
-int eegf_gemm_big_colsum_tiles(int M, int N, int K);
+                  float beta, float epi_scale, void* workspace, long ws_bytes, hipStream_t stream);
 int eegf_gemm_big_wgrad_bias(int M, int N, int K, const void* A, long lda, const void* B, long ldb, float* C, long ldc,
                              float beta, float* db, void* workspace, long ws_bytes, hipStream_t stream);
-
-static int lds_epi_enabled() {
-  static const int on = [] { const char* e = getenv("EEGF_GEMM_LDS_EPI"); return (e && e[0] == '0') ? 0 : 1; }();
-  return on;
-}
-
-static bool big_enabled() {
-  static const int on = [] { const char* e = getenv("EEGF_GEMM_BIG"); return (e && e[0] == '0') ? 0 : 1; }();
-  return on != 0;
-}
 
 static int gemm_impl(int dtype, int out_dtype, int a_kcontig, int b_kcontig, int epi, int M, int N, int K, int batch,
                      const void* A, long lda, long strideA, const void* B, long ldb, long strideB, void* C, long ldc,
                      long strideC, const float* bias, long strideBias, void* aux, long ldaux, long strideAux,
-                     float alpha, float beta, float epi_scale, void* workspace, long ws_bytes, float* a_colsum,
-                     hipStream_t stream) {
+                     float alpha, float beta, float epi_scale, void* workspace, long ws_bytes, hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0 || batch <= 0 || !A || !B || !C) return EEGF_ERR_ARG;
   if (batch > 65535) return EEGF_ERR_ARG;
   if (epi < EPI_NONE || epi > EPI_MUL_AUX) return EEGF_ERR_ARG;
@@ -515,13 +503,12 @@ static int gemm_impl(int dtype, int out_dtype, int a_kcontig, int b_kcontig, int
     if (!fwd && !(a_kcontig && !b_kcontig)) return EEGF_ERR_ARG;
   }
   GemmArgs a{A, B, C, bias, aux, lda, ldb, ldc, ldaux, strideA, strideB, strideC, strideAux, strideBias, M, N, K, alpha, beta, epi_scale, 0,
-             lds_epi_enabled(), 128};
-  if (dtype == EEGF_BF16 && batch == 1 && big_enabled()) {
+             1, 128};
+  if (dtype == EEGF_BF16 && batch == 1) {
     const int st = eegf_gemm_big(a_kcontig, b_kcontig, epi, out_dtype == EEGF_F32, M, N, K, A, lda, B, ldb, C, ldc,
-                                 bias, aux, ldaux, alpha, beta, epi_scale, workspace, ws_bytes, a_colsum, stream);
+                                 bias, aux, ldaux, alpha, beta, epi_scale, workspace, ws_bytes, stream);
     if (st != 1) return st;
   }
-  if (a_colsum) return EEGF_ERR_ARG;       // fused column sums exist only on the 256x256 path
   // under-filled grids (the batch-row decoder / head GEMMs, M = B): 64 x 64 tiles quadruple the
   // workgroups; then split-K for long contractions (weight gradients, K = tokens) and for the
   // batch-row GEMMs; the fixed-order slab reduction applies the epilogue.
@@ -599,27 +586,13 @@ extern "C" int eegf_gemm(int dtype, int out_dtype, int a_kcontig, int b_kcontig,
                          hipStream_t stream) {
   return gemm_impl(dtype, out_dtype, a_kcontig, b_kcontig, epi, M, N, K, batch, A, lda, strideA, B, ldb, strideB, C,
                    ldc, strideC, bias, strideBias, aux, ldaux, strideAux, alpha, beta, epi_scale, workspace, ws_bytes,
-                   nullptr, stream);
-}
-
-extern "C" int eegf_gemm_colsum_tiles(int dtype, int out_dtype, int a_kcontig, int M, int N, int K) {
-  if (dtype != EEGF_BF16 || out_dtype != EEGF_BF16 || !a_kcontig || !big_enabled()) return 0;
-  return eegf_gemm_big_colsum_tiles(M, N, K);
-}
-
-extern "C" int eegf_gemm_acs(int dtype, int out_dtype, int a_kcontig, int b_kcontig, int epi, int M, int N, int K,
-                             const void* A, long lda, const void* B, long ldb, void* C, long ldc, const float* bias,
-                             void* aux, long ldaux, float alpha, float beta, float epi_scale, float* a_colsum,
-                             hipStream_t stream) {
-  if (!a_colsum || eegf_gemm_colsum_tiles(dtype, out_dtype, a_kcontig, M, N, K) == 0) return EEGF_ERR_ARG;
-  return gemm_impl(dtype, out_dtype, a_kcontig, b_kcontig, epi, M, N, K, 1, A, lda, 0, B, ldb, 0, C, ldc, 0, bias, 0,
-                   aux, ldaux, 0, alpha, beta, epi_scale, nullptr, 0, a_colsum, stream);
+                   stream);
 }
 
 extern "C" int eegf_gemm_wgrad_bias(int dtype, int M, int N, int K, const void* dY, long ldd, const void* X, long ldx,
                                     float* dW, long ldw, float beta, float* db, void* workspace, long ws_bytes,
                                     hipStream_t stream) {
-  if (dtype != EEGF_BF16 || !big_enabled() || !dY || !X || !dW || !db || M <= 0 || N <= 0 || K <= 0) return EEGF_ERR_ARG;
+  if (dtype != EEGF_BF16 || !dY || !X || !dW || !db || M <= 0 || N <= 0 || K <= 0) return EEGF_ERR_ARG;
   const int st = eegf_gemm_big_wgrad_bias(M, N, K, dY, ldd, X, ldx, dW, ldw, beta, db, workspace, ws_bytes, stream);
   return st == 1 ? EEGF_ERR_ARG : st;
 }

@@ -1,22 +1,17 @@
-// gemm_big.hip — bf16 MFMA GEMM for the token-sized projections (M = B*L rows).
+// gemm_big.hip — bf16 MFMA GEMMs for the token-sized projections (M = B*L rows): every BERT forward
+// (x W^T + bias [+GELU / GELU']), input gradient (dY W [* act'] [+ residual]) and weight gradient
+// (dY^T X over the tokens, split-K, with the bias row sums fused).
 //
-// Used by eegf_gemm for the BERT forward (x W^T + bias [+GELU]) and input-gradient (dY W [*act'])
-// GEMMs when M, N, K are large and aligned.  Structure (cdna_hip_programming.md §5, "minimum
-// 2-phase" + T1/T2):
-//   * 256x256 output tile, 512 threads = 8 waves as 2 (M) x 4 (N), wave tile 128x64 = 8x4 MFMA
-//     16x16x32 accumulators (kept transposed: a lane owns 4 consecutive columns of one row);
-//   * BK = 64; operands staged global -> LDS with global_load_lds_dwordx4 (no VGPR round trip)
-//     into two LDS buffers: the next k-step's loads fly while the current one is consumed; one
-//     barrier per k-step;
-//   * XOR-swizzled LDS images written lane-linearly (swizzle applied to the SOURCE address):
-//     row-major [256][64] operands use chunk ^= (row>>1)&7 (conflict-free ds_read_b128); k-major
-//     [64][256] operands use chunk ^= 2*((k&3) | ((k>>3)&1)<<2) (spread ds_read_b64_tr_b16);
-//   * XCD-aware tile order; LDS-staged coalesced epilogue (bias, GELU / act' from aux);
-//   * optional fused column sums of a K-contiguous A (the bias gradient of an input-gradient
-//     GEMM, colsum over the token rows of dY): workgroups of tile column 0 sum each staged A tile
-//     (in-wave shuffles, then 8 waves through 4 KB of LDS left free by the operand buffers) and
-//     write one fp32 partial row per 256-row tile: colsum_part[tile_m][K].
-// Edges: rows/cols beyond M/N are clamped to valid memory and never stored; K % 64 == 0.
+//   gemm4r  persistent 256x256, 4 waves of 128x128, whole-line K-tile pairs, rolling A fragments: every
+//           full-tile bf16 GEMM with K % 64 == 0 (all of the bench step's forwards and input gradients);
+//   gemm4p  the same persistent structure on 64-B half-line K-tiles: full tiles with other K;
+//   gemm4w  non-persistent 4-wave 256x256: weight gradients (fp32 split-K slabs) and every other shape.
+// Common structure (cdna_hip_programming.md §5): operands staged global -> LDS by asm LDS-DMA into XOR-
+// swizzled images (conflict-free ds_read_b128 / ds_read_b64_tr_b16), accumulators pinned to AGPRs by
+// asm MFMAs, counted vmcnt waits, XCD-aware tile order.  Edges (gemm4w): rows / cols beyond M / N are
+// clamped to valid memory and never stored; K % 64 == 0.
+// Retired in round 6 (superseded; git history 829c7a6): the 2-phase gemm_big_kernel, the 8-wave gemm8,
+// the 256x128 two-workgroup gemm4h and the five-slot-ring gemm4q, with their timing probes.
 #include <type_traits>
 
 #include "common.h"
@@ -35,18 +30,14 @@ struct BigArgs {
   int M, N, K;
   float alpha, beta, epi_scale;
   int ksplit;            // >0: split-K slice length; C = fp32 slabs [blockIdx.y][M][N]
-  float* colsum_part;    // AKC only: [tiles_m][K] partial column sums of A (nullable)
   float* rowsum_part;    // gemm4w RS only: [splits][M] sums over this split's K of each row of a k-major A
   long long* ts;         // diagnostics (eegf_gemm_big_timestamps): per-workgroup phase times, null = off
   int group_m;           // tile raster: 0 row-major, G > 0 groups of G row panels walked column by column
-  int store_nt = 0;      // gemm4p: epilogue stores with the non-temporal hint
-  int order = 0;         // gemm4q persistent tile order (eegf_tune key 15, see q_walk)
 };
-// key 9: -1 (default) = groups of 4 row panels when the grid is at least 8 tile columns wide (the
-// K = 768 forward / input-gradient GEMMs with N >= 2304: +2-4 %, profiles/r2r_group.log), row-major
-// otherwise (N = 768: 3 tile columns, no gain)
-int g_group_m = [] { const char* e = getenv("EEGF_GEMM_GROUP"); return e ? atoi(e) : -1; }();
-int group_for(int N) { return g_group_m >= 0 ? g_group_m : ((N + 255) / 256 >= 8 ? 4 : 0); }
+// groups of 4 row panels when the grid is at least 8 tile columns wide (the K = 768 forward / input-
+// gradient GEMMs with N >= 2304: +2-4 %, profiles/r2r_group.log), row-major otherwise (N = 768: 3 tile
+// columns, no gain)
+int group_for(int N) { return (N + 255) / 256 >= 8 ? 4 : 0; }
 // Logical tile t (after xcd_remap: consecutive t share an XCD) -> (tile row, tile column).  Grouped
 // raster: G row panels x all column tiles per group, column-major inside the group, so the ~32 tiles
 // an XCD runs at once touch G A-panels and ~32/G B-panels instead of ~3 A-panels and every B-panel.
@@ -63,8 +54,11 @@ DEV void tile_coords(const BigArgs& g, int t, int tiles_m, int tiles_n, int& tm,
 }
 // Phase timestamps (100 MHz s_memrealtime) of one workgroup: 0 start, 1 prologue done, 2 K-loop done,
 // 3 epilogue issued; slot 4 = the CU it ran on (8 int64 per workgroup) -- tools/gemm_phases.py turns them into per-phase times and dispatch gaps
+#ifndef EEGF_DIAG
+#define EEGF_DIAG 0
+#endif
 DEV void ts_mark(const BigArgs& g, int k) {
-  if (g.ts && threadIdx.x == 0) {
+  if (EEGF_DIAG && g.ts && threadIdx.x == 0) {
     long long* p = g.ts + ((long)blockIdx.y * gridDim.x + blockIdx.x) * 8;
     p[k] = (long long)__builtin_amdgcn_s_memrealtime();
     if (k == 0) {                    // which CU: XCC id << 16 | HW_ID bits 8-15 (CU, SH, SE)
@@ -330,347 +324,10 @@ DEV void big_epilogue(const BigArgs& g, f32x4 (&acc)[8][NJ], bf16* lds, int m0, 
   }
 }
 
-constexpr int CS_KMAX = 3072;                 // fused column sums: K <= 3072 (sums parked in LDS)
-
-template <bool AKC, bool BKC, int EPI, typename TO, bool CS = false>
-__global__ void __launch_bounds__(NT, 1) gemm_big_kernel(BigArgs g) {
-  // CS: operand ring 128 KB | red[2][8][64] 4 KB | ks[K] fp32 12 KB  (the epilogue reuses the front)
-  __shared__ __attribute__((aligned(16))) bf16 lds[CS ? (4 * TILE + 1024 * 2 + CS_KMAX * 2) : LDS_ELEMS];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 2, wn = wave & 3;
-  const int tiles_n = (g.N + TN - 1) / TN, tiles_m = (g.M + TM - 1) / TM;
-  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  int tm, tn;
-  tile_coords(g, t, tiles_m, tiles_n, tm, tn);
-  const int m0 = tm * TM, n0 = tn * TN;
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  int kbeg = 0, kend = g.K;
-  if (g.ksplit > 0) { kbeg = blockIdx.y * g.ksplit; kend = min(g.K, kbeg + g.ksplit); }
-  const int nk = (kend - kbeg) / BK;
-  if (AKC) stage_rowmajor(lds, g.A, g.lda, m0, g.M, kbeg, wave, lane);
-  else stage_kmajor(lds, g.A, g.lda, m0, g.M, kbeg, wave, lane);
-  if (BKC) stage_rowmajor(lds + TILE, g.B, g.ldb, n0, g.N, kbeg, wave, lane);
-  else stage_kmajor(lds + TILE, g.B, g.ldb, n0, g.N, kbeg, wave, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  // fused A column sums (tile column 0 only): red[parity][wave][64] in the LDS tail
-  const bool do_cs = CS && AKC && tn == 0;
-  float* red = (float*)(lds + 4 * TILE);
-  float* ks = red + 2 * 8 * 64;
-  const int cs_rows = g.M - m0 - 32 * wave - 8 * (lane >> 4);   // rows of this lane's 8-row group below M
-
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = (kt & 1) * 2 * TILE, nxt = 2 * TILE - cur;
-    if (kt + 1 < nk) {
-      const int kn = kbeg + (kt + 1) * BK;
-      if (AKC) stage_rowmajor(lds + nxt, g.A, g.lda, m0, g.M, kn, wave, lane);
-      else stage_kmajor(lds + nxt, g.A, g.lda, m0, g.M, kn, wave, lane);
-      if (BKC) stage_rowmajor(lds + nxt + TILE, g.B, g.ldb, n0, g.N, kn, wave, lane);
-      else stage_kmajor(lds + nxt + TILE, g.B, g.ldb, n0, g.N, kn, wave, lane);
-    }
-    const bf16* As = lds + cur;
-    const bf16* Bs = lds + cur + TILE;
-    // fused column sums of this A tile on the MFMA: ones[16 x 256] . A[256 x 64] (rows past M masked in
-    // the ones operand); wave w contracts rows [32w, 32w+32), its 64 partial sums go through LDS
-    if (CS && do_cs) {
-      if (kt > 0 && tid < 64) {      // previous k-step's 8 wave partials (ordered by the barrier)
-        const float* rp = red + ((kt - 1) & 1) * 8 * 64;
-        float v = 0.f;
-#pragma unroll
-        for (int w = 0; w < 8; ++w) v += rp[w * 64 + tid];
-        ks[(kt - 1) * BK + tid] = v;
-      }
-      bf16x8 ones;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) ones[e] = (bf16)(e < cs_rows ? 1.0f : 0.0f);
-#pragma unroll
-      for (int f = 0; f < 4; ++f) {
-        const f32x4 c = mma16(ones, rd_col_rm(As, 32 * wave + 8 * (lane >> 4), 16 * f, lane), f32x4{0.f, 0.f, 0.f, 0.f});
-        if (lane < 16) red[(kt & 1) * 8 * 64 + wave * 64 + 16 * f + lane] = c[0];
-      }
-    }
-#pragma unroll
-    for (int kc = 0; kc < 2; ++kc) {
-      bf16x8 b[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c = wn * 64 + j * 16;
-        if (BKC) b[j] = rd_row(Bs, c + (lane & 15), 4 * kc + (lane >> 4));
-        else b[j] = rd_col(Bs, 32 * kc + 8 * (lane >> 4), c, lane);
-      }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const bf16x8 a = AKC ? rd_row(As, wm * 128 + i * 16 + (lane & 15), 4 * kc + (lane >> 4))
-                             : rd_col(As, 32 * kc + 8 * (lane >> 4), wm * 128 + i * 16, lane);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mma16(b[j], a, acc[i][j]);
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-  if (CS && do_cs && tid < 64) {
-    const float* rp = red + ((nk - 1) & 1) * 8 * 64;
-    float v = 0.f;
-#pragma unroll
-    for (int w = 0; w < 8; ++w) v += rp[w * 64 + tid];
-    ks[(nk - 1) * BK + tid] = v;
-  }
-  if (CS) {
-    __syncthreads();
-    if (do_cs)
-      for (int k = tid; k < g.K; k += NT) g.colsum_part[(long)tm * g.K + k] = ks[k];
-    __syncthreads();               // the epilogue reuses the front of the LDS
-  }
-
-  big_epilogue<EPI, TO>(g, acc, lds, m0, n0, tid, lane, wm, wn);
-}
-
-// ---------------------------------------------------------------------------------------------
-// 8-phase schedule for A and B both K-contiguous (the forward x W^T GEMMs), after the structure of
-// cdna_hip_programming.md §5 "The 256² 8-phase template": the two wave groups (wm = 0 / 1, one wave
-// of each per SIMD) run staggered by one barrier, so one group's MFMAs overlap the other's LDS
-// reads and staging; operands are staged in 16 KB half-tiles, one per phase, and retired with a
-// counted vmcnt (never 0 in the loop) under raw s_barriers.
-//   Half-tiles of K-tile t (buffer t&1): A_h0 = rows {0..63, 128..191}, A_h1 = rows {64..127,
-//   192..255} (the wave's m-quadrant 0 / 1), B_h0 / B_h1 = the wave's n-quadrant 0 / 1 (columns
-//   64w + 32h + 0..31).  Phase p of tile t computes quadrant (mh, nh) = (0,0) (0,1) (1,1) (1,0):
-//     reads  P0: A_h0 + B_h0    P1: B_h1    P2: A_h1    P3: -        (64 fragment VGPRs)
-//     stages P0: B_h1(t+1)  P1: A_h1(t+1)  P2: A_h0(t+2)  P3: B_h0(t+2)
-//   Every stage lands >= 2 phases after the last read of the half it overwrites (WAR with the
-//   stagger); each phase's vmcnt retires the half staged 4 phases earlier, read >= 1 phase later.
-constexpr int HALF = 128 * BK;                // elements per half-tile (16 KB)
-int g_gemm8 = [] { const char* e = getenv("EEGF_GEMM8"); return e ? atoi(e) : -1; }();   // -1: auto
-
-DEV void stage_half(bf16* dst, const bf16* src, long ld, int base, int sh, int stride, int off, int rmax, int k0,
-                    int wave, int lane) {
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int R0 = (wave * 2 + j) * 8;
-    const int l = R0 + (lane >> 3);
-    const int c = (lane & 7) ^ swz_row(l);
-    const int gr = min(base + (l >> sh) * stride + off + (l & ((1 << sh) - 1)), rmax - 1);
-    glds16(src + (long)gr * ld + k0 + c * 8, dst + R0 * BK);
-  }
-}
-
-// k-major half-tile image [64 k][128 local columns] (weight-gradient A and B, input-gradient B):
-// 2 glds per wave, each 4 k-rows x 256 B; local column lc maps to tile column
-// (lc >> sh) * stride + off + (lc & (2^sh - 1)) (the same half split as stage_half); the 16-B
-// chunk index is XOR-swizzled with swz_k(k) on the source side (conflict-free tr reads).
-DEV void stage_half_km(bf16* dst, const bf16* src, long ld, int base, int sh, int stride, int off, int cmax,
-                       int k0, int wave, int lane) {
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int K0 = (wave * 2 + j) * 4;
-    const int k = K0 + (lane >> 4);
-    const int lc = ((lane & 15) ^ swz_k(k)) * 8;
-    const int col = min(base + (lc >> sh) * stride + off + (lc & ((1 << sh) - 1)), cmax - 8);
-    glds16(src + (long)(k0 + k) * ld + col, dst + K0 * 128);
-  }
-}
-
-// rd_col on a k-major half image [64][128]: k-values k0..k0+7 of local column c0 + (lane&15)
-DEV bf16x8 rd_colh(const bf16* t, int k0, int c0, int lane) {
-  const int i = lane & 15, q = i >> 2, p = i & 3;
-  const int col = c0 + 4 * p;
-  const int ch = col >> 3, off = col & 7;
-  const int ka = k0 + q, kb = k0 + 4 + q;
-  const bf16* a0 = t + ka * 128 + (((ch ^ swz_k(ka)) << 3) | off);
-  const bf16* a1 = t + kb * 128 + (((ch ^ swz_k(kb)) << 3) | off);
-  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)a0);
-  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)a1);
-  bf16x8 r;
-  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
-  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
-  return r;
-}
-
-DEV void vm_wait(int n) {      // s_waitcnt vmcnt(2n), n = younger half-tiles in flight (0..4)
-  switch (n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-  }
-}
 DEV void raw_barrier() {
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_barrier" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
-}
-
-// Layouts: AKC/BKC as gemm_big_kernel (row-major half images read with ds_read_b128, k-major ones
-// with ds_read_b64_tr_b16); fp32 output = split-K slabs over blockIdx.y as gemm_big_kernel.
-// Schedule: the 8 waves run the 4 phases of a K-tile in lockstep (one barrier per phase, MFMAs at
-// s_setprio 1) with one counted vmcnt per K-tile (phase 3: every half staged up to phase 1 of this
-// tile retired, the two younger ones stay in flight across the barrier).  The staggered-group and
-// per-phase-vmcnt variants measured 2-25 % slower (profiles/r1s2_gemm_ab.log) and were removed.
-// CS: fused column sums of A (as gemm_big_kernel's): in workgroups of tile column 0, waves 0-3 contract
-// 32 local rows of A_h0 at phase 0 and waves 4-7 32 rows of A_h1 at phase 2 against a ones operand
-// (4 extra MFMAs per K-tile); the 8 partials go through red[2][8][64] in LDS and wave 0 folds the
-// previous K-tile's into ks[K] at phase 1.
-template <bool AKC, bool BKC, int EPI, typename TO, bool CS = false>
-__global__ void __launch_bounds__(NT, 1) gemm8_kernel(BigArgs g) {
-  // CS: operand ring 128 KB | red[2][8][64] 4 KB | ks[K] fp32 12 KB  (the epilogue reuses the front)
-  __shared__ __attribute__((aligned(16))) bf16 lds[CS ? (8 * HALF + 1024 * 2 + CS_KMAX * 2) : LDS_ELEMS];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 2, wn = wave & 3;
-  const int tiles_n = (g.N + TN - 1) / TN, tiles_m = (g.M + TM - 1) / TM;
-  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  int tm, tn;
-  tile_coords(g, t, tiles_m, tiles_n, tm, tn);
-  const int m0 = tm * TM, n0 = tn * TN;
-  int kbeg = 0, kend = g.K;
-  if (g.ksplit > 0) { kbeg = blockIdx.y * g.ksplit; kend = min(g.K, kbeg + g.ksplit); }
-  const int nk = (kend - kbeg) / BK;
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // half-tile slots: buffer b at b*4*HALF: [A_h0][A_h1][B_h0][B_h1]
-  auto stageA = [&](int tile, int h) {
-    bf16* d = lds + (tile & 1) * 4 * HALF + h * HALF;
-    if (AKC) stage_half(d, g.A, g.lda, m0, 6, 128, 64 * h, g.M, kbeg + tile * BK, wave, lane);
-    else stage_half_km(d, g.A, g.lda, m0, 6, 128, 64 * h, g.M, kbeg + tile * BK, wave, lane);
-  };
-  auto stageB = [&](int tile, int h) {
-    bf16* d = lds + (tile & 1) * 4 * HALF + (2 + h) * HALF;
-    if (BKC) stage_half(d, g.B, g.ldb, n0, 5, 64, 32 * h, g.N, kbeg + tile * BK, wave, lane);
-    else stage_half_km(d, g.B, g.ldb, n0, 5, 64, 32 * h, g.N, kbeg + tile * BK, wave, lane);
-  };
-  auto rdB = [&](const bf16* Bh, int jj, int kc) {
-    return BKC ? rd_row(Bh, wn * 32 + jj * 16 + (lane & 15), 4 * kc + (lane >> 4))
-               : rd_colh(Bh, 32 * kc + 8 * (lane >> 4), wn * 32 + jj * 16, lane);
-  };
-  auto rdA = [&](const bf16* Ah, int ii, int kc) {
-    return AKC ? rd_row(Ah, wm * 64 + ii * 16 + (lane & 15), 4 * kc + (lane >> 4))
-               : rd_colh(Ah, 32 * kc + 8 * (lane >> 4), wm * 64 + ii * 16, lane);
-  };
-  // global phase phi = 4t + p stages: p0 B_h1(t+1), p1 A_h1(t+1), p2 A_h0(t+2), p3 B_h0(t+2)
-  auto stage_tile_of = [&](int phi) { const int tt = phi >> 2, p = phi & 3; return tt + (p <= 1 ? 1 : 2); };
-  auto stage_phase = [&](int phi) {
-    const int tt = stage_tile_of(phi), p = phi & 3;
-    if (tt >= nk) return;
-    if (p == 0) stageB(tt, 1);
-    else if (p == 1) stageA(tt, 1);
-    else if (p == 2) stageA(tt, 0);
-    else stageB(tt, 0);
-  };
-  // prologue = the stages of phases -6 .. -1
-  auto younger2 = [&](int phi) {      // real stages among phases phi-1, phi
-    return (stage_tile_of(phi - 1) < nk ? 1 : 0) + (stage_tile_of(phi) < nk ? 1 : 0);
-  };
-  ts_mark(g, 0);
-  for (int phi = -6; phi < 0; ++phi) stage_phase(phi);
-  vm_wait(younger2(-1));              // retires phases -6 .. -3 (every half of tile 0)
-  raw_barrier();
-  ts_mark(g, 1);
-
-  const bool do_cs = CS && AKC && tn == 0;
-  float* red = (float*)(lds + 8 * HALF);
-  float* ks = red + 2 * 8 * 64;
-  const int cs_h = wave >> 2, cs_lr0 = 32 * (wave & 3);     // half, first local row of this wave's 32
-  // valid rows of the lane's 8-row group (local row lr of half h = tile row (lr >> 6) 128 + 64 h + (lr & 63))
-  const int cs_rows = g.M - m0 - ((cs_lr0 >> 6) * 128 + 64 * cs_h + (cs_lr0 & 63) + 8 * (lane >> 4));
-  bf16x8 ones;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) ones[e] = (bf16)(e < cs_rows ? 1.0f : 0.0f);
-
-  bf16x8 ar[4][2], br0[2][2], br1[2][2];
-  for (int kt = 0; kt < nk; ++kt) {
-    const bf16* Ab = lds + (kt & 1) * 4 * HALF;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int phi = 4 * kt + p;
-      if (CS && do_cs) {
-        if (p == 2 * cs_h) {            // this K-tile's column sums over the wave's 32 rows
-          const bf16* Ah = Ab + cs_h * HALF;
-#pragma unroll
-          for (int f = 0; f < 4; ++f) {
-            const f32x4 c = mma16(ones, rd_col_rm(Ah, cs_lr0 + 8 * (lane >> 4), 16 * f, lane), f32x4{0.f, 0.f, 0.f, 0.f});
-            if (lane < 16) red[(kt & 1) * 512 + wave * 64 + 16 * f + lane] = c[0];
-          }
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");    // visible after this phase's barrier
-        }
-        if (p == 1 && kt > 0 && tid < 64) {
-          const float* rp = red + ((kt - 1) & 1) * 512;
-          float v = 0.f;
-#pragma unroll
-          for (int w = 0; w < 8; ++w) v += rp[w * 64 + tid];
-          ks[(kt - 1) * BK + tid] = v;
-        }
-      }
-      // (a) fragment reads of this phase's quadrant
-      if (p == 0) {
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj)
-#pragma unroll
-          for (int kc = 0; kc < 2; ++kc) br0[jj][kc] = rdB(Ab + 2 * HALF, jj, kc);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if (p == 1) {
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj)
-#pragma unroll
-          for (int kc = 0; kc < 2; ++kc) br1[jj][kc] = rdB(Ab + 3 * HALF, jj, kc);
-      }
-      if (p == 0 || p == 2) {
-        const bf16* Ah = Ab + (p == 0 ? 0 : HALF);
-#pragma unroll
-        for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-          for (int kc = 0; kc < 2; ++kc) ar[ii][kc] = rdA(Ah, ii, kc);
-      }
-      // (b) stage one half-tile, (c) retire the one staged 4 phases ago
-      stage_phase(phi);
-      if (p == 3) vm_wait(younger2(phi));
-      raw_barrier();
-      // (e) the quadrant's 16 MFMAs
-      const int mh = (p == 0 || p == 1) ? 0 : 1, nh = (p == 1 || p == 2) ? 1 : 0;
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj)
-#pragma unroll
-          for (int kc = 0; kc < 2; ++kc) {
-            const bf16x8 bv = nh == 0 ? br0[jj][kc] : br1[jj][kc];
-            acc[mh * 4 + ii][nh * 2 + jj] = mma16(bv, ar[ii][kc], acc[mh * 4 + ii][nh * 2 + jj]);
-          }
-      __builtin_amdgcn_s_setprio(0);
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  ts_mark(g, 2);
-  if (CS) {
-    if (do_cs && tid < 64) {
-      const float* rp = red + ((nk - 1) & 1) * 512;
-      float v = 0.f;
-#pragma unroll
-      for (int w = 0; w < 8; ++w) v += rp[w * 64 + tid];
-      ks[(nk - 1) * BK + tid] = v;
-    }
-    __syncthreads();
-    if (do_cs)
-      for (int k = tid; k < g.K; k += NT) g.colsum_part[(long)tm * g.K + k] = ks[k];
-    __syncthreads();               // the epilogue reuses the front of the LDS
-  }
-  // acc[i][j]: i = 4*mh + ii -> rows wm*128 + 64*mh + 16*ii = wm*128 + 16*i (same map as gemm_big)
-  big_epilogue<EPI, TO>(g, acc, lds, m0, n0, tid, lane, wm, wn);
-  ts_mark(g, 3);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -682,15 +339,6 @@ __global__ void __launch_bounds__(NT, 1) gemm8_kernel(BigArgs g) {
 // LDS image of an operand K-tile: [256 rows][32 k] bf16 = 64-B rows; 16-B chunk c of row r stored at
 // chunk c ^ sw4(r), sw4(r) = 3 * ((r >> 3) & 1): conflict-free for the ds_read_b128 lane groups of a
 // 16-row fragment read (lanes 16q + i read row i, chunk q).
-#ifndef EEGF_W_PROBE
-#define EEGF_W_PROBE 0
-#endif
-#ifndef EEGF_W_READS
-#define EEGF_W_READS 0
-#endif
-#ifndef EEGF_W_STAGGER
-#define EEGF_W_STAGGER 0
-#endif
 #ifndef EEGF_W_NOP
 #define EEGF_W_NOP 0
 #endif
@@ -795,11 +443,8 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
   // uniform base of K-tile kt: K-contiguous advances 32 elements, k-major 32 rows
   const bf16* baseA = AKC ? g.A + (long)m0 * g.lda + kbeg : g.A + (long)kbeg * g.lda + m0;
   const bf16* baseB = BKC ? g.B + (long)n0 * g.ldb + kbeg : g.B + (long)kbeg * g.ldb + n0;
-  // EEGF_W_PROBE (diagnostic builds only, tools/variant_lib.sh; results are wrong): 1 every K-tile
-  // re-reads K-tile 0's addresses (L2-resident operands), 2 no staging after the prologue, 3 = 2 with no
-  // per-K-tile waits and barrier (the MFMA + LDS-read ceiling of the loop).  profiles/r4c_wgrad_ceilings.log
-  const long stepA = EEGF_W_PROBE == 1 ? 0 : AKC ? BK4 : (long)BK4 * g.lda;
-  const long stepB = EEGF_W_PROBE == 1 ? 0 : BKC ? BK4 : (long)BK4 * g.ldb;
+  const long stepA = AKC ? BK4 : (long)BK4 * g.lda;
+  const long stepB = BKC ? BK4 : (long)BK4 * g.ldb;
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr_of(lds));
   // part j of a K-tile -> ring slot; NOP as gemm4p's (0 in the K-loop, whose bases are pinned to SGPRs
   // at the top of each K-tile, 3 in the prologue)
@@ -878,7 +523,7 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
   auto ktile = [&](auto Hc, int k, int slot, int nslot, auto Ic, auto Tc) __attribute__((always_inline)) {
     constexpr int H = decltype(Hc)::value;
     constexpr bool INIT = decltype(Ic)::value, TAIL = decltype(Tc)::value;
-    const bool more = !TAIL || k + 1 < nk, st = EEGF_W_PROBE < 2 && (!TAIL || k + NSLOT4 < nk);
+    const bool more = !TAIL || k + 1 < nk, st = !TAIL || k + NSLOT4 < nk;
     const bf16* nimg = lds + nslot * SLOT4;
     // uniform K-tile bases of the stage, moved to SGPRs here, 50+ instructions ahead of the first DMA
     // (left to hipcc they stay in VGPRs and each DMA is preceded by a v_readfirstlane pair)
@@ -897,47 +542,33 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
       if (INIT) mma16_acc0(acc[s][jj], fb[H][jj], fa[H][s]);
       else mma16_acc(acc[s][jj], fb[H][jj], fa[H][s]);
     };
-    // next K-tile's fragment reads: EEGF_W_READS 1 issues them in groups 0..5 (as gemm4p's
-    // EEGF_P_READS), 0 one fa + one fb per group
+    // next K-tile's fragment reads: one fa + one fb per 8-MFMA group
     auto rd_next = [&](int s, int jj) __attribute__((always_inline)) {
       if (!more) return;
-      if (EEGF_W_READS == 0) {
-        if (jj == 0) fa[H ^ 1][s] = rdA(nimg, s);
-        if (jj == 1) fb[H ^ 1][s] = rdB(nimg, s);
-      } else if (s < 4) {
-        if (jj == 0) fa[H ^ 1][s] = rdA(nimg, s);
-        if (jj == 1) fb[H ^ 1][2 * s] = rdB(nimg, 2 * s);
-        if (jj == 3) fb[H ^ 1][2 * s + 1] = rdB(nimg, 2 * s + 1);
-      } else if (s < 6) {
-        if (jj == 0) fa[H ^ 1][2 * s - 4] = rdA(nimg, 2 * s - 4);
-        if (jj == 1) fa[H ^ 1][2 * s - 3] = rdA(nimg, 2 * s - 3);
-      }
+      if (jj == 0) fa[H ^ 1][s] = rdA(nimg, s);
+      if (jj == 1) fb[H ^ 1][s] = rdB(nimg, s);
     };
-    // group s: the non-MFMA work sits in the shadows of the group's first MFMAs
-    // EEGF_W_STAGGER 1: wave w issues its LDS-DMA of group s after the group's MFMA 2 w (as gemm4p's
-    // EEGF_P_STAGGER)
+    // group s: the non-MFMA work sits in the shadows of the group's first MFMAs (staggering the four
+    // waves' LDS-DMA over the group measured the same, profiles/r4zb_dma_position_prio_ab.log)
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       mma(s, 0);
       rd_next(s, 0);
-      if (EEGF_W_STAGGER && st && wave == 0) stage_part(sA, sB, slot, s, WNOP{});
       __builtin_amdgcn_sched_barrier(0);
       mma(s, 1);
       rd_next(s, 1);
       __builtin_amdgcn_sched_barrier(0);
       mma(s, 2);
-      if (EEGF_W_STAGGER ? st && wave == 1 : st) stage_part(sA, sB, slot, s, WNOP{});
+      if (st) stage_part(sA, sB, slot, s, WNOP{});
       __builtin_amdgcn_sched_barrier(0);
       mma(s, 3);
       rd_next(s, 3);
       __builtin_amdgcn_sched_barrier(0);
       mma(s, 4);
-      if (EEGF_W_STAGGER && st && wave == 2) stage_part(sA, sB, slot, s, WNOP{});
       __builtin_amdgcn_sched_barrier(0);
       mma(s, 5);
       __builtin_amdgcn_sched_barrier(0);
       mma(s, 6);
-      if (EEGF_W_STAGGER && st && wave == 3) stage_part(sA, sB, slot, s, WNOP{});
       __builtin_amdgcn_sched_barrier(0);
       mma(s, 7);
       // RS: row sums of this K-tile's A rows 16 s .. 16 s + 15 (D column j = row 16 s + j)
@@ -947,10 +578,6 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
       }
     }
     // K-tile k + 2 retired (its fragments are read in the next K-tile); younger: k + 3 .. k + NSLOT4
-    if constexpr (EEGF_W_PROBE == 3) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      return;
-    }
     if (!TAIL) vm_wait_tiles(NSLOT4 - 2);
     else vm_wait_tiles(max(0, min(nk - 1, k + NSLOT4) - (k + 2)));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads of k + 1 done: its slot may be restaged
@@ -1091,11 +718,9 @@ DEV u32x4 pack16(bf16x4 a, bf16x4 b) {
   const auto ry = __builtin_amdgcn_permlane16_swap(ua.y, ub.y, false, false);
   return u32x4{rx[0], ry[0], rx[1], ry[1]};
 }
-// non-temporal stores (eegf_tune key 12): 3-4 % off the store-bound epilogues, profiles/r4a_pol.log
-DEV void st_out(bf16* pp, u32x4 d, int nt) {
-  if (nt) asm volatile("global_store_dwordx4 %0, %1, off nt" :: "v"(pp), "v"(d) : "memory");
-  else *(u32x4*)pp = d;
-}
+// plain 16-B stores: the nt policy ran the store-bound epilogues 3-4 % faster alone but the step 0.8 %
+// slower (the consumers lose the outputs' MALL residency, profiles/r4b_store_nt_step_ab.log)
+DEV void st_out(bf16* pp, u32x4 d) { *(u32x4*)pp = d; }
 template <int EPI, bool ACC, class Sink>
 DEV void p_epi_tile(const BigArgs& g, f32x4 (&acc)[8][8], const f32x4 (&biasv)[8], int mrow, int nst, Sink&& sink) {
   constexpr bool HAS_BIAS = EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_D;
@@ -1164,33 +789,21 @@ DEV void p_epi_tile(const BigArgs& g, f32x4 (&acc)[8][8], const f32x4 (&biasv)[8
     }
   }
 }
-// NT: the runtime store policy (gemm4p / gemm4q, eegf_tune key 12).  gemm4r takes plain stores only
-// (NT = false): a runtime policy puts a scalar branch around each of the tile's 64 stores, and those
-// block boundaries keep the scheduler from interleaving the GELU chains of neighbouring chunks (an
-// s_nop between most dependent packed FMAs)
-template <int EPI, bool ACC, bool NT = true>
+// (no runtime store-policy branch around the tile's 64 stores: such block boundaries kept the scheduler
+// from interleaving the GELU chains of neighbouring chunks -- an s_nop between most dependent packed FMAs)
+template <int EPI, bool ACC>
 DEV void p_store_tile(const BigArgs& g, f32x4 (&acc)[8][8], const f32x4 (&biasv)[8], int mrow, int n0, int wn,
                       int lane) {
   const int nst = p_nst(n0, wn, lane);
   bf16* Cb = (bf16*)g.C;
-  const int nt = NT ? g.store_nt : 0;
   p_epi_tile<EPI, ACC>(g, acc, biasv, mrow, nst, [&](int i, int jp, const bf16x4 (&o)[2], const bf16x4 (&o2)[2]) {
     const long m = mrow + 16 * i;
     if ((EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_D) && (EPI == EPI_BIAS_GELU_D || g.aux))
-      st_out(g.aux + m * g.ldaux + nst + 32 * jp, pack16(o2[0], o2[1]), nt);
-    st_out(Cb + m * g.ldc + nst + 32 * jp, pack16(o[0], o[1]), nt);
+      st_out(g.aux + m * g.ldaux + nst + 32 * jp, pack16(o2[0], o2[1]));
+    st_out(Cb + m * g.ldc + nst + 32 * jp, pack16(o[0], o[1]));
   });
 }
 
-#ifndef EEGF_P_READS
-#define EEGF_P_READS 0
-#endif
-#ifndef EEGF_P_PROBE
-#define EEGF_P_PROBE 0
-#endif
-#ifndef EEGF_P_STAGGER
-#define EEGF_P_STAGGER 0
-#endif
 #ifndef EEGF_P_NOP
 #define EEGF_P_NOP 0
 #endif
@@ -1244,13 +857,8 @@ __global__ void __launch_bounds__(NT4, 1) gemm4p_kernel(BigArgs g) {
     tile_coords(g, l, tiles_m, tiles_n, tm, tn);
     m0 = __builtin_amdgcn_readfirstlane(tm * TM);
     n0 = __builtin_amdgcn_readfirstlane(tn * TN);
-    int am = m0, bn = n0;
-    if ((g.order & 3) == 2) {    // timing probe: operands from an L2-resident panel set (wrong results)
-      am = __builtin_amdgcn_readfirstlane((((tm & 3) + 4 * (blockIdx.x & 7)) % tiles_m) * TM);
-      bn = __builtin_amdgcn_readfirstlane((tn & 3) % tiles_n * TN);
-    }
-    bA = g.A + (long)am * g.lda;
-    bB = BKC ? g.B + (long)bn * g.ldb : g.B + bn;
+    bA = g.A + (long)m0 * g.lda;
+    bB = BKC ? g.B + (long)n0 * g.ldb : g.B + n0;
   };
   auto stage_first = [&](const bf16* bA, const bf16* bB) {   // K-tiles 0 .. NSLOT4-1 -> slots 0 .. 4
     for (int kt = 0; kt < NSLOT4; ++kt)
@@ -1325,64 +933,33 @@ __global__ void __launch_bounds__(NT4, 1) gemm4p_kernel(BigArgs g) {
         if (INIT) mma16_acc0(acc[s][jj], fb[H][jj], fa[H][s]);
         else mma16_acc(acc[s][jj], fb[H][jj], fa[H][s]);
       };
-      // EEGF_P_READS 1: the next K-tile's 16 fragment reads issued in groups 0..5 (fb in 0..3 two per
-      // group beside that group's fa, fa 4..7 in 4..5), so the last two groups carry no LDS read and the
-      // lgkmcnt(0) ahead of the barrier finds them landed; 0: one fa + one fb per group (fb[7] read in
-      // group 7, ~6 MFMAs before the wait)
-      // EEGF_P_PROBE (diagnostic builds only, results wrong): 1 no staging after the first K-tiles,
-      // 2 = 1 + no per-K-tile waits or barrier, 3 staging as built with no per-K-tile vmcnt waits
+      // the next K-tile's fragments: one fa + one fb per 8-MFMA group (fb[7] read in group 7, ~6 MFMAs
+      // before the wait); issuing them in groups 0..5 measured the same
       auto rd_next = [&](int s, int jj) __attribute__((always_inline)) {
         if (!more) return;
-        if (EEGF_P_READS == 0) {
-          if (jj == 0) fa[H ^ 1][s] = rdA(nimg, s);
-          if (jj == 1) fb[H ^ 1][s] = rdB(nimg, s);
-        } else if (s < 4) {
-          if (jj == 0) fa[H ^ 1][s] = rdA(nimg, s);
-          if (jj == 1) fb[H ^ 1][2 * s] = rdB(nimg, 2 * s);
-          if (jj == 3) fb[H ^ 1][2 * s + 1] = rdB(nimg, 2 * s + 1);
-        } else if (s < 6) {
-          if (jj == 0) fa[H ^ 1][2 * s - 4] = rdA(nimg, 2 * s - 4);
-          if (jj == 1) fa[H ^ 1][2 * s - 3] = rdA(nimg, 2 * s - 3);
-        }
+        if (jj == 0) fa[H ^ 1][s] = rdA(nimg, s);
+        if (jj == 1) fb[H ^ 1][s] = rdB(nimg, s);
       };
-      // EEGF_P_STAGGER 1: wave w issues its LDS-DMA of group s after the group's MFMA 2 w, so at any moment
-      // one wave of the CU is issuing one (the waves run the K-tile in lockstep: with the DMA at the same
-      // place in every wave, four queue for the CU's address unit at once and stall their MFMA streams)
-      const bool stw = st && EEGF_P_PROBE != 1 && EEGF_P_PROBE != 2;
 #pragma unroll
       for (int s = 0; s < 8; ++s) {
         mma(s, 0);
         rd_next(s, 0);
-        if (EEGF_P_STAGGER && stw && wave == 0) stage_part(sA, sB, slot, s, NOP0{});
         __builtin_amdgcn_sched_barrier(0);
         mma(s, 1);
         rd_next(s, 1);
         __builtin_amdgcn_sched_barrier(0);
         mma(s, 2);
-        if (EEGF_P_STAGGER ? stw && wave == 1 : stw) stage_part(sA, sB, slot, s, NOP0{});
+        if (st) stage_part(sA, sB, slot, s, NOP0{});
         __builtin_amdgcn_sched_barrier(0);
-        mma(s, 3);
-        rd_next(s, 3);
-        __builtin_amdgcn_sched_barrier(0);
-        mma(s, 4);
-        if (EEGF_P_STAGGER && stw && wave == 2) stage_part(sA, sB, slot, s, NOP0{});
-        __builtin_amdgcn_sched_barrier(0);
-        mma(s, 5);
-        __builtin_amdgcn_sched_barrier(0);
-        mma(s, 6);
-        if (EEGF_P_STAGGER && stw && wave == 3) stage_part(sA, sB, slot, s, NOP0{});
-        __builtin_amdgcn_sched_barrier(0);
-        mma(s, 7);
-      }
-      if constexpr (EEGF_P_PROBE == 2) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        return;
+#pragma unroll
+        for (int jj = 3; jj < 8; ++jj) {
+          mma(s, jj);
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
       // K-tile k + 2 retired (its fragments are read in the next K-tile): skipped when it landed before
       // the tile started (cross-staged, k + 2 <= 4) or when there is no such K-tile of this tile
-      if (EEGF_P_PROBE == 3) {
-        // probe 3: LDS-DMA issued as built, never waited for (results wrong): the DMA issue cost alone
-      } else if (!(landed && k < NSLOT4 - 2) && k + 2 < nk) {
+      if (!(landed && k < NSLOT4 - 2) && k + 2 < nk) {
         if (!TAIL || cross) vm_wait_tiles(NSLOT4 - 2);
         else vm_wait_tiles(max(0, min(nk - 1, k + NSLOT4) - (k + 2)));
       } else if (!cross && k + 2 >= nk) {
@@ -1442,327 +1019,38 @@ __global__ void __launch_bounds__(NT4, 1) gemm4p_kernel(BigArgs g) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// gemm4q: gemm4p with every K-contiguous operand staged in WHOLE 128-B lines.  gemm4p's LDS-DMA
-// instruction covers 16 rows x 64 B of a K-contiguous operand (one 32-deep K-tile of each row: half
-// of every 128-B line it touches); from L2-resident sources the CU's LDS-DMA path moves 31 B/cycle in
-// that pattern and 46 B/cycle in 8 rows x 128 B (profiles/r4e_dma_line_pattern.log), while a 256x256
-// K-tile needs 32 KB per 1,024 MFMA cycles, so gemm4p's forward K-loop ran at the DMA ceiling (its
-// no-staging probe: FFN2 forward 283 -> 207 us, profiles/r4c_gemm_probe_ab.log).  Here:
-//   * the ring holds K-tile PAIRS (64 deep) in operand images of 32 KB: [256 rows][64 k] per
-//     K-contiguous operand (16-B chunk c of row r stored at c ^ (r & 7): conflict-free ds_read_b128),
-//     [64 k][256 cols] per k-major operand (gemm4p's swz_k image, two K-tiles stacked);
-//   * default (EEGF_Q_RING5): five operand slots, A of pair u in slot 2u mod 5 and B in 2u + 1 mod 5;
-//     pair t + 2's A is staged during pair t's even K-tile (into pair t - 1's B slot), its B during the
-//     odd one (into pair t's A slot, free since the barrier that ended the even K-tile): 32 KB per
-//     K-tile, one part per 8-MFMA group.  The first form (EEGF_Q_RING5=0, two 64-KB pair slots) staged
-//     all of pair t + 2 in pair t's odd K-tile: 64 KB there and none in the even one;
-//   * one vmcnt + one barrier per pair (end of the even K-tile), none at odd K-tiles;
-//   * the same MFMA K order as gemm4p (bitwise identical results), the same epilogue (p_store_tile) and
-//     cross-tile staging (the last two pairs stage the next tile's pairs 0 and 1).
+// Whole-line staging of the persistent GEMMs (round 4, profiles/r4e_dma_line_pattern.log): gemm4p's
+// LDS-DMA instruction covers 16 rows x 64 B of a K-contiguous operand (one 32-deep K-tile: half of every
+// 128-B line it touches), which the CU's DMA path moves at 31 B/cycle from L2 against 46 B/cycle for
+// 8 rows x 128 B, while a 256x256 K-tile needs 32 KB per 1,024 MFMA cycles.  gemm4r therefore stages
+// K-tile PAIRS (64 deep) as operand images of 32 KB: [256 rows][64 k] per K-contiguous operand (16-B
+// chunk c of row r stored at c ^ (r & 7): conflict-free ds_read_b128), [64 k][256 cols] per k-major one
+// (gemm4p's swz_k image, two K-tiles stacked), 32 KB staged per K-tile, one 1-KB part per 8-MFMA group.
+// (The first whole-line kernel, gemm4q, held a whole K-tile of A fragments in registers over a
+// five-slot ring; gemm4r replaced it in round 5 with bitwise the same results, and it was retired in
+// round 6 with the other superseded kernels: gemm_big_kernel, gemm8, gemm4h -- git history, 829c7a6.)
 // Needs K % 64 == 0 and K >= 128 (launch_big routes other shapes to gemm4p).
-constexpr int BKP = 64, PSLOT = 2 * TM * BKP;          // K per pair, elements per pair slot (64 KB)
-constexpr int HSLOT = TM * BKP;                        // one operand of a pair (32 KB)
+constexpr int BKP = 64;                                // K per pair
+constexpr int HSLOT = TM * BKP;                        // one operand image of a pair (32 KB)
 #ifndef EEGF_Q_NOP
 #define EEGF_Q_NOP 0
 #endif
-// EEGF_Q_RING5 1 (default): the five-slot ring above; 64 KB per odd K-tile was above the 46 B/cycle the
-// CU's DMA path moves in whole lines (forward GEMMs 3-6 % faster, profiles/r4u_gemm4q_ring5_ab.log)
-#ifndef EEGF_Q_RING5
-#define EEGF_Q_RING5 1
-#endif
 #ifndef EEGF_Q_SPOS
-#define EEGF_Q_SPOS 4      // R5: the group's LDS-DMA part goes after its MFMA EEGF_Q_SPOS (0..7)
+#define EEGF_Q_SPOS 4      // the group's LDS-DMA part goes after its MFMA EEGF_Q_SPOS (0..7)
 #endif
-// Persistent tile walk of gemm4q (eegf_tune key 15).  order 0 (default): round r of workgroup b takes
-// logical tile r * G + xcd_remap(b), so each round an XCD runs the next contiguous block of 32 tiles of
-// the whole grid.  order 1 (XCD-blocked): XCD x = b % 8 owns the contiguous logical range
-// [x chunk, (x + 1) chunk) of the grouped raster and its G / 8 workgroups walk it in rounds, so an
-// XCD's consecutive rounds stay on the same row panels.  order 2 is a timing probe only (wrong
-// results): every tile reads its operands from 4 row x 4 column panels per XCD (L2-resident), stores
-// where order 0 would.  Probe bits (timing only, wrong results): + 4 no epilogue stores, + 8 no LDS-DMA
-// after the first tile's prologue (the K-loop reads stale LDS), + 16 stores from even workgroups only,
-// + 32 odd workgroups start (g.ksplit / 100) us late (desynchronised epilogues; the delay counts).
+// Persistent tile walk: round r of workgroup b takes logical tile r * G + xcd_remap(b), so each round an
+// XCD runs the next contiguous block of 32 tiles of the whole grid (tile_coords' grouped raster keeps
+// them on few A panels).  An XCD-blocked walk measured neutral (profiles/r5a_order_ab.log).
 struct QWalk {
   int L, end, step;
 };
-DEV QWalk q_walk(const BigArgs& g, int ntiles) {
-  const int G = gridDim.x, b = blockIdx.x;
-  if ((g.order & 3) == 1 && G % 8 == 0 && G >= 16) {
-    const int x = b & 7, chunk = (ntiles + 7) / 8;
-    return {x * chunk + (b >> 3), min(ntiles, (x + 1) * chunk), G >> 3};
-  }
-  return {xcd_remap(b, G), ntiles, G};
-}
-template <bool BKC, int EPI, bool ACC = false>
-__global__ void __launch_bounds__(NT4, 1) gemm4q_kernel(BigArgs g) {
-  constexpr bool HAS_BIAS = EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_D;
-  constexpr bool R5 = EEGF_Q_RING5 != 0;
-  static_assert(!(R5 && EEGF_P_STAGGER), "the staggered DMA placement is a two-slot-ring probe");
-  __shared__ __attribute__((aligned(16))) bf16 lds[R5 ? 5 * HSLOT : 2 * PSLOT];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  const int tiles_n = g.N / TN, tiles_m = g.M / TM, ntiles = tiles_m * tiles_n;
-  const int G = gridDim.x;
-  const int np = g.K / BKP;                            // pairs per tile (>= 2)
-  const QWalk walk = q_walk(g, ntiles);
-  int L = walk.L;
-  if (L >= walk.end) return;
-  if ((g.order & 32) && (blockIdx.x & 1)) {      // timing probe: desynchronise the odd workgroups
-    const long long t0 = __builtin_amdgcn_s_memrealtime();
-    while (__builtin_amdgcn_s_memrealtime() - t0 < g.ksplit) __builtin_amdgcn_s_sleep(2);
-  }
-
-  // Staging, 16 parts per pair and wave (8 A, 8 B), each one wave-instruction of 1 KB.
-  // K-contiguous part j: rows (8 wave + j) 8 + lane / 8, 16-B chunk lane & 7 of the row's 128 B, read from
-  // source chunk (lane & 7) ^ (row & 7); row & 7 = lane / 8 for every part, so one per-lane offset serves
-  // all parts (a part's first row is a uniform offset of the SGPR base).
-  // k-major part j: k-rows (8 wave + j) 2 + lane / 32 (512 B each), 16-B column chunk (lane & 31) ^
-  // swz_k(k); swz_k reads k bits 0, 1, 3 = lane / 32, j & 1, j >> 2: four per-lane offsets.
-  const int kr = lane >> 3;
-  const uint32_t voffA = (uint32_t)(((long)kr * g.lda + ((lane & 7) ^ kr) * 8) * 2);
-  uint32_t voffB[4];
-  if (BKC) {
-    voffB[0] = (uint32_t)(((long)kr * g.ldb + ((lane & 7) ^ kr) * 8) * 2);
-  } else {
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int j = (v & 1) | ((v >> 1) << 2);
-      const int k = (wave * 8 + j) * 2 + (lane >> 5);
-      voffB[v] = (uint32_t)(((long)(lane >> 5) * g.ldb + ((lane & 31) ^ swz_k(k)) * 8) * 2);
-    }
-  }
-  const long pstepB = BKC ? BKP : (long)BKP * g.ldb;
-  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr_of(lds));
-  // ps: pair slot (its A image at 0, B at TM * BKP) or, R5, the operand slot of the part (A parts j < 8,
-  // B parts j >= 8)
-  // NopC: wait states after the M0 write.  The K-loop's bases are SALU-computed (isa_lint: no
-  // VALU-written base within 5 states of any of its DMAs), so its DMAs need only the 1 state after the
-  // M0 write (EEGF_Q_NOP); the prologue's come right after tile_base's v_readfirstlane and keep 3, as
-  // gemm4p's do (once per tile: free), so they stay safe whatever the codegen puts in between
-  using QNOP = std::integral_constant<int, EEGF_Q_NOP>;
-  using PNOP = std::integral_constant<int, 3>;
-  auto stage_part = [&](const bf16* bA, const bf16* bB, int ps, int j, auto NopC) __attribute__((always_inline)) {
-    const int jj = j & 7, pr = wave * 8 + jj;
-    constexpr int NOP = decltype(NopC)::value;
-    const int b0 = R5 ? ps * HSLOT : ps * PSLOT + TM * BKP;    // element offset of the B image
-    if (j < 8) {
-      glds16_asm_sa<NOP>(bA + (long)pr * 8 * g.lda, voffA, lds0 + 2u * ((R5 ? ps * HSLOT : ps * PSLOT) + pr * 8 * BKP));
-    } else if (BKC) {
-      glds16_asm_sa<NOP>(bB + (long)pr * 8 * g.ldb, voffB[0], lds0 + 2u * (b0 + pr * 8 * BKP));
-    } else {
-      glds16_asm_sa<NOP>(bB + (long)pr * 2 * g.ldb, voffB[(jj & 1) | ((jj >> 2) << 1)], lds0 + 2u * (b0 + pr * 2 * TN));
-    }
-  };
-  auto tile_base = [&](int l, const bf16*& bA, const bf16*& bB, int& m0, int& n0) {
-    int tm, tn;
-    tile_coords(g, l, tiles_m, tiles_n, tm, tn);
-    m0 = __builtin_amdgcn_readfirstlane(tm * TM);
-    n0 = __builtin_amdgcn_readfirstlane(tn * TN);
-    int am = m0, bn = n0;
-    if ((g.order & 3) == 2) {    // timing probe: operands from an L2-resident panel set (wrong results)
-      am = __builtin_amdgcn_readfirstlane((((tm & 3) + 4 * (blockIdx.x & 7)) % tiles_m) * TM);
-      bn = __builtin_amdgcn_readfirstlane((tn & 3) % tiles_n * TN);
-    }
-    bA = g.A + (long)am * g.lda;
-    bB = BKC ? g.B + (long)bn * g.ldb : g.B + bn;
-  };
-  // fragments.  K-contiguous [256][64] image: half h of a pair (K-tile 2t + h) is chunk 4 h + fq of rows
-  // r0 + fr (r0 % 16 == 0, so the swizzle is fr & 7); k-major: gemm4p's rd_col offsets, half 1 32 k-rows on
-  const int fr = lane & 15, fq = lane >> 4;
-  const int offA0 = (wm * 128 + fr) * BKP + ((fq ^ (fr & 7)) << 3);
-  const int offA1 = (wm * 128 + fr) * BKP + (((4 + fq) ^ (fr & 7)) << 3);
-  constexpr int BIMG = R5 ? 0 : TM * BKP;     // B image offset from the image base rdB is given
-  const int offB0 = BIMG + (wn * 128 + fr) * BKP + ((fq ^ (fr & 7)) << 3);
-  const int offB1 = BIMG + (wn * 128 + fr) * BKP + (((4 + fq) ^ (fr & 7)) << 3);
-  int tB0[8], tB1[8];
-  if (!BKC) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int q = fr >> 2, p4 = fr & 3;
-      const int col = wn * 128 + 16 * i + 4 * p4, ch = col >> 3, off = col & 7;
-      const int ka = 8 * fq + q, kb = ka + 4;
-      tB0[i] = BIMG + ka * TN + (((ch ^ swz_k(ka)) << 3) | off);
-      tB1[i] = BIMG + kb * TN + (((ch ^ swz_k(kb)) << 3) | off);
-    }
-  }
-  auto rdA = [&](const bf16* img, auto Hc, int i) {
-    return *(const bf16x8*)(img + (decltype(Hc)::value ? offA1 : offA0) + i * 16 * BKP);
-  };
-  auto rdB = [&](const bf16* img, auto Hc, int i) {
-    constexpr int h = decltype(Hc)::value;
-    return BKC ? *(const bf16x8*)(img + (h ? offB1 : offB0) + i * 16 * BKP)
-               : rd_col_off(img + h * 32 * TN, tB0[i], tB1[i]);
-  };
-  using C0 = std::integral_constant<int, 0>;
-  using C1 = std::integral_constant<int, 1>;
-
-  const bf16* baseA;
-  const bf16* baseB;
-  int m0, n0;
-  tile_base(L, baseA, baseB, m0, n0);
-#pragma unroll 1
-  for (int j = 0; j < 16; ++j) stage_part(baseA, baseB, R5 ? j >> 3 : 0, j, PNOP{});                 // pair 0
-#pragma unroll 1
-  for (int j = 0; j < 16; ++j) stage_part(baseA + BKP, baseB + pstepB, R5 ? 2 + (j >> 3) : 1, j, PNOP{});  // pair 1
-  f32x4 acc[8][8];
-  int ps0 = 0;                  // pair slot of the tile's pair 0 (R5: operand slot of its A, 0..4)
-  bool landed = false;          // the tile's pairs 0 and 1 retired (cross-staged and waited for)
-  for (;;) {
-    const int Ln = L + walk.step;
-    const bool more_tiles = Ln < walk.end;
-    int m0n = 0, n0n = 0;
-    const bf16* nA = nullptr;
-    const bf16* nB = nullptr;
-    if (more_tiles) tile_base(Ln, nA, nB, m0n, n0n);
-    if (!landed) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");      // pair 0 (pair 1 younger)
-    raw_barrier();
-    bf16x8 fa[2][8], fb[2][8];
-    // R5 operand-slot arithmetic: slot + c mod 5 for 0 <= c <= 5 (uniform, on the SALU)
-    auto add5 = [](int x, int c) { const int y = x + c; return y >= 5 ? y - 5 : y; };
-    {
-      const bf16* img0 = lds + (R5 ? ps0 * HSLOT : ps0 * PSLOT);
-      const bf16* imb0 = R5 ? lds + add5(ps0, 1) * HSLOT : img0;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        fa[0][i] = rdA(img0, C0{}, i);
-        fb[0][i] = rdB(imb0, C0{}, i);
-      }
-    }
-    // K-tile s = 2 t + H of pair t (slot ps = (ps0 + t) & 1): its fragments are in fa / fb[H]; the next
-    // K-tile's are read into [H ^ 1] (H = 0: the same slot's half 1; H = 1: pair t + 1's half 0); the odd
-    // K-tile stages pair t + 2 (or the next tile's pair t + 2 - np) into slot ps
-    // TAIL (the last two pairs): whether there is a next K-tile to read and what to stage are decided at
-    // run time; in the steady state (t + 2 < np) both are compile-time true, so the K-tile body carries no
-    // branch and hipcc's waitcnt pass sees straight-line LDS reads
-    // hA (R5): operand slot of pair t's A
-    auto ktile = [&](auto Hc, int t, int hA, auto Ic, auto Tc) __attribute__((always_inline)) {
-      constexpr int H = decltype(Hc)::value;
-      constexpr bool INIT = decltype(Ic)::value, TAIL = decltype(Tc)::value;
-      const int ps = R5 ? hA : (ps0 + t) & 1;
-      const bool more = !TAIL || H == 0 || t + 1 < np;
-      // next K-tile's images: R5 operand slots of pair t (H = 0) or t + 1 (H = 1)
-      const bf16* nimg = R5 ? lds + add5(hA, 2 * H) * HSLOT : lds + (H == 0 ? ps : ps ^ 1) * PSLOT;
-      const bf16* nimb = R5 ? lds + add5(hA, 2 * H + 1) * HSLOT : nimg;
-      const bool own = !TAIL || t + 2 < np;
-      // R5: both K-tiles stage (A of pair t + 2 into pair t - 1's B slot, B into pair t's A slot)
-      const bool st = (R5 || H == 1) && (own || more_tiles) && !(g.order & 8);
-      const int sslot = R5 ? (H == 0 ? add5(hA, 4) : hA) : ps;
-      const bf16* sA = own ? baseA + (t + 2) * BKP : nA + (t + 2 - np) * BKP;
-      const bf16* sB = own ? baseB + (t + 2) * pstepB : nB + (t + 2 - np) * pstepB;
-      auto mma = [&](int s8, int jj) {
-        if (INIT) mma16_acc0(acc[s8][jj], fb[H][jj], fa[H][s8]);
-        else mma16_acc(acc[s8][jj], fb[H][jj], fa[H][s8]);
-      };
-      using HN = std::integral_constant<int, H ^ 1>;
-#pragma unroll
-      for (int s8 = 0; s8 < 8; ++s8) {
-        auto r5st = [&](int pos) __attribute__((always_inline)) {
-          if (R5 && pos == EEGF_Q_SPOS && st) stage_part(sA, sB, sslot, 8 * H + s8, QNOP{});
-        };
-        mma(s8, 0);
-        if (more) fa[H ^ 1][s8] = rdA(nimg, HN{}, s8);
-        r5st(0);
-        __builtin_amdgcn_sched_barrier(0);
-        mma(s8, 1);
-        if (more) fb[H ^ 1][s8] = rdB(nimb, HN{}, s8);
-        r5st(1);
-        __builtin_amdgcn_sched_barrier(0);
-        if (EEGF_P_STAGGER) {     // wave w: its two parts after MFMAs 2 w and 2 w + 1 of the group
-          if (H == 1 && st && wave == 0) stage_part(sA, sB, ps, 2 * s8, QNOP{});
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        mma(s8, 2);
-        r5st(2);
-        if (!R5 && (EEGF_P_STAGGER ? H == 1 && st && wave == 1 : H == 1 && st)) stage_part(sA, sB, ps, 2 * s8, QNOP{});
-        if (EEGF_P_STAGGER && H == 1 && st && wave == 0) stage_part(sA, sB, ps, 2 * s8 + 1, QNOP{});
-        __builtin_amdgcn_sched_barrier(0);
-        mma(s8, 3);
-        r5st(3);
-        if (EEGF_P_STAGGER && H == 1 && st && wave == 1) stage_part(sA, sB, ps, 2 * s8 + 1, QNOP{});
-        __builtin_amdgcn_sched_barrier(0);
-        mma(s8, 4);
-        r5st(4);
-        if (!R5 && (EEGF_P_STAGGER ? H == 1 && st && wave == 2 : H == 1 && st))
-          stage_part(sA, sB, ps, 2 * s8 + (EEGF_P_STAGGER ? 0 : 1), QNOP{});
-        __builtin_amdgcn_sched_barrier(0);
-        mma(s8, 5);
-        r5st(5);
-        if (EEGF_P_STAGGER && H == 1 && st && wave == 2) stage_part(sA, sB, ps, 2 * s8 + 1, QNOP{});
-        __builtin_amdgcn_sched_barrier(0);
-        mma(s8, 6);
-        r5st(6);
-        if (EEGF_P_STAGGER && H == 1 && st && wave == 3) stage_part(sA, sB, ps, 2 * s8, QNOP{});
-        __builtin_amdgcn_sched_barrier(0);
-        mma(s8, 7);
-        r5st(7);
-        if (EEGF_P_STAGGER && H == 1 && st && wave == 3) stage_part(sA, sB, ps, 2 * s8 + 1, QNOP{});
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if (H == 0) {
-        // pair t + 1 (staged during pair t - 1's odd K-tile, the only DMAs in flight) must have landed
-        // before the next K-tile reads its fragments; the barrier also frees pair t's slot for pair t + 2
-        // (R5: except this K-tile's 8 A parts of pair t + 2)
-        if (R5) {
-          if (!TAIL || t + 1 < np) {
-            if (st) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          }
-        } else if ((!TAIL || t + 1 < np) && !(landed && t == 0)) {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        raw_barrier();
-      }
-    };
-    using F = std::false_type;
-    using T = std::true_type;
-    int hA = ps0;
-    if (np > 2) {
-      ktile(C0{}, 0, hA, T{}, F{});
-      ktile(C1{}, 0, hA, F{}, F{});
-    } else {
-      ktile(C0{}, 0, hA, T{}, T{});
-      ktile(C1{}, 0, hA, F{}, T{});
-    }
-    hA = add5(hA, 2);
-#pragma unroll 1
-    for (int t = 1; t + 2 < np; ++t) {
-      ktile(C0{}, t, hA, F{}, F{});
-      ktile(C1{}, t, hA, F{}, F{});
-      hA = add5(hA, 2);
-    }
-#pragma unroll 1
-    for (int t = max(1, np - 2); t < np; ++t) {
-      ktile(C0{}, t, hA, F{}, T{});
-      ktile(C1{}, t, hA, F{}, T{});
-      hA = add5(hA, 2);
-    }
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-    const int mrow = m0 + wm * 128 + (lane & 15);
-    const int ncol = n0 + wn * 128 + 4 * (lane >> 4);
-    f32x4 biasv[8];
-    if (HAS_BIAS) load_bias8(biasv, g.bias + ncol);
-    // the next tile's pairs 0 and 1 (cross-staged) retired before the first store
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    if (!(g.order & 4) && !((g.order & 16) && (blockIdx.x & 1))) p_store_tile<EPI, ACC>(g, acc, biasv, mrow, n0, wn, lane);
-    if (!more_tiles) break;
-    L = Ln;
-    m0 = m0n;
-    n0 = n0n;
-    baseA = nA;
-    baseB = nB;
-    landed = true;
-    ps0 = R5 ? hA : (ps0 + np) & 1;
-  }
-}
+DEV QWalk q_walk(int ntiles) { return {xcd_remap(blockIdx.x, gridDim.x), ntiles, (int)gridDim.x}; }
 
 // ---------------------------------------------------------------------------------------------
-// gemm4r: gemm4q with ROLLING A fragments.  Each A fragment is used by one 8-MFMA group, so it is read
-// two groups ahead (across the K-tile boundary too) into four register sets instead of a whole K-tile
-// ahead into sixteen: 48 fewer VGPRs in the K-loop.  The price is the ring: pair t's A image is read
-// until the end of its odd K-tile, so it cannot take pair t + 2's B there as gemm4q's ring does.
+// gemm4r: the whole-line K-tile pairs above with ROLLING A fragments.  Each A fragment is used by one
+// 8-MFMA group, so it is read two groups ahead (across the K-tile boundary too) into four register sets
+// instead of a whole K-tile ahead into sixteen (gemm4q): 48 fewer VGPRs in the K-loop.  The price is the
+// ring: pair t's A image is read until the end of its odd K-tile, so it cannot take pair t + 2's B there.
 // Instead A images rotate through three slots and B images through two (A of global pair u in slot
 // 2 (u mod 3), B in 1 + 2 (u mod 2)): pair t + 2's A is staged during pair t's even K-tile into pair
 // t - 1's A slot (free since the barrier that ends pair t - 1's odd K-tile -- a second barrier per
@@ -1778,7 +1066,7 @@ __global__ void __launch_bounds__(NT4, 1) gemm4r_kernel(BigArgs g) {
   const int wm = wave >> 1, wn = wave & 1;
   const int tiles_n = g.N / TN, tiles_m = g.M / TM, ntiles = tiles_m * tiles_n;
   const int np = g.K / BKP;
-  const QWalk walk = q_walk(g, ntiles);
+  const QWalk walk = q_walk(ntiles);
   int L = walk.L;
   if (L >= walk.end) return;
 
@@ -1952,7 +1240,7 @@ __global__ void __launch_bounds__(NT4, 1) gemm4r_kernel(BigArgs g) {
     if (HAS_BIAS) load_bias8(biasv, g.bias + ncol);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    p_store_tile<EPI, ACC, false>(g, acc, biasv, mrow, n0, wn, lane);
+    p_store_tile<EPI, ACC>(g, acc, biasv, mrow, n0, wn, lane);
     if (!more_tiles) break;
     L = Ln;
     m0 = m0n;
@@ -1965,185 +1253,14 @@ __global__ void __launch_bounds__(NT4, 1) gemm4r_kernel(BigArgs g) {
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// 4-wave 256x128 kernel for the K = 768 bf16-output GEMMs with heavy epilogues (QKV and FFN1
-// forward with bias / GELU / GELU', the out-projection, the input gradients with an activation
-// product): the same K-loop as gemm4w (asm LDS-DMA in the saddr form, next K-tile's fragments read
-// inside the current one's MFMA shadows, accumulators pinned to AGPRs, one counted vmcnt + one
-// barrier per K-tile) on a half-width tile: 2 x 2 waves of 128x64 (128 accumulator AGPRs, <= 256
-// registers per lane) and a 3-deep ring of BK = 32 K-tiles (3 x 24 KB), so TWO workgroups share a
-// CU and one's epilogue (bias / GELU VALU, LDS-staged stores) runs under the other's MFMAs — the
-// one-workgroup-per-CU kernels leave the MFMA idle for the whole epilogue.
-// A K-contiguous; B K-contiguous (forward) or k-major (input gradient).
-constexpr int TNH = 128, SLOTH = (TM + TNH) * BK4, NSLOTH = 3;
-constexpr int LDSH = NSLOTH * SLOTH > TM * (TNH + 8) ? NSLOTH * SLOTH : TM * (TNH + 8);
-static_assert(LDSH * 2 <= 80 * 1024, "two workgroups per CU");
-DEV void vm_wait_h(int n) {      // n younger K-tiles (6 LDS-DMAs each) may stay in flight
-  switch (n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-  }
-}
-
-template <bool BKC, int EPI>
-__global__ void __launch_bounds__(NT4, 2) gemm4h_kernel(BigArgs g) {
-  __shared__ __attribute__((aligned(16))) bf16 lds[LDSH];   // ring NSLOTH x 24 KB | epilogue tile
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  ts_mark(g, 0);
-  const int wm = wave >> 1, wn = wave & 1;
-  const int tiles_n = (g.N + TNH - 1) / TNH, tiles_m = (g.M + TM - 1) / TM;
-  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  int tm, tn;
-  tile_coords(g, t, tiles_m, tiles_n, tm, tn);
-  const int m0 = tm * TM, n0 = tn * TNH;
-  const int nk = g.K / BK4;
-
-  // staging per K-tile: 4 A parts (16 rows x 64 B each) + 2 B parts per wave; B k-major: [32 k][128 cols]
-  // images, 4 k-rows x 256 B per wave-instruction, 16-B column chunk (lane & 15) ^ swz_k(k)
-  auto voffA = [&](int j) -> uint32_t {
-    const int r = (wave * 4 + j) * 16 + (lane >> 2);
-    const int c = (lane & 3) ^ sw4(r);
-    return (uint32_t)(((long)(min(m0 + r, g.M - 1) - m0) * g.lda + c * 8) * 2);
-  };
-  auto voffB = [&](int j) -> uint32_t {
-    if (BKC) {
-      const int r = (wave * 2 + j) * 16 + (lane >> 2);
-      const int c = (lane & 3) ^ sw4(r);
-      return (uint32_t)(((long)(min(n0 + r, g.N - 1) - n0) * g.ldb + c * 8) * 2);
-    }
-    const int k = (wave * 2 + j) * 4 + (lane >> 4);
-    const int c = (lane & 15) ^ swz_k(k);
-    return (uint32_t)(((long)k * g.ldb + min(n0 + c * 8, g.N - 8) - n0) * 2);
-  };
-  uint32_t vA[4], vB[2];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) vA[j] = voffA(j);
-#pragma unroll
-  for (int j = 0; j < 2; ++j) vB[j] = voffB(j);
-  const bf16* baseA = g.A + (long)m0 * g.lda;
-  const bf16* baseB = BKC ? g.B + (long)n0 * g.ldb : g.B + n0;
-  const long stepB = BKC ? BK4 : (long)BK4 * g.ldb;
-  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr_of(lds));
-  auto stage_part = [&](int kt, int slot, int j) {      // part j (0-3 A, 4-5 B) of K-tile kt -> slot
-    if (j < 4) {
-      glds16_asm_sa(baseA + kt * BK4, vA[j], lds0 + 2u * (slot * SLOTH + (wave * 4 + j) * 16 * BK4));
-    } else {
-      const int jb = j - 4;
-      glds16_asm_sa(baseB + kt * stepB, vB[jb],
-                    lds0 + 2u * (slot * SLOTH + TM * BK4 + (BKC ? (wave * 2 + jb) * 16 * BK4 : (wave * 2 + jb) * 4 * TNH)));
-    }
-  };
-  const int fr = lane & 15, fq = lane >> 4;
-  const int offA = (wm * 128 + fr) * BK4 + ((fq ^ sw4(fr)) << 3);
-  const int offB = TM * BK4 + (wn * 64 + fr) * BK4 + ((fq ^ sw4(fr)) << 3);
-  int tB0[4], tB1[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    if (!BKC) {
-      const int q = fr >> 2, p4 = fr & 3;
-      const int col = wn * 64 + 16 * i + 4 * p4, ch = col >> 3, off = col & 7;
-      const int ka = 8 * fq + q, kb = ka + 4;
-      tB0[i] = TM * BK4 + ka * TNH + (((ch ^ swz_k(ka)) << 3) | off);
-      tB1[i] = TM * BK4 + kb * TNH + (((ch ^ swz_k(kb)) << 3) | off);
-    }
-  }
-  auto rdA = [&](const bf16* img, int i) { return *(const bf16x8*)(img + offA + i * 16 * BK4); };
-  auto rdB = [&](const bf16* img, int i) {
-    return BKC ? *(const bf16x8*)(img + offB + i * 16 * BK4) : rd_col_off(img, tB0[i], tB1[i]);
-  };
-
-  f32x4 acc[8][4];
-  for (int kt = 0; kt < NSLOTH; ++kt)
-    if (kt < nk)
-      for (int j = 0; j < 6; ++j) stage_part(kt, kt, j);
-  vm_wait_h(max(0, min(nk, NSLOTH) - 2));
-  raw_barrier();
-  bf16x8 fa[2][8], fb[2][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) fa[0][i] = rdA(lds, i);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) fb[0][i] = rdB(lds, i);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  raw_barrier();
-  ts_mark(g, 1);
-
-  auto ktile = [&](auto Hc, int k, int slot, int nslot, auto Ic, auto Tc) __attribute__((always_inline)) {
-    constexpr int H = decltype(Hc)::value;
-    constexpr bool INIT = decltype(Ic)::value, TAIL = decltype(Tc)::value;
-    const bool more = !TAIL || k + 1 < nk, st = !TAIL || k + NSLOTH < nk;
-    const bf16* nimg = lds + nslot * SLOTH;
-    auto mma = [&](int s, int jj) {
-      if (INIT) mma16_acc0(acc[s][jj], fb[H][jj], fa[H][s]);
-      else mma16_acc(acc[s][jj], fb[H][jj], fa[H][s]);
-    };
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      mma(s, 0);
-      if (more) fa[H ^ 1][s] = rdA(nimg, s);
-      __builtin_amdgcn_sched_barrier(0);
-      mma(s, 1);
-      if (more && s < 4) fb[H ^ 1][s] = rdB(nimg, s);
-      __builtin_amdgcn_sched_barrier(0);
-      mma(s, 2);
-      if (st && s < 6) stage_part(k + NSLOTH, slot, s);
-      __builtin_amdgcn_sched_barrier(0);
-      mma(s, 3);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    // K-tile k + 2 retired (its fragments are read in the next K-tile); younger: k + 3
-    if (!TAIL) vm_wait_h(NSLOTH - 2);
-    else vm_wait_h(max(0, min(nk - 1, k + NSLOTH) - (k + 2)));
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads of k + 1 done: its slot may be restaged
-    raw_barrier();
-  };
-  using C0 = std::integral_constant<int, 0>;
-  using C1 = std::integral_constant<int, 1>;
-  using F = std::false_type;
-  using T = std::true_type;
-  auto nxt = [](int sl) { return sl == NSLOTH - 1 ? 0 : sl + 1; };
-  int slot = 0;
-  if (nk > NSLOTH) ktile(C0{}, 0, slot, nxt(slot), T{}, F{});
-  else ktile(C0{}, 0, slot, nxt(slot), T{}, T{});
-  slot = nxt(slot);
-  int kt = 1;
-  for (; kt + 1 + NSLOTH < nk; kt += 2) {
-    ktile(C1{}, kt, slot, nxt(slot), F{}, F{});
-    slot = nxt(slot);
-    ktile(C0{}, kt + 1, slot, nxt(slot), F{}, F{});
-    slot = nxt(slot);
-  }
-  for (; kt < nk; kt += 2) {
-    ktile(C1{}, kt, slot, nxt(slot), F{}, T{});
-    slot = nxt(slot);
-    if (kt + 1 < nk) {
-      ktile(C0{}, kt + 1, slot, nxt(slot), F{}, T{});
-      slot = nxt(slot);
-    }
-  }
-  // the asm MFMAs are opaque to the hazard recognizer: cover the result latency before the first
-  // accumulator read
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  ts_mark(g, 2);
-  big_epilogue<EPI, bf16, 4, NT4, TNH>(g, acc, lds, m0, n0, tid, lane, wm, wn);
-  ts_mark(g, 3);
-}
-
-int g_gemm4h = [] { const char* e = getenv("EEGF_GEMM4H"); return e ? atoi(e) : 2; }();   // eegf_tune key 8
-// eegf_tune key 11: the persistent kernel (gemm4p_kernel) for the bf16-output GEMMs it takes: 0 off,
-// 1 (default) every eligible shape (full 256 x 256 tiles, K-contiguous A: every BERT forward and input
-// gradient of the bench step), 2 the GELU / GELU' forward GEMMs and the plain / residual-accumulating
-// input gradients with K >= 2048, 3 = 2 + the aux-product input gradient.  Whole-step interleaved A/B
-// after the widened stores and the cross-tile staging (profiles/r3y_step_ab.log): 1 < 3 < 2 in every
-// round (median 64.01 / 64.88 / 65.01 ms); before them the bias-only forwards lost on this kernel
-// (QKV 265 -> 293 us, profiles/r3f_p_ab.log)
-int g_store_nt = [] { const char* e = getenv("EEGF_STORE_NT"); return e ? atoi(e) : 0; }();   // eegf_tune key 12
-int g_gemm4p = [] { const char* e = getenv("EEGF_GEMM4P"); return e ? atoi(e) : 1; }();
-// key 14: the persistent GEMM's staging: 1 (default) whole 128-B lines (gemm4q) where K % 64 == 0 and
-// K >= 128, 0 gemm4p's 64-B half lines everywhere
-int g_gemm4q = [] { const char* e = getenv("EEGF_GEMM4Q"); return e ? atoi(e) : 2; }();
+// eegf_tune key 11: the persistent kernels (gemm4r / gemm4p) for the bf16-output GEMMs they take: 1
+// (default) every eligible shape (full 256 x 256 tiles, K-contiguous A: every BERT forward and input
+// gradient of the bench step), 0 none (gemm4w, the non-persistent 4-wave kernel: the bit-identity
+// reference of tests/test_gemm_gpu.py)
+int g_persistent = 1;
+// key 14: gemm4r (whole-line K-tile pairs, rolling A fragments) where K % 64 == 0 and K >= 128 (1,
+// default), or gemm4p's 64-B half lines everywhere (0); bitwise the same results
+int g_gemm4r = 1;
 int cu_count() {
   static const int cus = [] {
     int dev = 0, n = 256;
@@ -2153,10 +1270,6 @@ int cu_count() {
   return cus;
 }
 int g_cu_reserve = 0;      // eegf_tune key 13
-// key 18: the persistent GEMMs that take gemm4q on gemm4r (rolling A fragments) instead: 0 off, 1 on
-int g_gemm4r = [] { const char* e = getenv("EEGF_GEMM4R"); return e ? atoi(e) : 1; }();
-int g_tile_order = [] { const char* e = getenv("EEGF_TILE_ORDER"); return e ? atoi(e) : 0; }();   // key 15
-int g_probe_delay = [] { const char* e = getenv("EEGF_PROBE_DELAY"); return e ? atoi(e) : 0; }();   // key 16: the key-15 + 32 probe's start delay, s_memrealtime ticks (100 MHz)
 }  // namespace
 // workgroups of a persistent grid: every CU but the reserved ones (room for RCCL kernels, key 13)
 int persistent_cus() {
@@ -2164,99 +1277,40 @@ int persistent_cus() {
   return n > 0 ? n : 1;
 }
 namespace {
+// Routing of the 256-row GEMMs: bf16 outputs with a K-contiguous A on full tiles go to the persistent
+// kernel (gemm4r where K splits into >= 2 K-tile pairs, else gemm4p); everything else -- ragged M / N,
+// other epilogues, beta with an aux epilogue, and the fp32 split-K weight gradients -- to gemm4w.
 template <bool AKC, bool BKC, int EPI, typename TO>
 int launch_big(const BigArgs& a, int splits, hipStream_t s) {
   const int tiles = ((a.M + TM - 1) / TM) * ((a.N + TN - 1) / TN);
   if constexpr (AKC && sizeof(TO) == 2 && (EPI == EPI_NONE || EPI == EPI_BIAS || EPI == EPI_BIAS_GELU ||
                                            EPI == EPI_BIAS_GELU_D || (EPI == EPI_MUL_AUX && !BKC))) {
-    const bool won = EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_D || (EPI == EPI_NONE && !BKC && a.K >= 2048);
-    const bool p_ok = g_gemm4p == 1 || (g_gemm4p >= 2 && won) || (g_gemm4p == 3 && EPI == EPI_MUL_AUX);
     // beta * C: the EPI_NONE input tile only (the aux epilogue ignores beta, as big_epilogue does)
     const bool beta_ok = a.beta == 0.f || EPI == EPI_NONE;
     const bool aux_ok = EPI != EPI_MUL_AUX || (a.aux && a.ldaux % 8 == 0 && (((uintptr_t)a.aux) & 15) == 0);
-    if (p_ok && beta_ok && aux_ok && g_gemm8 < 0 && splits == 1 && !a.colsum_part && a.M % TM == 0 &&
-        a.N % TN == 0 && a.ldc % 8 == 0 && (((uintptr_t)a.C) & 15) == 0 &&
-        a.K % BK4 == 0 && (((uintptr_t)a.bias) & 15) == 0) {
+    if (g_persistent && beta_ok && aux_ok && splits == 1 && a.M % TM == 0 && a.N % TN == 0 && a.ldc % 8 == 0 &&
+        (((uintptr_t)a.C) & 15) == 0 && a.K % BK4 == 0 && (((uintptr_t)a.bias) & 15) == 0) {
       const dim3 grid(tiles < persistent_cus() ? tiles : persistent_cus());
-      BigArgs ap = a;
-      ap.store_nt = g_store_nt;
-      ap.order = g_tile_order;
-      if (g_tile_order & 32) ap.ksplit = g_probe_delay;
       bool acc = false;
       if constexpr (EPI == EPI_NONE) acc = a.beta != 0.f;
-      // whole-line staging (gemm4q) wherever K splits into >= 2 pairs of K-tiles (key 14 = 2, default):
-      // the forward layout (both operands K-contiguous) 3-6 % faster; the input gradients (k-major B)
-      // lost 1-6 % on its first, two-pair-slot ring (profiles/r4i_gemm_ab.log) and gain 3-5 % on the
-      // five-slot one (the K-contiguous dY in whole lines; profiles/r4ze_dgrad_gemm4q_ab.log).
-      // key 14 = 1: forward layout only, 0: gemm4p everywhere
-      const bool q = g_gemm4q >= 1 && (BKC || g_gemm4q == 2) && a.K % BKP == 0 && a.K >= 2 * BKP;
-      const bool r = q && g_gemm4r;
+      // whole-line staging wherever K splits into >= 2 pairs of K-tiles: the forward layout 3-6 % faster
+      // than gemm4p's half lines (profiles/r4u_gemm4q_ring5_ab.log), the input gradients 3-5 %
+      // (profiles/r4ze_dgrad_gemm4q_ab.log), gemm4r's rolling A fragments another 2-14 % (r5t_4r_ab.log)
+      const bool r = g_gemm4r && a.K % BKP == 0 && a.K >= 2 * BKP;
       if (acc) {
         if constexpr (EPI == EPI_NONE) {
-          if (r) EEGF_LAUNCH((gemm4r_kernel<BKC, EPI, true>), grid, dim3(NT4), 0, s, ap);
-          else if (q) EEGF_LAUNCH((gemm4q_kernel<BKC, EPI, true>), grid, dim3(NT4), 0, s, ap);
-          else EEGF_LAUNCH((gemm4p_kernel<BKC, EPI, true>), grid, dim3(NT4), 0, s, ap);
+          if (r) EEGF_LAUNCH((gemm4r_kernel<BKC, EPI, true>), grid, dim3(NT4), 0, s, a);
+          else EEGF_LAUNCH((gemm4p_kernel<BKC, EPI, true>), grid, dim3(NT4), 0, s, a);
         }
       } else if (r) {
-        EEGF_LAUNCH((gemm4r_kernel<BKC, EPI>), grid, dim3(NT4), 0, s, ap);
-      } else if (q) {
-        EEGF_LAUNCH((gemm4q_kernel<BKC, EPI>), grid, dim3(NT4), 0, s, ap);
+        EEGF_LAUNCH((gemm4r_kernel<BKC, EPI>), grid, dim3(NT4), 0, s, a);
       } else {
-        EEGF_LAUNCH((gemm4p_kernel<BKC, EPI>), grid, dim3(NT4), 0, s, ap);
+        EEGF_LAUNCH((gemm4p_kernel<BKC, EPI>), grid, dim3(NT4), 0, s, a);
       }
       return (int)hipGetLastError();
     }
   }
-  if (g_gemm8 < 0) {
-    // default schedule (tools/gemm_bench.py --ab, profiles/r1s2_gemm_ab.log): the 8-phase lockstep
-    // schedule with one vmcnt per K-tile for the input-gradient GEMMs (+10-25 %) and the forward
-    // GEMMs except the smallest (N, K <= 768); the 2-phase kernel for the weight gradients
-    const bool use8 = sizeof(TO) == 2 && AKC && (!BKC || a.N > 768 || a.K > 768);
-    // the 4-wave kernel (profiles/r1s2_gemm4w_ab.log, r1s2_gemm4w_kmajor_ab.log): +7-8 % on the
-    // weight gradients and on K >= 2048 (K-loop-bound; at K = 768 its unoverlapped epilogue loses)
-    if (sizeof(TO) == 4 ? (!AKC && !BKC) : a.K >= 2048) {
-      if (!a.colsum_part) {
-        EEGF_LAUNCH((gemm4w_kernel<AKC, BKC, EPI, TO>), dim3(tiles, splits), dim3(NT4), 0, s, a);
-        return (int)hipGetLastError();
-      }
-    }
-    if constexpr (AKC && sizeof(TO) == 2) {
-      // 256x128 two-workgroups-per-CU kernel (eegf_tune key 8: 0 off, 1 every short-K GEMM, 2 (default)
-      // N <= 768 only: the attention out-projection forward / input gradient, 940 -> 969 and
-      // 808 -> 947 TFLOP/s; wider N stays on the 8-phase kernel, profiles/r2h_gemm_ab.log)
-      const bool h_ok = g_gemm4h == 1 || (g_gemm4h == 2 && a.N <= 768);
-      if (h_ok && splits == 1 && !a.colsum_part && a.K < 2048 && a.K % BK4 == 0 && a.N >= 128) {
-        const int tiles_h = ((a.M + TM - 1) / TM) * ((a.N + TNH - 1) / TNH);
-        EEGF_LAUNCH((gemm4h_kernel<BKC, EPI>), dim3(tiles_h), dim3(NT4), 0, s, a);
-        return (int)hipGetLastError();
-      }
-    }
-    if (use8) {
-      if constexpr (AKC && !BKC && sizeof(TO) == 2) {
-        if (a.colsum_part) {
-          EEGF_LAUNCH((gemm8_kernel<AKC, BKC, EPI, TO, true>), dim3(tiles, splits), dim3(NT), 0, s, a);
-          return (int)hipGetLastError();
-        }
-      }
-      if (!a.colsum_part) {
-        EEGF_LAUNCH((gemm8_kernel<AKC, BKC, EPI, TO>), dim3(tiles, splits), dim3(NT), 0, s, a);
-        return (int)hipGetLastError();
-      }
-    }
-  } else if ((g_gemm8 == 4 || g_gemm8 == 6) && !a.colsum_part) {
-    const dim3 grid(tiles, splits);
-    if (g_gemm8 == 4) EEGF_LAUNCH((gemm8_kernel<AKC, BKC, EPI, TO>), grid, dim3(NT), 0, s, a);
-    else EEGF_LAUNCH((gemm4w_kernel<AKC, BKC, EPI, TO>), grid, dim3(NT4), 0, s, a);
-    return (int)hipGetLastError();
-  }
-  if constexpr (AKC && !BKC && sizeof(TO) == 2) {
-    if (a.colsum_part) {
-      EEGF_LAUNCH((gemm_big_kernel<AKC, BKC, EPI, TO, true>), dim3(tiles, splits), dim3(NT), 0, s, a);
-      return (int)hipGetLastError();
-    }
-  }
-  if (a.colsum_part) return EEGF_ERR_ARG;
-  EEGF_LAUNCH((gemm_big_kernel<AKC, BKC, EPI, TO>), dim3(tiles, splits), dim3(NT), 0, s, a);
+  EEGF_LAUNCH((gemm4w_kernel<AKC, BKC, EPI, TO>), dim3(tiles, splits), dim3(NT4), 0, s, a);
   return (int)hipGetLastError();
 }
 
@@ -2336,7 +1390,7 @@ int eegf_gemm_big_wgrad_bias(int M, int N, int K, const void* A, long lda, const
   float* slabs = (float*)workspace;
   float* part = slabs + (splits > 1 ? (long)splits * M * N : 0);
   BigArgs a{(const bf16*)A, (const bf16*)B, splits > 1 ? (void*)slabs : (void*)C, nullptr, nullptr, lda, ldb, ldc, 0,
-            M, N, K, 1.0f, beta, 1.0f, splits > 1 ? ks : 0, nullptr, part, g_ts_buf, group_for(N)};
+            M, N, K, 1.0f, beta, 1.0f, splits > 1 ? ks : 0, part, g_ts_buf, group_for(N)};
   const int tiles = ((M + TM - 1) / TM) * ((N + TN - 1) / TN);
   EEGF_LAUNCH((gemm4w_kernel<false, false, EPI_NONE, float, true>), dim3(tiles, splits), dim3(NT4), 0,
                      stream, a);
@@ -2358,13 +1412,12 @@ int eegf_gemm_big_wgrad_bias(int M, int N, int K, const void* A, long lda, const
 //             in `workspace` reduced in a fixed order (bitwise reproducible), beta applied once.
 int eegf_gemm_big(int a_kc, int b_kc, int epi, int out_f32, int M, int N, int K, const void* A, long lda,
                   const void* B, long ldb, void* C, long ldc, const float* bias, void* aux, long ldaux, float alpha,
-                  float beta, float epi_scale, void* workspace, long ws_bytes, float* a_colsum, hipStream_t stream) {
+                  float beta, float epi_scale, void* workspace, long ws_bytes, hipStream_t stream) {
   if (K % BK != 0 || M % 8 != 0 || N % 8 != 0) return 1;
   if (lda % 8 || ldb % 8 || ldc % 8 || (aux && ldaux % 8)) return 1;
   if ((((uintptr_t)A | (uintptr_t)B | (uintptr_t)C | (uintptr_t)aux) & 15) != 0) return 1;
   BigArgs a{(const bf16*)A, (const bf16*)B, C, bias, (bf16*)aux, lda, ldb, ldc, ldaux, M, N, K, alpha, beta,
-            epi_scale, 0, a_colsum, nullptr, g_ts_buf, group_for(N)};
-  if (a_colsum && (!a_kc || out_f32)) return 1;
+            epi_scale, 0, nullptr, g_ts_buf, group_for(N)};
   if (out_f32) {
     if (a_kc || b_kc || epi != EPI_NONE || M < 256 || N < 256 || K < 4096 || ldc % 4) return 1;
     int splits = wgrad_splits(M, N, K, ws_bytes, 0);
@@ -2381,7 +1434,6 @@ int eegf_gemm_big(int a_kc, int b_kc, int epi, int out_f32, int M, int N, int K,
     return (int)hipGetLastError();
   }
   if (!a_kc || M < 2048 || N < 256) return 1;
-  if (a_colsum && K > CS_KMAX) return 1;
   if (b_kc) {
     switch (epi) {
       case EPI_NONE: return launch_big<true, true, EPI_NONE, bf16>(a, 1, stream);
@@ -2403,48 +1455,34 @@ int eegf_gemm_big(int a_kc, int b_kc, int epi, int out_f32, int M, int N, int K,
   return 1;
 }
 
-// Row-tile count of the fused A column sums (rows of the a_colsum partial buffer) when eegf_gemm
-// would take the 256x256 path for this shape with a K-contiguous A and bf16 output, else 0.
-int eegf_gemm_big_colsum_tiles(int M, int N, int K) {
-  if (K % BK != 0 || M % 8 != 0 || N % 8 != 0 || M < 2048 || N < 256 || K > CS_KMAX) return 0;
-  return (M + TM - 1) / TM;
-}
-
 extern int g_attn256_mode;     // attention.hip
 extern int g_ln_fwd768;        // layernorm.hip
 
 // Tuning / A-B hook (returns the old value; test and benchmark state, include/eegfusion.h lists the
-// keys): 1 = 256x256 GEMM kernel (-1 automatic routing (default), 0 2-phase, 4 8-phase, 6 4-wave);
-// 2 = L = 256 attention kernels (bit 0 forward, bit 1 backward); 6 / 7 = LayerNorm rows; 8 = the
-// 256x128 two-workgroups-per-CU GEMM.
-// Diagnostics: every following big-GEMM launch writes 4 phase timestamps + the CU id per workgroup
-// into buf (int64 [grid.y][grid.x][8], s_memrealtime 100 MHz ticks) until called again with nullptr.
+// keys): 2 = L = 256 attention kernels (bit 0 forward, bit 1 backward); 6 / 7 = LayerNorm rows; 10 = the
+// 768-wide LayerNorm forward; 11 = persistent GEMMs on / off; 13 = CUs left free by the persistent grids;
+// 14 = gemm4r / gemm4p; 19 = the MFMA cross-attention kernels.
+#if EEGF_DIAG
+// Diagnostics builds only (-DEEGF_DIAG=1): every following gemm4w launch writes 4 phase timestamps + the
+// CU id per workgroup into buf (int64 [grid.y][grid.x][8], s_memrealtime 100 MHz ticks) until called
+// again with nullptr.  tools/gemm_phases.py.
 extern "C" int eegf_gemm_big_timestamps(long long* buf) {
   g_ts_buf = buf;
   return 0;
 }
+#else
+extern "C" int eegf_gemm_big_timestamps(long long* buf) { return buf ? EEGF_ERR_ARG : 0; }
+#endif
 
 extern int g_xbwd_mfma;   // decoder.hip
 extern "C" int eegf_tune(int key, int value) {
   if (key == 19) { const int o = g_xbwd_mfma; if (value < 0 || value > 1) return EEGF_ERR_ARG; g_xbwd_mfma = value; return o; }
-  if (key == 1) {
-    if (value != -1 && value != 0 && value != 4 && value != 6) return EEGF_ERR_ARG;
-    const int o = g_gemm8;
-    g_gemm8 = value;
-    return o;
-  }
-  if (key == 2) { const int o = g_attn256_mode; g_attn256_mode = value; return o; }
-  if (key == 8) { const int o = g_gemm4h; g_gemm4h = value; return o; }
-  if (key == 9) { const int o = g_group_m; g_group_m = value; return o; }
+  if (key == 2) { const int o = g_attn256_mode; if (value < 0 || value > 3) return EEGF_ERR_ARG; g_attn256_mode = value; return o; }
   if (key == 7) { const int o = g_ln_bwd_rpb; if (value < 4 || value > 1024 || value % 4) return EEGF_ERR_ARG; g_ln_bwd_rpb = value; return o; }
-  if (key == 10) { const int o = g_ln_fwd768; g_ln_fwd768 = value; return o; }
-  if (key == 12) { const int o = g_store_nt; if (value < 0 || value > 1) return EEGF_ERR_ARG; g_store_nt = value; return o; }
-  if (key == 11) { const int o = g_gemm4p; if (value < 0 || value > 3) return EEGF_ERR_ARG; g_gemm4p = value; return o; }
-  if (key == 14) { const int o = g_gemm4q; if (value < 0 || value > 2) return EEGF_ERR_ARG; g_gemm4q = value; return o; }
+  if (key == 10) { const int o = g_ln_fwd768; if (value < 0 || value > 1) return EEGF_ERR_ARG; g_ln_fwd768 = value; return o; }
+  if (key == 11) { const int o = g_persistent; if (value < 0 || value > 1) return EEGF_ERR_ARG; g_persistent = value; return o; }
+  if (key == 14) { const int o = g_gemm4r; if (value < 0 || value > 1) return EEGF_ERR_ARG; g_gemm4r = value; return o; }
   if (key == 13) { const int o = g_cu_reserve; if (value < 0 || value >= cu_count()) return EEGF_ERR_ARG; g_cu_reserve = value; return o; }
-  if (key == 15) { const int o = g_tile_order; if (value < 0 || value > 63 || (value & 3) == 3) return EEGF_ERR_ARG; g_tile_order = value; return o; }
-  if (key == 18) { const int o = g_gemm4r; if (value < 0 || value > 1) return EEGF_ERR_ARG; g_gemm4r = value; return o; }
-  if (key == 16) { const int o = g_probe_delay; g_probe_delay = value; return o; }
   if (key == 6) { const int o = g_ln_rpw; if (value < 1 || value > 64) return EEGF_ERR_ARG; g_ln_rpw = value; return o; }
   return EEGF_ERR_ARG;
 }

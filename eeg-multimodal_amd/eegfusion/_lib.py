@@ -27,7 +27,6 @@ SIGNATURES: dict[str, list] = {
     "eegf_gemm": [i32, i32, i32, i32, i32, i32, i32, i32, i32,
                   vp, i64, i64, vp, i64, i64, vp, i64, i64,
                   vp, i64, vp, i64, i64, f32, f32, f32, vp, i64, vp],
-    "eegf_gemm_colsum_tiles": [i32, i32, i32, i32, i32, i32],
     "eegf_seq_lengths": [i32, i32, vp, vp, vp, vp],
     "eegf_varlen_embed": [i32, i32, i32, i32, vp, i64, i64, vp, vp, vp, vp, vp, vp],
     "eegf_varlen_rows": [i32, i32, i32, i32, vp, i64, i64, vp, i64, vp, i64, i32, vp],
@@ -40,8 +39,6 @@ SIGNATURES: dict[str, list] = {
     "eegf_seq_mean": [i32, i32, i32, i32, vp, i64, vp, i64, vp],
     "eegf_seq_mean_bwd": [i32, i32, i32, i32, vp, i64, vp, i64, f32, vp],
     "eegf_gemm_wgrad_bias": [i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, f32, vp, vp, i64, vp],
-    "eegf_gemm_acs": [i32, i32, i32, i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, vp, vp, i64, f32, f32, f32,
-                      vp, vp],
     "eegf_tune": [i32, i32],
     "eegf_gemm_big_timestamps": [vp],
     "eegf_ring_proxy": [i64, i32, i32, vp, vp],

@@ -214,9 +214,8 @@ class FusionEngine:
 
     def dgrad(self, dy, w, out, M, ldd=None, ldo=None, epi=_lib.EPI_NONE, aux=None, scale=1.0, beta=0.0,
               bias_grad=None, tag=None):
-        """out = dy W (* act'(aux)) (+ beta out).  bias_grad: fp32 tensor that receives += dy.sum(0) —
-        fused into the GEMM (per-256-row-tile column sums of dy, eegf_gemm_acs) when the shape takes
-        the 256x256 path, else a separate column reduction."""
+        """out = dy W (* act'(aux)) (+ beta out).  bias_grad: fp32 tensor that receives += dy.sum(0)
+        (a column reduction of dy)."""
         N, K = w.shape
         ldaux = aux.shape[-1] if aux is not None else 0
         if bias_grad is not None and self.psn is not None:
@@ -224,15 +223,6 @@ class FusionEngine:
             self._psn_bias(dy, M, N, ldd or N)
             bias_grad = None
         if bias_grad is not None:
-            tiles = _lib.lib().eegf_gemm_colsum_tiles(_code(dy), _code(out), 1, M, K, N)
-            if tiles > 0 and (ldd or N) == N:
-                part = self._part("acs", tiles * N)
-                ev = self._ev_start(tag)
-                call("eegf_gemm_acs", _code(dy), _code(out), 1, 0, epi, M, K, N, P(dy), N, P(w), K, P(out), ldo or K,
-                     None, P(aux), ldaux, 1.0, float(beta), float(scale), P(part), _stream())
-                self._ev_end(tag, ev, 2.0 * M * N * K)
-                self.colsum(part, N, tiles, N, bias_grad)
-                return out
             self.colsum(dy, ldd or N, M, N, bias_grad)
         ev = self._ev_start(tag)
         self.gemm(dy, w, out, M, K, N, 1, 0, ldd or N, K, ldo or K, epi=epi, aux=aux, ldaux=ldaux, scale=scale,

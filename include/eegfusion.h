@@ -9,10 +9,11 @@
  *   - all pointers are caller-owned device pointers (row-major, contiguous unless a leading
  *     dimension / stride argument says otherwise); sizes are in elements;
  *   - no allocation, no host synchronisation, no global state: a caller may capture any sequence
- *     of calls into a hipGraph.  Two diagnostics are the exception, declared as such below and used
+ *     of calls into a hipGraph.  The diagnostics are the exception, declared as such below and used
  *     by tests / benchmarks only: eegf_tune (process-global kernel-routing keys, A/B switches with
  *     production defaults; set them before launching, not concurrently with launches on other
- *     threads) and eegf_gemm_big_timestamps (a process-global stamp buffer, off by default);
+ *     threads), the launch counters (eegf_launch_log_*, host-side) and eegf_gemm_big_timestamps
+ *     (diagnostics builds only);
  *   - work is enqueued on `stream`;
  *   - returns 0 on success, EEGF_ERR_ARG (<0) on an argument error (nothing launched), or the
  *     hipError_t of the launch; never throws.
@@ -61,52 +62,29 @@ int eegf_gemm(int dtype, int out_dtype, int a_kcontig, int b_kcontig, int epi,
               const float* bias, long strideBias, void* aux, long ldaux, long strideAux,
               float alpha, float beta, float epi_scale, void* workspace, long ws_bytes,
               hipStream_t stream);
-/* Tuning / A-B hook (benchmarks, parity tests; not part of the reference interface).  Returns the
- * previous value, or EEGF_ERR_ARG.
- *   key 1: 256x256 GEMM kernel: -1 = automatic routing (default), 0 = 2-phase 8-wave, 4 = 8-phase
- *          8-wave (the schedule the router uses for short K), 6 = the 4-wave 128x128-per-wave kernel;
- *   key 2: L = 256 attention kernels (bit 0 persistent forward, bit 1 persistent backward; default 3);
- *   key 6: maximum rows per wave of eegf_ln_fwd (1..64, default 16; fewer when the grid would drop
- *          below 1024 workgroups);
- *   key 7: rows per workgroup of eegf_ln_bwd when rows >= 65536 (multiple of 4, default 64);
- *   key 8: 256x128 two-workgroups-per-CU GEMM for K < 2048 bf16 outputs: 0 off, 1 every such GEMM,
- *          2 (default) N <= 768 only;
- *   key 9: tile raster of the 256-row GEMMs: -1 (default) groups of 4 row panels when N >= 2048,
- *          row-major otherwise; 0 row-major; G > 0 groups of G row panels walked column by column;
- *   key 10: bf16 768-wide rows of eegf_ln_fwd on the 16-B-access kernel (1, default) or the generic
- *          4-columns-per-lane kernel (0);
- *   key 11: the persistent 256x256 bf16 GEMM (one workgroup per CU over the tiles, the next tile's
- *          operands staged by the current tile's K-loop tail, epilogue stores draining under the next
- *          tile's first K-tiles) for full-tile bf16-output GEMMs with a K-contiguous A and epilogue
- *          NONE (any beta) / BIAS / BIAS_GELU / BIAS_GELU_D / MUL_AUX (k-major B): 0 off, 1 (default)
- *          every such GEMM, 2 the GELU / GELU' forward GEMMs and the input gradients with K >= 2048,
- *          3 = 2 + the MUL_AUX input gradients;
- *   key 12: persistent-GEMM epilogue stores with the non-temporal hint: 0 (default) off, 1 on (the
- *          store-bound GEMMs run 3-4 % faster alone but the step 0.8 % slower, profiles/r4b_*).
+/* Tuning / A-B hook (tests and benchmarks; not part of the reference interface).  Returns the previous
+ * value, or EEGF_ERR_ARG for an unknown key or an out-of-range value.  Every key selects between
+ * kernels that compute the same results (bitwise, or up to summation order where stated); the defaults
+ * are the production routes.
+ *   key 2:  L = 256 attention kernels: bit 0 the persistent forward, bit 1 the persistent backward
+ *           (default 3; 0 = the generic flash kernels, up to summation order);
+ *   key 6:  maximum rows per wave of eegf_ln_fwd (1..64, default 16);
+ *   key 7:  rows per workgroup of eegf_ln_bwd when rows >= 65536 (multiple of 4, default 64);
+ *   key 10: bf16 768-wide rows of eegf_ln_fwd on the 16-B-access kernel (1, default) or the generic one (0);
+ *   key 11: the persistent 256x256 GEMMs for the full-tile bf16-output GEMMs they take: 1 (default), 0 the
+ *           non-persistent 4-wave kernel (bitwise the same results: tests/test_gemm_gpu.py);
+ *   key 13: CUs left free by the persistent grids (0 = default): room for RCCL's kernels during the
+ *           backward (tools/overlap_proxy.py prices it);
+ *   key 14: the persistent GEMMs with K % 64 == 0 on gemm4r (whole-line K-tile pairs, rolling A
+ *           fragments; 1, default) or gemm4p (64-B half lines; 0): bitwise the same results;
+ *   key 19: eegf_xattn_fwd / _bwd with a bf16 memory: the context and backward on the fp32 MFMA (1, default)
+ *           or the VALU kernels (0); fp32 products and sums either way, equal up to summation order.
  * Process-global (see the contract above): test / benchmark state, not for production callers. */
 int eegf_tune(int key, int value);
-/*   key 13: CUs left free by the persistent kernels (the 256x256 GEMM and the L = 256 attention grids
- *          launch cu_count - value workgroups; 0 = default): room for RCCL's kernels during the
- *          backward when world > 1 (tools/overlap_proxy.py prices it).
- *   key 14: the persistent GEMMs with K % 64 == 0, K >= 128 on gemm4q (K-tile pairs staged in whole
- *          128-B lines, five 32-KB operand slots): 2 (default) every such GEMM, 1 the forward layout
- *          (both operands K-contiguous) only, 0 none (gemm4p); bit-identical results
- *          (tests/test_gemm_gpu.py), env EEGF_GEMM4Q.
- *   key 15: gemm4q's persistent tile walk: 0 (default) round-major (each round an XCD takes the next
- *          32 tiles of the whole grid), 1 XCD-blocked (each XCD walks its own contiguous eighth of the
- *          grouped raster), 2 a timing probe with L2-resident operands (wrong results); probe bits
- *          (timing only, wrong results): + 4 no epilogue stores, + 8 no staging after the prologue,
- *          + 16 stores from even workgroups only, + 32 odd workgroups start key-16 ticks (100 MHz)
- *          late; env EEGF_TILE_ORDER.
- *   key 16: the start delay of the key-15 + 32 probe.
- *   key 18: the gemm4q-eligible GEMMs on gemm4r (rolling A fragments, A / B images in 3 + 2 ring slots,
- *          bitwise the same results): 1 (default) on, 0 gemm4q; env EEGF_GEMM4R.
- *   key 19: eegf_xattn_fwd / eegf_xattn_bwd with a bf16 memory: 1 (default) the context and the backward
- *          on the fp32 MFMA (xctx_mfma / xbwd_mfma), 0 the VALU kernels; fp32 products and sums either
- *          way, results equal up to summation order (tests/test_kernels_gpu.py). */
-/* Diagnostics (no reference counterpart): every following 256-row GEMM launch of the 8-wave / 4-wave
- * kernels writes 4 s_memrealtime stamps per workgroup (start, prologue done, K-loop done, epilogue
- * issued, slot 4 the CU id) into buf = int64 [grid.y][grid.x][8]; nullptr switches it off.  tools/gemm_phases.py. */
+/* Diagnostics (no reference counterpart), libraries built with -DEEGF_DIAG=1 only (elsewhere a non-null
+ * buf returns EEGF_ERR_ARG): every following gemm4w launch writes 4 s_memrealtime stamps per workgroup
+ * (start, prologue done, K-loop done, epilogue issued, slot 4 the CU id) into buf = int64
+ * [grid.y][grid.x][8]; nullptr switches it off.  tools/gemm_phases.py. */
 int eegf_gemm_big_timestamps(long long* buf);
 /* Diagnostics (no reference counterpart): a stand-in for the CU use of an RCCL all-reduce kernel, for
  * the one-GPU overlap proxy of the gradient all-reduces (tools/overlap_proxy.py): `wgs`
@@ -120,13 +98,6 @@ int eegf_ring_proxy(long n, int passes, int wgs, float* x, hipStream_t stream);
  * (tests/test_production_gpu.py). */
 int eegf_launch_log_reset(void);
 long eegf_launch_log_read(char* buf, long cap);
-/* Rows of the a_colsum partial buffer eegf_gemm_acs writes for this shape (ceil(M/256)), or 0 when
- * the fused column sums are unavailable (needs bf16 in/out, K-contiguous A, M >= 2048, N >= 256,
- * K % 64 == 0, 8-aligned dims). */
-int eegf_gemm_colsum_tiles(int dtype, int out_dtype, int a_kcontig, int M, int N, int K);
-/* eegf_gemm (batch 1, no split-K) that also writes the column sums of A over each 256-row tile:
- * a_colsum [ceil(M/256)][K] fp32.  For an input-gradient GEMM (A = dY) these are the partial bias
- * gradients (nn.Linear bias.grad = dY.sum(0)), reduced with eegf_colsum over ceil(M/256) rows. */
 /* Weight gradient of an nn.Linear with its bias gradient fused (autograd of F.linear, the weight and
  * bias grads of every BERT projection, modeling_bert.py:139-351): dW [M][N] = dY^T X + beta dW over
  * K tokens, db [M] += dY.sum(0).  dY [K][M] (row stride ldd) and X [K][N] (ldx) bf16; dW, db fp32.
@@ -140,11 +111,6 @@ int eegf_gemm_colsum_tiles(int dtype, int out_dtype, int a_kcontig, int M, int N
 int eegf_gemm_wgrad_bias(int dtype, int M, int N, int K, const void* dY, long ldd, const void* X, long ldx,
                          float* dW, long ldw, float beta, float* db, void* workspace, long ws_bytes,
                          hipStream_t stream);
-int eegf_gemm_acs(int dtype, int out_dtype, int a_kcontig, int b_kcontig, int epi, int M, int N, int K,
-                  const void* A, long lda, const void* B, long ldb, void* C, long ldc, const float* bias,
-                  void* aux, long ldaux, float alpha, float beta, float epi_scale, float* a_colsum,
-                  hipStream_t stream);
-
 /* ---- contract T pad skipping (varlen BERT).  The reference runs BERT over the
  * padded 512 tokens (get_embedding.py:115) with the padded keys masked (model.py:37-43); the packed
  * rows of the real tokens give the same outputs.  cu_seqlens [B+1] int32 (device): sequence b owns

@@ -41,23 +41,21 @@ def test_argument_errors_return_status_without_gpu():
 
 def test_tune_routing_keys_validate_and_restore_without_gpu():
     """eegf_tune is host state only: the GEMM routing keys report the production defaults (key 11 = 1
-    persistent GEMM, key 14 = 2 gemm4q for every eligible shape, key 19 = 1 the MFMA cross-attention
-    backward), refuse out-of-range values with
-    EEGF_ERR_ARG and return the previous value when set."""
-    import os
-
+    persistent GEMMs, key 14 = 1 gemm4r, key 19 = 1 the MFMA cross-attention backward), refuse
+    out-of-range values and retired keys (1, 8, 12, 15, 16, 18) with EEGF_ERR_ARG, and return the previous
+    value when set."""
     from eegfusion import _lib
     lib = _lib.lib()
     lib.eegf_tune.argtypes = [_lib.i32, _lib.i32]
-    for key, default, hi in ((11, 1, 3), (14, 2, 2), (19, 1, 1)):
-        env = {11: "EEGF_GEMM4P", 14: "EEGF_GEMM4Q"}.get(key, "")
+    for key, default, hi in ((11, 1, 1), (14, 1, 1), (19, 1, 1)):
         old = lib.eegf_tune(key, default)
-        if not env or env not in os.environ:
-            assert old == default, (key, old)
+        assert old == default, (key, old)
         assert lib.eegf_tune(key, hi + 1) == _lib.ERR_ARG
         assert lib.eegf_tune(key, -1) == _lib.ERR_ARG
         assert lib.eegf_tune(key, 0) == default
         assert lib.eegf_tune(key, old) == 0
+    for key in (1, 8, 9, 12, 15, 16, 18):
+        assert lib.eegf_tune(key, 0) == _lib.ERR_ARG, key
 
 
 def test_launch_log_reads_empty_without_gpu():

@@ -290,36 +290,6 @@ def test_gemm_big_dgrad_beta(M, N, K):
     _check(c, ref, torch.bfloat16)
 
 
-@pytest.mark.parametrize("epi", ["none", "dgelu"])
-@pytest.mark.parametrize("M,N,K,beta", [(4352, 808, 768, 0.0), (2056, 768, 3072, 1.0), (4096, 768, 2304, 1.0),
-                                        (16648, 808, 2304, 0.0), (4104, 3072, 3072, 1.0)])
-def test_gemm_acs_fused_bias_grad(epi, M, N, K, beta):
-    if epi == "dgelu":
-        beta = 0.0          # activation-derivative epilogues read aux in place of C (beta must be 0)
-    """eegf_gemm_acs: the input-gradient GEMM plus per-256-row-tile column sums of dY (the fused
-    bias gradient); ragged M (tiles past M excluded), beta accumulate, epilogue."""
-    from eegfusion import _lib
-    torch.manual_seed(13)
-    dy = torch.randn(M, K, device="cuda").to(torch.bfloat16)          # [M, N_out=K]
-    w = (torch.randn(K, N, device="cuda") * 0.1).to(torch.bfloat16)   # [N_out, N_in]
-    c = torch.randn(M, N, device="cuda").to(torch.bfloat16)
-    aux = torch.randn(M, N, device="cuda").to(torch.bfloat16) if epi == "dgelu" else None
-    c0 = c.double().clone()
-    tiles = _lib.lib().eegf_gemm_colsum_tiles(1, 1, 1, M, N, K)
-    assert tiles == (M + 255) // 256
-    part = torch.full((tiles, K), float("nan"), device="cuda")
-    _lib.call("eegf_gemm_acs", 1, 1, 1, 0, _lib.EPI_DGELU if epi == "dgelu" else _lib.EPI_NONE, M, N, K,
-              dy.data_ptr(), K, w.data_ptr(), N, c.data_ptr(), N, None,
-              aux.data_ptr() if aux is not None else None, N if aux is not None else 0, 1.0, beta, 1.0,
-              part.data_ptr(), torch.cuda.current_stream().cuda_stream)
-    torch.cuda.synchronize()
-    ref, _ = _ref_epi(dy.double() @ w.double(), epi, None, aux, 1.0)
-    _check(c, ref + beta * c0, torch.bfloat16)
-    pref = torch.nn.functional.pad(dy.double(), (0, 0, 0, tiles * 256 - M)).view(tiles, 256, K).sum(1)
-    assert ((part.double() - pref).abs().max() / pref.abs().max()).item() < 1e-5
-    assert _lib.lib().eegf_gemm_colsum_tiles(0, 0, 1, M, N, K) == 0      # fp32: not fused
-
-
 def _tune(key, value):
     from eegfusion import _lib
     lib = _lib.lib()
@@ -334,8 +304,8 @@ ROUTE_SHAPES = [(16384, 3072, 768), (16640, 808, 320), (16384, 1024, 128), (8192
 @pytest.mark.parametrize("epi", ["bias", "bias_gelu", "bias_gelu_d", "gelu_noaux", "none_beta"])
 @pytest.mark.parametrize("M,N,K", ROUTE_SHAPES)
 def test_gemm_big_routed_fwd(epi, M, N, K):
-    """Forward GEMMs with every bf16 epilogue through the default routing (8-phase 256x256 kernel for
-    wide N, 256x128 two-workgroup kernel for N <= 768) against a float64 reference."""
+    """Forward GEMMs with every bf16 epilogue through the default routing (the persistent kernels on full
+    tiles, the 4-wave gemm4w on ragged ones) against a float64 reference."""
     k = _k()
     torch.manual_seed(21)
     x = (torch.randn(M, K, device="cuda") * 0.3).to(torch.bfloat16)
@@ -360,38 +330,35 @@ def test_gemm_big_routed_fwd(epi, M, N, K):
 
 @pytest.mark.parametrize("epi", ["none", "mul_aux", "dgelu"])
 @pytest.mark.parametrize("M,N,K", ROUTE_SHAPES)
-def test_gemm_big_routed_dgrad_colsum(epi, M, N, K):
-    """Input-gradient GEMM with fused dY column sums (per-tile sums of the column-0 tiles, 8-phase
-    kernel) and without the sums (default routing), same result bit for bit."""
-    from eegfusion import _lib
+def test_gemm_big_routed_dgrad(epi, M, N, K):
+    """Input-gradient GEMMs through the default routing against a float64 reference, and bit for bit
+    against the non-persistent gemm4w (eegf_tune key 11 = 0: the same MFMA K order and epilogue math)."""
+    k = _k()
     torch.manual_seed(22)
     dy = torch.randn(M, K, device="cuda").to(torch.bfloat16)
     w = (torch.randn(K, N, device="cuda") * 0.1).to(torch.bfloat16)
-    c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
     aux = torch.randn(M, N, device="cuda").to(torch.bfloat16) if epi != "none" else None
-    code = {"none": _lib.EPI_NONE, "mul_aux": _lib.EPI_MUL_AUX, "dgelu": _lib.EPI_DGELU}[epi]
-    tiles = (M + 255) // 256
-    part = torch.full((tiles, K), float("nan"), device="cuda")
-    _lib.call("eegf_gemm_acs", 1, 1, 1, 0, code, M, N, K, dy.data_ptr(), K, w.data_ptr(), N, c.data_ptr(), N,
-              None, aux.data_ptr() if aux is not None else None, N if aux is not None else 0, 1.0, 0.0, 1.0,
-              part.data_ptr(), torch.cuda.current_stream().cuda_stream)
-    torch.cuda.synchronize()
+    outs = []
+    for key in (1, 0):
+        old = _tune(11, key)
+        try:
+            outs.append(k.linear_dgrad(dy, w, epi=epi, aux=aux))
+            torch.cuda.synchronize()
+        finally:
+            _tune(11, old)
     ref, _ = _ref_epi(dy.double() @ w.double(), epi, None, aux, 1.0)
-    _check(c, ref, torch.bfloat16)
-    pref = torch.nn.functional.pad(dy.double(), (0, 0, 0, tiles * 256 - M)).view(tiles, 256, K).sum(1)
-    assert ((part.double() - pref).abs().max() / pref.abs().max()).item() < 1e-5
-    k_out = _k().linear_dgrad(dy, w, epi=epi, aux=aux)
-    torch.cuda.synchronize()
-    assert torch.equal(k_out, c)
+    _check(outs[0], ref, torch.bfloat16)
+    if K >= 256:
+        assert torch.equal(outs[0], outs[1])
 
 
 @pytest.mark.parametrize("epi", ["none", "bias", "bias_gelu", "bias_gelu_d", "gelu_noaux", "none_beta"])
 @pytest.mark.parametrize("M,N,K", [(4352, 808, 768), (2048, 2304, 96), (8192, 3072, 32), (16384, 768, 3072)])
 def test_gemm_big_4wave_fwd(epi, M, N, K):
-    """The 4-wave 256x256 kernel (128x128 per wave, AGPR accumulators, BK = 32 ring) on the forward
-    layout, selected with eegf_tune(1, 6): edge tiles, K = one K-tile, odd K-tile counts."""
+    """The 4-wave 256x256 kernel gemm4w (128x128 per wave, AGPR accumulators, BK = 32 ring) on the forward
+    layout, every shape on it with eegf_tune(11, 0): edge tiles, K = one K-tile, odd K-tile counts."""
     k = _k()
-    old = _tune(1, 6)
+    old = _tune(11, 0)
     try:
         torch.manual_seed(23)
         x = (torch.randn(M, K, device="cuda") * 0.3).to(torch.bfloat16)
@@ -414,15 +381,15 @@ def test_gemm_big_4wave_fwd(epi, M, N, K):
         if aux is not None:
             _check(aux, pre, torch.bfloat16)
     finally:
-        _tune(1, old)
+        _tune(11, old)
 
 
 @pytest.mark.parametrize("epi", ["none", "mul_aux", "dgelu"])
 @pytest.mark.parametrize("M,N,K", [(4352, 808, 768), (2048, 3072, 96), (8192, 768, 2304)])
 def test_gemm_big_4wave_dgrad(epi, M, N, K):
-    """4-wave kernel with a k-major B (input gradient, ds_read_b64_tr_b16 fragments)."""
+    """gemm4w with a k-major B (input gradient, ds_read_b64_tr_b16 fragments)."""
     k = _k()
-    old = _tune(1, 6)
+    old = _tune(11, 0)
     try:
         torch.manual_seed(24)
         dy = torch.randn(M, K, device="cuda").to(torch.bfloat16)
@@ -433,27 +400,23 @@ def test_gemm_big_4wave_dgrad(epi, M, N, K):
         ref, _ = _ref_epi(dy.double() @ w.double(), epi, None, aux, 1.0)
         _check(out, ref, torch.bfloat16)
     finally:
-        _tune(1, old)
+        _tune(11, old)
 
 
 @pytest.mark.parametrize("M,N,K", [(2304, 768, 65536), (768, 3072, 16384), (808, 264, 8192)])
 def test_gemm_big_4wave_wgrad(M, N, K):
-    """4-wave kernel with k-major A and B (weight gradient), fp32 split-K slabs, beta accumulate."""
+    """gemm4w with k-major A and B (weight gradient), fp32 split-K slabs, beta accumulate, ragged M / N."""
     k = _k()
-    old = _tune(1, 6)
-    try:
-        torch.manual_seed(25)
-        dy = torch.randn(K, M, device="cuda").to(torch.bfloat16)
-        x = torch.randn(K, N, device="cuda").to(torch.bfloat16)
-        dw = torch.randn(M, N, device="cuda")
-        ref = dw.double() + dy.double().t() @ x.double()
-        ws = torch.empty(24 << 20, device="cuda")
-        k.gemm(dy, x, dw, M=M, N=N, K=K, a_kc=0, b_kc=0, lda=M, ldb=N, ldc=N, beta=1.0, workspace=ws)
-        torch.cuda.synchronize()
-        err = ((dw.double() - ref).abs().max() / ref.abs().max()).item()
-        assert err <= 2e-3, err
-    finally:
-        _tune(1, old)
+    torch.manual_seed(25)
+    dy = torch.randn(K, M, device="cuda").to(torch.bfloat16)
+    x = torch.randn(K, N, device="cuda").to(torch.bfloat16)
+    dw = torch.randn(M, N, device="cuda")
+    ref = dw.double() + dy.double().t() @ x.double()
+    ws = torch.empty(24 << 20, device="cuda")
+    k.gemm(dy, x, dw, M=M, N=N, K=K, a_kc=0, b_kc=0, lda=M, ldb=N, ldc=N, beta=1.0, workspace=ws)
+    torch.cuda.synchronize()
+    err = ((dw.double() - ref).abs().max() / ref.abs().max()).item()
+    assert err <= 2e-3, err
 
 
 @pytest.mark.parametrize("M,N,K,ws_mb", [(2304, 768, 65536, 96), (3072, 768, 65536, 96), (768, 3072, 65536, 96),
@@ -504,68 +467,13 @@ def test_gemm_wgrad_bias_ineligible():
     assert st == _lib.ERR_ARG
 
 
-@pytest.mark.parametrize("epi", ["none", "bias", "bias_gelu", "bias_gelu_d", "gelu_noaux", "bias_relu", "bias_tanh",
-                                 "none_beta"])
-@pytest.mark.parametrize("M,N,K", [(4352, 808, 768), (2048, 2304, 96), (8192, 3072, 32), (65536, 3072, 768)])
-def test_gemm_4h_fwd(epi, M, N, K):
-    """The 256x128 two-workgroups-per-CU kernel (eegf_tune key 8) on the forward layout: N / M edge
-    tiles, K = one K-tile, the bench's FFN1 shape with every epilogue."""
-    k = _k()
-    old = _tune(8, 1)
-    try:
-        torch.manual_seed(31)
-        x = (torch.randn(M, K, device="cuda") * 0.3).to(torch.bfloat16)
-        w = (torch.randn(N, K, device="cuda") * 0.3).to(torch.bfloat16)
-        b = torch.randn(N, device="cuda")
-        if epi in ("none", "none_beta"):
-            c = torch.randn(M, N, device="cuda").to(torch.bfloat16)
-            beta = 1.0 if epi == "none_beta" else 0.0
-            ref = beta * c.double() + 0.5 * (x.double() @ w.double().t())
-            k.gemm(x, w, c, M=M, N=N, K=K, a_kc=1, b_kc=1, lda=K, ldb=K, ldc=N, alpha=0.5, beta=beta)
-            torch.cuda.synchronize()
-            _check(c, ref, torch.bfloat16)
-            return
-        e = "bias_gelu" if epi == "gelu_noaux" else epi
-        aux = torch.empty(M, N, device="cuda", dtype=torch.bfloat16) if epi in ("bias_gelu", "bias_gelu_d") else None
-        out = k.linear(x, w, b, epi=e, aux=aux)
-        torch.cuda.synchronize()
-        ref, pre = _ref_epi(x.double() @ w.double().t(), e, b, None, 1.0)
-        _check(out, ref, torch.bfloat16)
-        if aux is not None:
-            _check(aux, pre, torch.bfloat16)
-    finally:
-        _tune(8, old)
-
-
-@pytest.mark.parametrize("epi", ["none", "mul_aux", "dgelu", "drelu", "dtanh"])
-@pytest.mark.parametrize("M,N,K", [(4352, 808, 768), (2048, 3072, 96), (65536, 3072, 768), (65536, 768, 768)])
-def test_gemm_4h_dgrad(epi, M, N, K):
-    """256x128 kernel with a k-major B (input gradient, transpose-read fragments of a 128-column image)."""
-    k = _k()
-    old = _tune(8, 1)
-    try:
-        torch.manual_seed(32)
-        dy = torch.randn(M, K, device="cuda").to(torch.bfloat16)
-        w = (torch.randn(K, N, device="cuda") * 0.1).to(torch.bfloat16)
-        aux = torch.randn(M, N, device="cuda").to(torch.bfloat16) if epi != "none" else None
-        if epi == "dtanh":
-            aux = torch.tanh(aux.float()).to(torch.bfloat16)
-        out = k.linear_dgrad(dy, w, epi=epi, aux=aux, epi_scale=1.25)
-        torch.cuda.synchronize()
-        ref, _ = _ref_epi(dy.double() @ w.double(), epi, None, aux, 1.25)
-        _check(out, ref, torch.bfloat16)
-    finally:
-        _tune(8, old)
-
-
-
 # the persistent kernel (eegf_tune key 11): full tiles only; production-sized grids loop several rounds,
 # K below the ring depth (3 and 1 K-tiles) prefetches fewer K-tiles, a 24-tile grid runs one round
 # nk = K / 32 K-tiles: 24, 24, 3, 1, 96, and the ring-edge cases 5..7 (a full 5-slot ring, no cross-tile
 # staging) and 8 (the first cross-staged shape: the next tile's K-tiles 0..4 landed before it starts),
 # each with three rounds per CU on a 256-CU grid (768 tiles)
-# K = 128 / 320: gemm4q with 2 / 5 K-tile pairs per tile (its five operand slots advance 2 np mod 5 per
-# tile: 4 and 0), several tiles per CU
+# K = 128 / 320: gemm4r with 2 / 5 K-tile pairs per tile (its 3 + 2 operand slots advance np mod 3 /
+# mod 2 per tile), several tiles per CU
 P_SHAPES = [(65536, 2304, 768), (4096, 768, 768), (8192, 3072, 96), (2048, 1024, 32), (16384, 768, 3072),
             (16384, 3072, 160), (16384, 3072, 192), (16384, 3072, 224), (16384, 3072, 256), (16384, 3072, 128),
             (16384, 3072, 320)]
@@ -574,9 +482,9 @@ P_SHAPES = [(65536, 2304, 768), (4096, 768, 768), (8192, 3072, 96), (2048, 1024,
 @pytest.mark.parametrize("epi", ["bias", "bias_gelu", "bias_gelu_d", "gelu_noaux", "none"])
 @pytest.mark.parametrize("M,N,K", P_SHAPES)
 def test_gemm_persistent_fwd(epi, M, N, K):
-    """gemm4p_kernel (persistent, next tile's K-tiles staged under the epilogue, direct stores) on the
-    forward layout against a float64 reference, and bit for bit against the default routing (the same
-    MFMA K-order and the same epilogue arithmetic)."""
+    """The persistent kernels (next tile's K-tiles staged under the epilogue, direct stores) on the
+    forward layout against a float64 reference, gemm4r bit for bit against gemm4p, and both against the
+    non-persistent gemm4w (the same MFMA K-order and the same epilogue arithmetic)."""
     k = _k()
     torch.manual_seed(26)
     x = (torch.randn(M, K, device="cuda") * 0.3).to(torch.bfloat16)
@@ -584,8 +492,8 @@ def test_gemm_persistent_fwd(epi, M, N, K):
     b = torch.randn(N, device="cuda")
     e = "bias_gelu" if epi == "gelu_noaux" else epi
     outs = []
-    # (key 11, key 14): persistent with whole-line staging (gemm4q), non-persistent, persistent gemm4p
-    for k11, k14 in ((1, 2), (0, 2), (1, 0)):
+    # (key 11, key 14): persistent gemm4r (default; gemm4p where K % 64 != 0), gemm4w, persistent gemm4p
+    for k11, k14 in ((1, 1), (0, 1), (1, 0)):
         old, old14 = _tune(11, k11), _tune(14, k14)
         try:
             aux = torch.full((M, N), float("nan"), device="cuda", dtype=torch.bfloat16) \
@@ -596,7 +504,7 @@ def test_gemm_persistent_fwd(epi, M, N, K):
         finally:
             _tune(11, old)
             _tune(14, old14)
-    # gemm4q and gemm4p: the same MFMA K order and epilogue, bit for bit
+    # gemm4r and gemm4p: the same MFMA K order and epilogue, bit for bit
     assert torch.equal(outs[0][0], outs[2][0])
     if outs[0][1] is not None:
         assert torch.equal(outs[0][1], outs[2][1])
@@ -614,9 +522,9 @@ def test_gemm_persistent_fwd(epi, M, N, K):
 @pytest.mark.parametrize("epi", ["none", "mul_aux", "none_beta"])
 @pytest.mark.parametrize("M,N,K", P_SHAPES)
 def test_gemm_persistent_dgrad(epi, M, N, K):
-    """gemm4p_kernel with a k-major B (input gradient), with the input-tile epilogues (aux product, beta = 1
-    residual accumulate: the tile read in the widened store layout and swapped back), against a float64
-    reference and bit for bit against the default routing (key 11 = 0)."""
+    """The persistent kernels with a k-major B (input gradient), with the input-tile epilogues (aux product,
+    beta = 1 residual accumulate: the tile read in the widened store layout and swapped back), against a
+    float64 reference, gemm4r against gemm4p and both against gemm4w (key 11 = 0), bit for bit."""
     k = _k()
     torch.manual_seed(27)
     dy = torch.randn(M, K, device="cuda").to(torch.bfloat16)
@@ -624,8 +532,8 @@ def test_gemm_persistent_dgrad(epi, M, N, K):
     aux = torch.randn(M, N, device="cuda").to(torch.bfloat16) if epi == "mul_aux" else None
     c0 = torch.randn(M, N, device="cuda").to(torch.bfloat16)
     outs = []
-    # (key 11, key 14): forward-only gemm4q (so gemm4p here), non-persistent, gemm4p, gemm4q (default)
-    for k11, k14 in ((1, 1), (0, 1), (1, 0), (1, 2)):
+    # (key 11, key 14): gemm4r (default), gemm4w, gemm4p
+    for k11, k14 in ((1, 1), (0, 1), (1, 0)):
         old, old14 = _tune(11, k11), _tune(14, k14)
         try:
             if epi == "none_beta":
@@ -638,8 +546,7 @@ def test_gemm_persistent_dgrad(epi, M, N, K):
         finally:
             _tune(11, old)
             _tune(14, old14)
-    assert torch.equal(outs[0], outs[2])          # gemm4p (key 14 = 1) == gemm4p (key 14 = 0)
-    assert torch.equal(outs[0], outs[3])          # gemm4q with a k-major B == gemm4p bit for bit
+    assert torch.equal(outs[0], outs[2])          # gemm4r with a k-major B == gemm4p bit for bit
     if epi == "none_beta":
         ref = c0.double() + dy.double() @ w.double()
     else:
@@ -650,7 +557,7 @@ def test_gemm_persistent_dgrad(epi, M, N, K):
 
 
 def test_gemm_persistent_falls_back_on_ragged_shapes():
-    """N % 256 != 0 / beta != 0: key 11 leaves those shapes on the other kernels (same results)."""
+    """N % 256 != 0: the persistent kernels leave the shape to gemm4w whatever key 11 says (same results)."""
     k = _k()
     torch.manual_seed(28)
     M, N, K = 4352, 808, 768
@@ -671,9 +578,10 @@ def test_gemm_persistent_falls_back_on_ragged_shapes():
 @pytest.mark.parametrize("M,N,K", P_SHAPES)
 @pytest.mark.parametrize("epi", ["bias", "none", "mul_aux", "none_beta", "bias_gelu_d"])
 def test_gemm_persistent_ring_variants(epi, M, N, K):
-    """eegf_tune key 18: gemm4q (0) and gemm4r (1, default: rolling A fragments in a 3 + 2 slot ring, two
-    barriers per K-tile pair) give the same bits on every persistent shape and epilogue (pair counts
-    np = K / 64 of 2..48; the cross-tile staging of both rings)."""
+    """eegf_tune key 14: gemm4p (0: 64-B half-line K-tiles, five-slot ring) and gemm4r (1, default: whole-
+    line K-tile pairs, rolling A fragments in a 3 + 2 slot ring, two barriers per pair) give the same bits on
+    every persistent shape and epilogue (pair counts np = K / 64 of 2..48; the cross-tile staging of both
+    rings)."""
     k = _k()
     torch.manual_seed(29)
     fwd = epi in ("bias", "bias_gelu_d")      # the others on the input-gradient layout (k-major B)
@@ -685,7 +593,7 @@ def test_gemm_persistent_ring_variants(epi, M, N, K):
     c0 = torch.randn(M, N, device="cuda").to(torch.bfloat16)
     outs = []
     for key in (0, 1):
-        old = _tune(18, key)
+        old = _tune(14, key)
         try:
             if epi == "none_beta":
                 out = c0.clone()
@@ -700,7 +608,7 @@ def test_gemm_persistent_ring_variants(epi, M, N, K):
             torch.cuda.synchronize()
             outs.append(out)
         finally:
-            _tune(18, old)
+            _tune(14, old)
     for o in outs[1:]:
         for a, r in zip(o, outs[0]):
             if r is not None:
