@@ -14,7 +14,11 @@
 
 namespace {
 
-__global__ void __launch_bounds__(256) adam_kernel(long n, float* __restrict__ p, const float* __restrict__ g,
+// ZERO (eegf_adam_consume): the gradient is written back as 0 once read, so the trainer's next backward
+// accumulates into a clean arena without a separate fill pass over it (4 B more per parameter here
+// instead of a 4-B-per-parameter memset launch: 148 M elements, 75 us per step)
+template <bool ZERO>
+__global__ void __launch_bounds__(256) adam_kernel(long n, float* __restrict__ p, float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v,
                                                    bf16* __restrict__ shadow, float b1, float b2, float eps, float wd,
                                                    float gscale, float step_size, float sqrt_bc2) {
@@ -35,6 +39,7 @@ __global__ void __launch_bounds__(256) adam_kernel(long n, float* __restrict__ p
     *(f32x4*)(p + i4) = pv;
     *(f32x4*)(m + i4) = mv;
     *(f32x4*)(v + i4) = vv;
+    if (ZERO) *(f32x4*)(g + i4) = f32x4{0.f, 0.f, 0.f, 0.f};
     if (shadow) {
       bf16x4 s;
       s[0] = (bf16)pv[0]; s[1] = (bf16)pv[1]; s[2] = (bf16)pv[2]; s[3] = (bf16)pv[3];
@@ -48,6 +53,7 @@ __global__ void __launch_bounds__(256) adam_kernel(long n, float* __restrict__ p
       v[i] = b2 * v[i] + (1.f - b2) * gr * gr;
       p[i] = p[i] - step_size * (m[i] / (sqrtf(v[i]) / sqrt_bc2 + eps));
       if (shadow) shadow[i] = (bf16)p[i];
+      if (ZERO) g[i] = 0.f;
     }
   }
 }
@@ -71,17 +77,32 @@ __global__ void __launch_bounds__(256) key_bias_kernel(long n, const long long* 
 
 }  // namespace
 
-extern "C" int eegf_adam(long n, float* p, const float* g, float* m, float* v, void* bf16_shadow, float lr, float beta1,
-                         float beta2, float eps, float weight_decay, float grad_scale, int step, hipStream_t stream) {
+namespace {
+template <bool ZERO>
+int adam_launch(long n, float* p, float* g, float* m, float* v, void* bf16_shadow, float lr, float beta1, float beta2,
+                float eps, float weight_decay, float grad_scale, int step, hipStream_t stream) {
   if (n <= 0 || !p || !g || !m || !v || step <= 0) return EEGF_ERR_ARG;
   if ((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) != 0) return EEGF_ERR_ARG;
   if (bf16_shadow && ((uintptr_t)bf16_shadow & 7) != 0) return EEGF_ERR_ARG;
   const double bc1 = 1.0 - pow((double)beta1, step), bc2 = 1.0 - pow((double)beta2, step);
   const float step_size = (float)(lr / bc1), sqrt_bc2 = (float)sqrt(bc2);
   const long blocks = (n + 1023) / 1024;
-  EEGF_LAUNCH(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, n, p, g, m, v, (bf16*)bf16_shadow,
-                     beta1, beta2, eps, weight_decay, grad_scale, step_size, sqrt_bc2);
+  EEGF_LAUNCH(adam_kernel<ZERO>, dim3((unsigned)blocks), dim3(256), 0, stream, n, p, g, m, v, (bf16*)bf16_shadow,
+              beta1, beta2, eps, weight_decay, grad_scale, step_size, sqrt_bc2);
   return (int)hipGetLastError();
+}
+}  // namespace
+
+extern "C" int eegf_adam(long n, float* p, const float* g, float* m, float* v, void* bf16_shadow, float lr, float beta1,
+                         float beta2, float eps, float weight_decay, float grad_scale, int step, hipStream_t stream) {
+  return adam_launch<false>(n, p, const_cast<float*>(g), m, v, bf16_shadow, lr, beta1, beta2, eps, weight_decay,
+                            grad_scale, step, stream);
+}
+
+extern "C" int eegf_adam_consume(long n, float* p, float* g, float* m, float* v, void* bf16_shadow, float lr,
+                                 float beta1, float beta2, float eps, float weight_decay, float grad_scale, int step,
+                                 hipStream_t stream) {
+  return adam_launch<true>(n, p, g, m, v, bf16_shadow, lr, beta1, beta2, eps, weight_decay, grad_scale, step, stream);
 }
 
 extern "C" int eegf_cast_f32_bf16(long n, const float* src, void* dst, hipStream_t stream) {

@@ -64,6 +64,7 @@ SIGNATURES: dict[str, list] = {
     "eegf_cross_entropy": [i32, i32, i32, vp, vp, i32, f32, vp, vp, vp, vp],
     "eegf_feawei_init": [i32, vp, i64, f32, i32, vp, vp, vp],
     "eegf_adam": [i64, vp, vp, vp, vp, vp, f32, f32, f32, f32, f32, f32, i32, vp],
+    "eegf_adam_consume": [i64, vp, vp, vp, vp, vp, f32, f32, f32, f32, f32, f32, i32, vp],
     "eegf_cast_f32_bf16": [i64, vp, vp, vp],
     "eegf_axpby": [i32, i64, f32, vp, f32, vp, vp],
     "eegf_tanh_bwd": [i32, i64, vp, vp, vp, vp],

@@ -13,6 +13,11 @@ clears it before its next use) and is not computed.  Parameter values after the 
 identical to the reference loop.  With world_size > 1 the gradients are averaged over ranks with
 RCCL all-reduce on arena grad ranges before each Adam; pass 2's all-reduces start during the
 backward, one BERT layer at a time (GradReducer).
+
+consume_grads (default True): each Adam step zeroes the gradient range it read (eegf_adam_consume) and
+the next zero_grad() skips its fill pass, so after step() the arena gradients read as zero instead of
+holding the last step's values until the next zero_grad (the reference order); pass False to inspect
+gradients after a step.
 """
 from __future__ import annotations
 
@@ -32,7 +37,7 @@ class FlatAdam:
     """torch.optim.Adam over one contiguous arena range, one fused launch per step (eegf_adam)."""
 
     def __init__(self, engine: FusionEngine, rng: tuple[int, int], lr=1e-6, betas=(0.9, 0.999), eps=1e-8,
-                 weight_decay=0.0, write_shadow=True, names=None):
+                 weight_decay=0.0, write_shadow=True, names=None, consume=True):
         self.e = engine
         self.lo, self.hi = rng
         # names: the group's parameters that take part in the graph.  torch.optim.Adam skips a
@@ -48,9 +53,16 @@ class FlatAdam:
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
         self.t = 0
         self.write_shadow = write_shadow
+        # consume: the step zeroes the gradient it read (eegf_adam_consume), so the next zero_grad() has
+        # nothing to clear.  The gradient range is then zero outside the backward that fills it; the
+        # trainers are its only writers (the sub-ranges Adam skips are never written at all).
+        self.consume = consume
+        self._clean = False
 
     def zero_grad(self):
-        self.e.a.grad[self.lo:self.hi].zero_()
+        if not self._clean:
+            self.e.a.grad[self.lo:self.hi].zero_()
+        self._clean = False
 
     def step(self, grad_scale: float = 1.0):
         """grad_scale multiplies the gradient as Adam reads it (1/N over an all-reduced sum)."""
@@ -63,12 +75,15 @@ class FlatAdam:
         for lo, hi in self.sub:
             o = lo - self.lo
             ev = self.e._ev_start("adam")
-            call("eegf_adam", hi - lo, a.master[lo:].data_ptr(), a.grad[lo:].data_ptr(), self.m[o:].data_ptr(),
+            call("eegf_adam_consume" if self.consume else "eegf_adam", hi - lo, a.master[lo:].data_ptr(), a.grad[lo:].data_ptr(), self.m[o:].data_ptr(),
                  self.v[o:].data_ptr(), None if sh is None else a.shadow[lo:].data_ptr(), float(self.lr),
                  float(self.betas[0]), float(self.betas[1]), float(self.eps), float(self.wd), float(grad_scale),
                  self.t, _s())
-            # master, gradient, m, v in; master, m, v out (+ the bf16 shadow): 28 (30) B per parameter
-            self.e._ev_end("adam", ev, 0.0, (hi - lo) * (28 + (2 if sh is not None else 0)))
+            # master, gradient, m, v in; master, m, v (+ the zeroed gradient, + the bf16 shadow) out
+            self.e._ev_end("adam", ev, 0.0, (hi - lo) * (28 + (4 if self.consume else 0) + (2 if sh is not None else 0)))
+        if self.consume:
+            # every written element of [lo, hi) lies in a stepped sub-range (the graph parameters' ranges)
+            self._clean = True
 
 
 class GradReducer:
@@ -224,13 +239,14 @@ def _merge_adjacent(rngs):
 
 
 class PriGumbelTrainer:
-    def __init__(self, engine: FusionEngine, lr: float = 1e-6, reducer: GradReducer | None = None):
+    def __init__(self, engine: FusionEngine, lr: float = 1e-6, reducer: GradReducer | None = None,
+                 consume_grads: bool = True):
         self.e = engine
         a = engine.a
         gp = engine.graph_params()
         self.model_params = {n for n in gp if n != "DP"}
-        self.model_opt = FlatAdam(engine, a.model_range, lr=lr, names=self.model_params)
-        self.dp_opt = FlatAdam(engine, a.dp_range, lr=lr, write_shadow=False)
+        self.model_opt = FlatAdam(engine, a.model_range, lr=lr, names=self.model_params, consume=consume_grads)
+        self.dp_opt = FlatAdam(engine, a.dp_range, lr=lr, write_shadow=False, consume=consume_grads)
         self.reduce = reducer or GradReducer()
         dev = a.device
         self.loss = torch.zeros(2, dtype=torch.float32, device=dev)
@@ -277,10 +293,11 @@ class SinglePassTrainer:
     """PriConcat / ConcatModel step: one fwd(hard=True) + bwd + Adam over all graph params
     (main_0430.train finetune loop :177-187; train.py:94-113)."""
 
-    def __init__(self, engine: FusionEngine, lr: float = 1e-6, reducer: GradReducer | None = None):
+    def __init__(self, engine: FusionEngine, lr: float = 1e-6, reducer: GradReducer | None = None,
+                 consume_grads: bool = True):
         self.e = engine
         self.params = engine.graph_params()
-        self.opt = FlatAdam(engine, (0, engine.a.numel), lr=lr, names=self.params)
+        self.opt = FlatAdam(engine, (0, engine.a.numel), lr=lr, names=self.params, consume=consume_grads)
         self.reduce = reducer or GradReducer()
         self.loss = torch.zeros(1, dtype=torch.float32, device=engine.a.device)
         self.correct = torch.zeros(1, dtype=torch.int32, device=engine.a.device)
@@ -310,10 +327,11 @@ class PriGumbelV1Trainer:
     loss = alpha * CE(mean) + max_j((1 - w_j) e^eps + w_j) (loss_function :80-93); the CE gradient
     scaled by alpha in the loss kernel, the privacy term's gradient added by eegf_v1_wloss."""
 
-    def __init__(self, engine: FusionEngine, alpha: float, lr: float = 1e-5, reducer: GradReducer | None = None):
+    def __init__(self, engine: FusionEngine, alpha: float, lr: float = 1e-5, reducer: GradReducer | None = None,
+                 consume_grads: bool = True):
         self.e, self.alpha = engine, float(alpha)
         self.params = engine.graph_params()
-        self.opt = FlatAdam(engine, (0, engine.a.numel), lr=lr, names=self.params)
+        self.opt = FlatAdam(engine, (0, engine.a.numel), lr=lr, names=self.params, consume=consume_grads)
         self.reduce = reducer or GradReducer()
         dev = engine.a.device
         self.loss = torch.zeros(2, dtype=torch.float32, device=dev)     # [alpha * CE, privacy term]

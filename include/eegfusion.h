@@ -307,6 +307,11 @@ int eegf_dropout(int dtype, long n, int group, float p, unsigned long long seed,
  * read is g * grad_scale (1 for a plain step, 1/N to average an all-reduced sum over N ranks). */
 int eegf_adam(long n, float* p, const float* g, float* m, float* v, void* bf16_shadow, float lr,
               float beta1, float beta2, float eps, float weight_decay, float grad_scale, int step, hipStream_t stream);
+/* eegf_adam that also writes g[i] = 0 once read: the optimizer step and the next iteration's
+ * optimizer.zero_grad() (past_acc.py:197,204) in one pass over the gradient range. */
+int eegf_adam_consume(long n, float* p, float* g, float* m, float* v, void* bf16_shadow, float lr,
+                      float beta1, float beta2, float eps, float weight_decay, float grad_scale, int step,
+                      hipStream_t stream);
 int eegf_cast_f32_bf16(long n, const float* src, void* dst, hipStream_t stream);
 /* attention_mask (int64, 1 = keep) -> additive key bias (0 / -1e30) */
 int eegf_key_bias(long n, const long long* mask, float* bias, hipStream_t stream);

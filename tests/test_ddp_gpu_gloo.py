@@ -36,7 +36,7 @@ def _worker(rank, world, port, q):
             m = PriGumbelModel(1.0, contract="W", dropout=0.0).cuda()
             # lr 0: pass 1's DP step must not differ between the local and the reduced run (the
             # averaged DP gradient would move DP differently and change pass 2's gradients)
-            tr = PriGumbelTrainer(m.engine, lr=0.0, reducer=reducer)
+            tr = PriGumbelTrainer(m.engine, lr=0.0, reducer=reducer, consume_grads=False)
             g = torch.Generator(device="cuda").manual_seed(100 + rank)       # rank-specific shard
             eeg = torch.randn(2, 64, 256, generator=g, device="cuda")
             act = torch.randn(2, 32, generator=g, device="cuda") * 0.5

@@ -578,6 +578,15 @@ def test_adam_matches_torch():
     torch.cuda.synchronize()
     assert torch.equal(p, p2) and torch.equal(m, m2) and torch.equal(v, v2)
     assert (shadow.float() - p).abs().max().item() <= 1e-2 * p.abs().max().item()
+    # eegf_adam_consume: bitwise the same step, and the gradient left zero (ragged tail included)
+    p3, m3, v3, g3 = p.clone(), m.clone(), v.clone(), g.clone()
+    lib.call("eegf_adam", n, p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), None, 1e-3, 0.9,
+             0.999, 1e-8, 0.01, 1.0, 5, _s())
+    lib.call("eegf_adam_consume", n, p3.data_ptr(), g3.data_ptr(), m3.data_ptr(), v3.data_ptr(), None, 1e-3, 0.9,
+             0.999, 1e-8, 0.01, 1.0, 5, _s())
+    torch.cuda.synchronize()
+    assert torch.equal(p, p3) and torch.equal(m, m3) and torch.equal(v, v3)
+    assert not bool(g3.any()) and bool(g.any())
 
 
 @pytest.mark.parametrize("dt", DT)
