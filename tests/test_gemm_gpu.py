@@ -228,11 +228,13 @@ def test_gemm_big_dgrad(epi, M, N, K):
 @pytest.mark.parametrize("epi", ["bias", "bias_gelu", "bias_relu", "bias_tanh", "dgelu", "drelu", "dtanh", "none",
                                  "bias_gelu_d", "mul_aux"])
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-def test_gemm_small_m_splitk_epilogues(dt, epi):
-    """Batch-row GEMMs (M = B) take split-K with the epilogue applied in the slab reduction."""
+@pytest.mark.parametrize("K", [2304, 768])
+def test_gemm_small_m_splitk_epilogues(dt, epi, K):
+    """Batch-row GEMMs (M = B): K = 2304 takes split-K with the epilogue applied in the slab reduction,
+    K = 768 the 32 x 32 tiles over the whole K (no slabs)."""
     k = _k()
     torch.manual_seed(10)
-    M, N, K = 256, 768, 2304
+    M, N = 256, 768
     ws = torch.empty(8 << 20, device="cuda")
     x = (torch.randn(M, K, device="cuda") * 0.2).to(dt)
     if epi.startswith("bias") or epi == "none":
