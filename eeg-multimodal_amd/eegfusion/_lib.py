@@ -100,6 +100,8 @@ def lib() -> C.CDLL:
                 "`python -m eegfusion.build` (hipcc --offload-arch=gfx950). There is no CPU fallback.")
         _LIB = C.CDLL(str(LIB_PATH), mode=os.RTLD_NOW | os.RTLD_GLOBAL)
         for name, argtypes in SIGNATURES.items():
+            if os.environ.get("EEGF_LIB") and not hasattr(_LIB, name):
+                continue        # an older build under A/B (tools/ab_round.sh) may lack newer entry points
             fn = getattr(_LIB, name)
             fn.argtypes = argtypes
             fn.restype = C.c_long if name in RESTYPE_LONG else C.c_int
@@ -123,6 +125,10 @@ def launch_counts() -> dict[str, int]:
         cnt, name = line.split("\t", 1)
         out[name] = out.get(name, 0) + int(cnt)
     return out
+
+
+def has(name: str) -> bool:
+    return hasattr(lib(), name)
 
 
 def exported_symbols() -> list[str]:

@@ -56,7 +56,7 @@ class FlatAdam:
         # consume: the step zeroes the gradient it read (eegf_adam_consume), so the next zero_grad() has
         # nothing to clear.  The gradient range is then zero outside the backward that fills it; the
         # trainers are its only writers (the sub-ranges Adam skips are never written at all).
-        self.consume = consume
+        self.consume = consume and _lib.has("eegf_adam_consume")   # (absent only in an older A/B build)
         self._clean = False
 
     def zero_grad(self):
