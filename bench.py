@@ -365,7 +365,7 @@ def hbm_kernel_graph_times(dev, B: int, adam_elems: int, seed: int, reps: int = 
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
             for _ in range(reps_t):
                 fn()
         graph.replay()
@@ -554,7 +554,7 @@ def main():
 
     # the small HBM-bound kernels timed by hipGraph replay (after the timed region; no effect on value)
     hbm_times = {}
-    if rank == 0 and not args.no_probe:
+    if world == 1 and not args.no_probe:
         try:
             adam_elems = sum(hi - lo for lo, hi in trainer.model_opt.sub) if hasattr(trainer, "model_opt") else \
                 sum(hi - lo for lo, hi in trainer.opt.sub)

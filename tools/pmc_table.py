@@ -58,7 +58,14 @@ GROUPS = {     # bf16 instantiations appear mangled in rocprofv3's CSV (DF16b), 
     "attn_bwd": ("attn_bwd256_kernel",),
     "ln_fwd": ("ln_fwd_kernel", "ln_fwd768_kernel"),
     "ln_bwd": ("ln_bwd_kernel",),
+    # the HBM-bound kernels bench.py reports in GB/s (its hbm_kernels object)
+    "fusion_fwd": ("fusion_fwd_kernel",),
+    "fusion_bwd": ("fusion_bwd_kernel",),
+    "cross_entropy": ("ce_kernel",),
+    "ln_fwd768": ("ln_fwd768_kernel",),
+    "adam": ("adam_kernel",),
 }
+HBM_GROUPS = ("fusion_fwd", "fusion_bwd", "cross_entropy", "ln_fwd768", "adam")
 # bench.py probes the QKV and FFN1 input gradients separately; they share one kernel and grid here
 # (and, on the persistent kernel, the three bias-only forwards share one)
 ALIASES = {"dgrad_qkv": "dgrad_qkv_ffn1", "dgrad_ffn1": "dgrad_qkv_ffn1", "qkv_fwd": "fwd_bias_qkv_ao_ffn2",
@@ -162,6 +169,15 @@ def main():
                    f"{f(r['mfma_busy'], '.3f')} | {f(r['clock_ghz'], '.2f')} | {f(mix, '.2f')} | "
                    f"{f(r['lds_conflict_frac'], '.3f')} | {f(r['hbm_bytes'] and r['hbm_bytes'] / 1e6, '.1f')} | "
                    f"{f(r['hbm_gbs'], '.0f')} | {f(r['l2_hit'], '.3f')} | `{short(r['kernel'])}` ({r['grid']}) |")
+    # the small HBM-bound kernels whatever their rank (the top-20 cut drops kernels of a few us)
+    out += ["", "HBM-bound kernels (bench.py hbm_kernels): HBM bytes from FETCH_SIZE / WRITE_SIZE as above", "",
+            "| ms/step | launches/step | avg us | HBM MB/launch | HBM GB/s | L2 hit | kernel (grid) |",
+            "|---:|---:|---:|---:|---:|---:|---|"]
+    for r in rows:
+        if any(fr in r["kernel"] for g in HBM_GROUPS for fr in GROUPS[g]):
+            out.append(f"| {f(r['ms_per_step'], '.3f')} | {r['launches_per_step']:.1f} | {r['avg_us']:.1f} | "
+                       f"{f(r['hbm_bytes'] and r['hbm_bytes'] / 1e6, '.2f')} | {f(r['hbm_gbs'], '.0f')} | "
+                       f"{f(r['l2_hit'], '.3f')} | `{short(r['kernel'])}` ({r['grid']}) |")
     (ROOT / "profiles" / f"{tag}_pmc_table.md").write_text("\n".join(out) + "\n")
     print("\n".join(out))
 
