@@ -27,7 +27,7 @@ struct GemmArgs {
   float alpha, beta, epi_scale;
   int ksplit;          // >0: split-K slice length (grid.z = slices, C = fp32 slabs [z][M][N])
   int lds_epi;         // LDS-staged coalesced epilogue (bf16 out, beta == 0)
-  int bt;              // output tile: 128, 64 or 32
+  int bt;              // output tile: 128 or 64
 };
 
 DEV void load4(const float* p, float (&v)[4]) { const f32x4 x = *(const f32x4*)p; v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3]; }
@@ -123,7 +123,7 @@ DEV void store_tile(T* lds, const u32x4* reg, int tid) {
   }
 }
 
-// BT: output tile BT x BT (128; 64 or 32 for the batch-row GEMMs whose 128-tile grids would leave most
+// BT: output tile BT x BT (128, or 64 for the batch-row GEMMs whose 128-tile grids would leave most
 // CUs idle); 4 waves in 2 x 2, each a (BT/2) x (BT/2) block of NI x NI 16x16 accumulators.
 template <typename T, bool AKC, bool BKC, typename TO, int EPI, int BT = 128>
 __global__ void __launch_bounds__(NT) gemm_kernel(GemmArgs g) {
@@ -436,9 +436,6 @@ int launch(const GemmArgs& a, int batch, hipStream_t s, int splits = 1) {
   if (a.bt == 64) {
     const int tiles = ((a.M + 63) / 64) * ((a.N + 63) / 64);
     EEGF_LAUNCH((gemm_kernel<T, AKC, BKC, TO, EPI, 64>), dim3(tiles, batch, splits), dim3(NT), 0, s, a);
-  } else if (a.bt == 32) {
-    const int tiles = ((a.M + 31) / 32) * ((a.N + 31) / 32);
-    EEGF_LAUNCH((gemm_kernel<T, AKC, BKC, TO, EPI, 32>), dim3(tiles, batch, splits), dim3(NT), 0, s, a);
   } else {
     const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
     EEGF_LAUNCH((gemm_kernel<T, AKC, BKC, TO, EPI>), dim3(tiles, batch, splits), dim3(NT), 0, s, a);
@@ -516,12 +513,11 @@ static int gemm_impl(int dtype, int out_dtype, int a_kcontig, int b_kcontig, int
   // workgroups; then split-K for long contractions (weight gradients, K = tokens) and for the
   // batch-row GEMMs; the fixed-order slab reduction applies the epilogue.
   if (((M + BM - 1) / BM) * ((N + BN - 1) / BN) * batch < 192) a.bt = 64;
-  // still under-filled at 64 x 64 with a short contraction (the decoder / head GEMMs over M = B rows, K
-  // <= 1024): 32 x 32 tiles, each workgroup over the whole K, instead of split-K slabs and a reduce
-  // launch (a 256 x 768 x 768 fp32 product was 11.8 us + a 5 us reduce on 48 tiles x 4 splits)
-  if (a.bt == 64 && ((M + 63) / 64) * ((N + 63) / 64) * batch < 192 && K <= 1024) a.bt = 32;
+  // (32 x 32 tiles over the whole K instead of split-K measured slower: a 256 x 768 x 768 fp32 product
+  // took 19.3 us on 192 workgroups against 11.7 us + a 5 us reduce on 48 tiles x 4 splits,
+  // profiles/r6e_prof_ab.log)
   const int tiles = ((M + a.bt - 1) / a.bt) * ((N + a.bt - 1) / a.bt);
-  if (a.bt != 32 && batch > 1 && epi == EPI_NONE && workspace && tiles * batch <= 256 && K >= 512) {
+  if (batch > 1 && epi == EPI_NONE && workspace && tiles * batch <= 256 && K >= 512) {
     // batched plain GEMMs on an under-filled grid (the decoder's per-head dq = dqp Wk_h, 48 workgroups
     // over K = 768 took 28 us): split K as for the batch-row GEMMs, slabs [split][batch][M][N]
     const int kt = dtype == EEGF_F32 ? 32 : 64;
@@ -550,7 +546,7 @@ static int gemm_impl(int dtype, int out_dtype, int a_kcontig, int b_kcontig, int
       }
     }
   }
-  if (a.bt != 32 && batch == 1 && workspace && tiles < 512 && (K >= 4096 || (tiles <= 256 && K >= 512))) {
+  if (batch == 1 && workspace && tiles < 512 && (K >= 4096 || (tiles <= 256 && K >= 512))) {
     const int kt = dtype == EEGF_F32 ? 32 : 64;
     int splits = 1;
     // fp32 batch-row GEMMs (decoder / head, 48-96 tiles): slices down to 128 so ~200 workgroups fill

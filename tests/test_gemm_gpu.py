@@ -230,8 +230,7 @@ def test_gemm_big_dgrad(epi, M, N, K):
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("K", [2304, 768])
 def test_gemm_small_m_splitk_epilogues(dt, epi, K):
-    """Batch-row GEMMs (M = B): K = 2304 takes split-K with the epilogue applied in the slab reduction,
-    K = 768 the 32 x 32 tiles over the whole K (no slabs)."""
+    """Batch-row GEMMs (M = B) take split-K with the epilogue applied in the slab reduction."""
     k = _k()
     torch.manual_seed(10)
     M, N = 256, 768
