@@ -482,8 +482,7 @@ int eegf_gemm_big(int a_kc, int b_kc, int epi, int out_f32, int M, int N, int K,
                   const void* B, long ldb, void* C, long ldc, const float* bias, void* aux, long ldaux, float alpha,
                   float beta, float epi_scale, void* workspace, long ws_bytes, hipStream_t stream);
 int eegf_gemm_big_wgrad_bias(int M, int N, int K, const void* A, long lda, const void* B, long ldb, float* C, long ldc,
-                             float beta, float* db, void* workspace, long ws_bytes, unsigned* counters,
-                             long n_counters, hipStream_t stream);
+                             float beta, float* db, void* workspace, long ws_bytes, hipStream_t stream);
 
 static int gemm_impl(int dtype, int out_dtype, int a_kcontig, int b_kcontig, int epi, int M, int N, int K, int batch,
                      const void* A, long lda, long strideA, const void* B, long ldb, long strideB, void* C, long ldc,
@@ -593,25 +592,10 @@ extern "C" int eegf_gemm(int dtype, int out_dtype, int a_kcontig, int b_kcontig,
                    stream);
 }
 
-extern "C" int eegf_gemm_wgrad_bias_tc(int dtype, int M, int N, int K, const void* dY, long ldd, const void* X,
-                                       long ldx, float* dW, long ldw, float beta, float* db, void* workspace,
-                                       long ws_bytes, unsigned int* tile_counters, long n_counters,
-                                       hipStream_t stream) {
-  if (dtype != EEGF_BF16 || !dY || !X || !dW || !db || M <= 0 || N <= 0 || K <= 0) return EEGF_ERR_ARG;
-  if (n_counters < 0 || (tile_counters && ((uintptr_t)tile_counters & 3))) return EEGF_ERR_ARG;
-  const int st = eegf_gemm_big_wgrad_bias(M, N, K, dY, ldd, X, ldx, dW, ldw, beta, db, workspace, ws_bytes,
-                                          tile_counters, n_counters, stream);
-  return st == 1 ? EEGF_ERR_ARG : st;
-}
-
 extern "C" int eegf_gemm_wgrad_bias(int dtype, int M, int N, int K, const void* dY, long ldd, const void* X, long ldx,
                                     float* dW, long ldw, float beta, float* db, void* workspace, long ws_bytes,
                                     hipStream_t stream) {
-  return eegf_gemm_wgrad_bias_tc(dtype, M, N, K, dY, ldd, X, ldx, dW, ldw, beta, db, workspace, ws_bytes, nullptr, 0,
-                                 stream);
-}
-
-extern "C" long eegf_gemm_wgrad_counters(int M, int N) {
-  if (M <= 0 || N <= 0) return EEGF_ERR_ARG;
-  return (long)((M + 255) / 256) * ((N + 255) / 256);
+  if (dtype != EEGF_BF16 || !dY || !X || !dW || !db || M <= 0 || N <= 0 || K <= 0) return EEGF_ERR_ARG;
+  const int st = eegf_gemm_big_wgrad_bias(M, N, K, dY, ldd, X, ldx, dW, ldw, beta, db, workspace, ws_bytes, stream);
+  return st == 1 ? EEGF_ERR_ARG : st;
 }

@@ -31,9 +31,6 @@ struct BigArgs {
   float alpha, beta, epi_scale;
   int ksplit;            // >0: split-K slice length; C = fp32 slabs [blockIdx.y][M][N]
   float* rowsum_part;    // gemm4w RS only: [splits][M] sums over this split's K of each row of a k-major A
-  unsigned* counters;    // gemm4w RS, split-K: per-tile arrival counters (zero on entry, left zero), or null
-  float* rs_C;           // with counters: the weight gradient C (row stride ldc) the slabs are reduced into
-  float* rs_db;          // with counters: the bias gradient db[M] the last arrival of a tile-column-0 tile adds to
   long long* ts;         // diagnostics (eegf_gemm_big_timestamps): per-workgroup phase times, null = off
   int group_m;           // tile raster: 0 row-major, G > 0 groups of G row panels walked column by column
 };
@@ -385,82 +382,6 @@ DEV bf16x8 rd_col_off(const bf16* t, int o0, int o1) {
   return r;
 }
 
-// In-kernel split-K reduction of the weight gradients (eegf_gemm_wgrad_bias with tile counters): every
-// (split, tile) workgroup has stored its fp32 slab (and, in tile column 0, its row sums); the workgroup
-// that arrives last at the tile's counter sums the tile's slabs in split order into C (+ beta C) and, in
-// tile column 0, the row-sum partials into db -- the arithmetic of splitk_rowsum_reduce in the same
-// order, so bitwise its results -- and resets the counter to zero for the next call.  Nobody waits: the
-// other workgroups just exit.  Device-scope release (every thread's slab stores retired, then an agent-
-// scope fence before the counter increment) and acquire (a fence before the slab reads) make the other
-// XCDs' slabs visible through the non-coherent L2s.
-// flag: one int of the (by now idle) operand ring, the workgroup's broadcast of the arrival test
-DEV void splitk_last_arrival_reduce(const BigArgs& g, int t, int m0, int n0, bool col0, int splits, int tid,
-                                    int* flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    __threadfence();
-    const unsigned old = atomicAdd(g.counters + t, 1u);
-    const int last = old == (unsigned)(splits - 1);
-    if (last) atomicExch(g.counters + t, 0u);
-    *flag = last;
-  }
-  __syncthreads();
-  if (!*flag) return;
-  __threadfence();
-  const long MN = (long)g.M * g.N;
-  const float* slabs = (const float*)g.C;
-  float* C = g.rs_C;
-  // 64 float4 per thread: row e / 64, column group (e % 64) * 4 of the 256 x 256 tile, RB of them at a
-  // time, the splits' loads issued 8 at a time before they are summed (in split order)
-  constexpr int RB = 4, SB = 8;
-#pragma unroll 1
-  for (int e0 = 0; e0 < 64; e0 += RB) {
-    long off[RB];
-    bool ok[RB];
-    f32x4 o[RB];
-#pragma unroll
-    for (int q = 0; q < RB; ++q) {
-      const int e = tid + 256 * (e0 + q);
-      const int m = m0 + e / 64, n = n0 + (e % 64) * 4;
-      ok[q] = m < g.M && n < g.N;
-      off[q] = ok[q] ? (long)m * g.N + n : 0;
-      o[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-#pragma unroll 1
-    for (int s0 = 0; s0 < splits; s0 += SB) {
-      f32x4 v[RB][SB];
-#pragma unroll
-      for (int q = 0; q < RB; ++q)
-#pragma unroll
-        for (int s = 0; s < SB; ++s)
-          if (s0 + s < splits) v[q][s] = *(const f32x4*)(slabs + (long)(s0 + s) * MN + off[q]);
-#pragma unroll
-      for (int q = 0; q < RB; ++q)
-#pragma unroll
-        for (int s = 0; s < SB; ++s)
-          if (s0 + s < splits) o[q] += v[q][s];
-    }
-#pragma unroll
-    for (int q = 0; q < RB; ++q) {
-      if (!ok[q]) continue;
-      const long m = off[q] / g.N, n = off[q] % g.N;
-      float* c = C + m * g.ldc + n;
-      f32x4 r = o[q];
-      if (g.beta != 0.f) r += g.beta * *(const f32x4*)c;
-      *(f32x4*)c = r;
-    }
-  }
-  if (col0) {
-    const int m = m0 + tid;
-    if (m < g.M) {
-      float v = 0.f;
-      for (int s = 0; s < splits; ++s) v += g.rowsum_part[(long)s * g.M + m];
-      g.rs_db[m] += v;
-    }
-  }
-}
-
 // AKC / BKC: operand K-contiguous (row-major [rows][K] image, ds_read_b128 fragments) or k-major
 // ([K][cols] in memory: [32 k][256 cols] image with the swz_k chunk swizzle of stage_kmajor,
 // ds_read_b64_tr_b16 fragments: input-gradient B, weight-gradient A and B)
@@ -701,10 +622,6 @@ __global__ void __launch_bounds__(NT4, 1) gemm4w_kernel(BigArgs g) {
   ts_mark(g, 2);
   big_epilogue<EPI, TO, 8, NT4>(g, acc, lds, m0, n0, tid, lane, wm, wn, split);
   ts_mark(g, 3);
-  if constexpr (RS && sizeof(TO) == 4) {
-    if (g.counters && gridDim.y > 1)
-      splitk_last_arrival_reduce(g, t, m0, n0, tn == 0, (int)gridDim.y, tid, (int*)lds);
-  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1462,8 +1379,7 @@ int wgrad_splits(int M, int N, int K, long ws_bytes, long extra) {
 // fp32 split-K slabs followed by the fixed-order slab and row-sum reductions.  Returns 1 when the shape
 // is not eligible (the caller then runs the plain GEMM and a column reduction).
 int eegf_gemm_big_wgrad_bias(int M, int N, int K, const void* A, long lda, const void* B, long ldb, float* C, long ldc,
-                             float beta, float* db, void* workspace, long ws_bytes, unsigned* counters,
-                             long n_counters, hipStream_t stream) {
+                             float beta, float* db, void* workspace, long ws_bytes, hipStream_t stream) {
   if (K % BK != 0 || M % 8 != 0 || N % 8 != 0 || M < 256 || N < 256 || K < 4096) return 1;
   if (lda % 8 || ldb % 8 || ldc % 4 || !workspace) return 1;
   if ((((uintptr_t)A | (uintptr_t)B) & 15) != 0) return 1;
@@ -1473,22 +1389,13 @@ int eegf_gemm_big_wgrad_bias(int M, int N, int K, const void* A, long lda, const
   splits = (K + ks - 1) / ks;
   float* slabs = (float*)workspace;
   float* part = slabs + (splits > 1 ? (long)splits * M * N : 0);
-  const int tiles = ((M + TM - 1) / TM) * ((N + TN - 1) / TN);
   BigArgs a{(const bf16*)A, (const bf16*)B, splits > 1 ? (void*)slabs : (void*)C, nullptr, nullptr, lda, ldb, ldc, 0,
-            M, N, K, 1.0f, beta, 1.0f, splits > 1 ? ks : 0, part, nullptr, nullptr, nullptr, g_ts_buf, group_for(N)};
-  // tile counters given: the last-arriving workgroup of each tile reduces its slabs (no reduce launch)
-  const bool fused = splits > 1 && counters && n_counters >= tiles && ((uintptr_t)C & 15) == 0;
-  if (fused) {
-    a.counters = counters;
-    a.rs_C = C;
-    a.rs_db = db;
-  }
+            M, N, K, 1.0f, beta, 1.0f, splits > 1 ? ks : 0, part, g_ts_buf, group_for(N)};
+  const int tiles = ((M + TM - 1) / TM) * ((N + TN - 1) / TN);
   EEGF_LAUNCH((gemm4w_kernel<false, false, EPI_NONE, float, true>), dim3(tiles, splits), dim3(NT4), 0,
                      stream, a);
   const int nrow = (M + 255) / 256;
-  if (fused) {
-    return (int)hipGetLastError();
-  } else if (splits > 1) {
+  if (splits > 1) {
     const long MN = (long)M * N;
     const int nslab = (int)((MN / 4 + 255) / 256);
     EEGF_LAUNCH(splitk_rowsum_reduce, dim3((unsigned)(nslab + nrow)), dim3(256), 0, stream, (const float*)slabs,
@@ -1510,7 +1417,7 @@ int eegf_gemm_big(int a_kc, int b_kc, int epi, int out_f32, int M, int N, int K,
   if (lda % 8 || ldb % 8 || ldc % 8 || (aux && ldaux % 8)) return 1;
   if ((((uintptr_t)A | (uintptr_t)B | (uintptr_t)C | (uintptr_t)aux) & 15) != 0) return 1;
   BigArgs a{(const bf16*)A, (const bf16*)B, C, bias, (bf16*)aux, lda, ldb, ldc, ldaux, M, N, K, alpha, beta,
-            epi_scale, 0, nullptr, nullptr, nullptr, nullptr, g_ts_buf, group_for(N)};
+            epi_scale, 0, nullptr, g_ts_buf, group_for(N)};
   if (out_f32) {
     if (a_kc || b_kc || epi != EPI_NONE || M < 256 || N < 256 || K < 4096 || ldc % 4) return 1;
     int splits = wgrad_splits(M, N, K, ws_bytes, 0);

@@ -39,8 +39,6 @@ SIGNATURES: dict[str, list] = {
     "eegf_seq_mean": [i32, i32, i32, i32, vp, i64, vp, i64, vp],
     "eegf_seq_mean_bwd": [i32, i32, i32, i32, vp, i64, vp, i64, f32, vp],
     "eegf_gemm_wgrad_bias": [i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, f32, vp, vp, i64, vp],
-    "eegf_gemm_wgrad_bias_tc": [i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, f32, vp, vp, i64, vp, i64, vp],
-    "eegf_gemm_wgrad_counters": [i32, i32],
     "eegf_tune": [i32, i32],
     "eegf_gemm_big_timestamps": [vp],
     "eegf_ring_proxy": [i64, i32, i32, vp, vp],
@@ -85,7 +83,7 @@ SIGNATURES: dict[str, list] = {
     "eegf_dp_clip_rows": [i32, i32, vp, f32, vp, vp, vp],
     "eegf_dp_noise": [i64, vp, f32, f32, u64, u64, vp],
 }
-RESTYPE_LONG = {"eegf_ln_bwd_partial_rows", "eegf_gemm_wgrad_counters", "eegf_attn_bwd_workspace", "eegf_ghost_norm_workspace",
+RESTYPE_LONG = {"eegf_ln_bwd_partial_rows", "eegf_attn_bwd_workspace", "eegf_ghost_norm_workspace",
                 "eegf_attn_varlen_bwd_workspace", "eegf_launch_log_read"}
 
 

@@ -257,13 +257,8 @@ class FusionEngine:
         ev = self._ev_start("wgrad" if M >= 4096 else None)
         if gb is not None and _code(dy) == BF16 and _code(x) == BF16:
             ws = self.ws.get("splitk", SPLITK_WS, torch.float32)
-            if _lib.has("eegf_gemm_wgrad_bias_tc"):       # (absent only in an older A/B build)
-                cnt = self._tile_counters()
-                st = _lib.lib().eegf_gemm_wgrad_bias_tc(BF16, N, K, M, P(dy), ldd or N, P(x), ldx or K, P(g), K, 1.0,
-                                                        P(gb), P(ws), ws.numel() * 4, P(cnt), cnt.numel(), _stream())
-            else:
-                st = _lib.lib().eegf_gemm_wgrad_bias(BF16, N, K, M, P(dy), ldd or N, P(x), ldx or K, P(g), K, 1.0,
-                                                     P(gb), P(ws), ws.numel() * 4, _stream())
+            st = _lib.lib().eegf_gemm_wgrad_bias(BF16, N, K, M, P(dy), ldd or N, P(x), ldx or K, P(g), K, 1.0,
+                                                 P(gb), P(ws), ws.numel() * 4, _stream())
             if st != 0 and st != _lib.ERR_ARG:
                 raise RuntimeError(f"eegf_gemm_wgrad_bias failed with status {st} (hipError)")
             if st == 0:
@@ -273,14 +268,6 @@ class FusionEngine:
         self._ev_end("wgrad" if M >= 4096 else None, ev, 2.0 * M * N * K)
         if gb is not None:
             self.colsum(dy, ldd or N, M, N, gb)
-
-    def _tile_counters(self):
-        """the weight-gradient GEMM's split-K tile counters: zeroed once here, left zero by every call
-        (eegf_gemm_wgrad_bias), so they need no per-call clearing"""
-        c = getattr(self, "_wgrad_counters", None)
-        if c is None:
-            c = self._wgrad_counters = torch.zeros(4096, dtype=torch.int32, device=self.a.device)
-        return c
 
     def bgrad(self, dy, name, rows, width=None, ld=None, period=1, out=None):
         if out is None and not self.need(name):

@@ -104,24 +104,13 @@ long eegf_launch_log_read(char* buf, long cap);
  * The row sums ride on the weight-gradient kernel: the workgroups of tile column 0 run one
  * v_mfma_f32_16x16x32_bf16 per 16-row block and K-tile against a ones operand (a column of the result
  * holds the K-tile's sum of one row), into a VGPR accumulator; deterministic, in the MFMA's summation
- * order (not bitwise the earlier VALU order).  workspace: fp32 split-K slabs (splits x (M*N + M)
- * floats).  The slabs are summed in split order (bitwise reproducible) either by a separate reduce
- * launch or, in eegf_gemm_wgrad_bias_tc when tile_counters is given (n_counters >= eegf_gemm_wgrad_counters(M, N) zero-initialised
- * uint32, e.g. once at allocation; every call leaves them zero again), inside the GEMM: the workgroup
- * that arrives last at a tile's counter sums that tile's slabs (same order, same bits) -- no reduce
- * launch.  Calls sharing one counter array must be stream-ordered.  EEGF_ERR_ARG when the shape is not
- * eligible (bf16, M, N >= 256, K >= 4096, K % 64 == 0, 8-aligned dims, 16-B aligned dY / X, workspace
- * too small): run eegf_gemm and eegf_colsum instead. */
-int eegf_gemm_wgrad_bias_tc(int dtype, int M, int N, int K, const void* dY, long ldd, const void* X, long ldx,
-                            float* dW, long ldw, float beta, float* db, void* workspace, long ws_bytes,
-                            unsigned int* tile_counters, long n_counters, hipStream_t stream);
-/* the same without tile counters (the separate reduce launch) */
+ * order (not bitwise the earlier VALU order), and reduced over the splits in a fixed order.  workspace: fp32 split-K slabs
+ * (splits x (M*N + M) floats).  EEGF_ERR_ARG when the shape is not eligible (bf16, M, N >= 256,
+ * K >= 4096, K % 64 == 0, 8-aligned dims, 16-B aligned dY / X, workspace too small): run eegf_gemm and
+ * eegf_colsum instead. */
 int eegf_gemm_wgrad_bias(int dtype, int M, int N, int K, const void* dY, long ldd, const void* X, long ldx,
                          float* dW, long ldw, float beta, float* db, void* workspace, long ws_bytes,
                          hipStream_t stream);
-/* tile counters eegf_gemm_wgrad_bias's in-kernel reduction needs for an M x N weight gradient */
-long eegf_gemm_wgrad_counters(int M, int N);
-
 /* ---- contract T pad skipping (varlen BERT).  The reference runs BERT over the
  * padded 512 tokens (get_embedding.py:115) with the padded keys masked (model.py:37-43); the packed
  * rows of the real tokens give the same outputs.  cu_seqlens [B+1] int32 (device): sequence b owns
