@@ -62,8 +62,12 @@ template <typename T, int BT = 128>
 struct TileCfg {
   static constexpr int KT = 128 / (int)sizeof(T);        // contraction elements per k-step
   static constexpr int VE = 16 / (int)sizeof(T);         // elements per 16-B chunk
-  // K-contiguous LDS tile: [BT rows][KT] + 16 B pad per row
-  static constexpr int RS_KC = KT + VE;
+  // K-contiguous LDS tile: [BT rows][KT], rows of exactly 128 B with 16-B chunk c of row r stored at
+  // c ^ kc_swz(r) (below).  The round-5 layout padded each row by 16 B (36 words): ds_read_b128 serves
+  // a wave in four 16-lane groups of mixed rows and chunks (MI355X_MICROARCH.md, LDS table), and rows
+  // 10 / 12 and 11 / 13 of such a group met on one bank quad -- 2-way conflicts, 0.17-0.33 of the fp32
+  // decoder GEMMs' LDS cycles in profiles/r6x_pmc_table.md
+  static constexpr int RS_KC = KT;
   // k-major LDS tile: [KT rows][BT] + 32 B pad per row
   static constexpr int RS_KM = BT + 2 * VE;
   // fp32 k-major tiles: rows 8 apart (the four 16-lane groups of an fp32 ld_col8) would sit a multiple
@@ -74,6 +78,12 @@ struct TileCfg {
   static constexpr int SKEW = sizeof(T) == 4 ? 16 : 0;
   static DEV int skew(int krow) { return SKEW * ((krow >> 3) & 3); }
   static constexpr int SZ_KC = BT * RS_KC;
+  // chunk swizzle of the K-contiguous tiles: a function of bits 1-2 of the row, so every fragment read
+  // (rows r0 + (lane & 15), r0 % 16 == 0) and every staging store (rows (tid >> 3) + 32 i) keeps one
+  // per-lane value.  Chosen by exhaustive search over the linear XOR maps of the row's low bits: every
+  // 16-lane group of the bf16 (chunk 4 kc + lane / 16) and fp32 (chunks 2 (lane / 16) + {0, 1}) fragment
+  // reads covers the 16 bank quads once; the 8-lane ds_write_b128 groups write one whole 128-B row
+  static DEV int kc_swz(int r) { return (((r >> 1) & 1) << 2) ^ (((r >> 2) & 1) * 3); }
   static constexpr int SZ_KM = KT * RS_KM + 3 * SKEW;
   static constexpr int CHUNKS = BT * 8 / NT;             // 16-B chunks per thread per operand tile
 };
@@ -110,6 +120,17 @@ DEV void load_tile(u32x4* reg, const T* __restrict__ base, long ld, int mn0, int
   }
 }
 
+// 8 contiguous K elements at K offset kk (a multiple of 8) of a swizzled K-contiguous tile row
+DEV bf16x8 ld_kc8(const bf16* row, int kk, int s) { return *(const bf16x8*)(row + (((kk >> 3) ^ s) << 3)); }
+DEV f32x8 ld_kc8(const float* row, int kk, int s) {
+  const f32x4 a = *(const f32x4*)(row + (((kk >> 2) ^ s) << 2));
+  const f32x4 b = *(const f32x4*)(row + ((((kk >> 2) + 1) ^ s) << 2));
+  f32x8 r;
+  r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
+  r[4] = b[0]; r[5] = b[1]; r[6] = b[2]; r[7] = b[3];
+  return r;
+}
+
 template <typename T, bool KC, int BT>
 DEV void store_tile(T* lds, const u32x4* reg, int tid) {
   using C = TileCfg<T, BT>;
@@ -119,7 +140,7 @@ DEV void store_tile(T* lds, const u32x4* reg, int tid) {
     int r, col;
     if (KC) { r = c >> 3; col = (c & 7) * C::VE; }
     else    { constexpr int CPR = BT / C::VE; r = c / CPR; col = (c % CPR) * C::VE; }
-    st16(lds + (KC ? r * C::RS_KC : r * C::RS_KM + C::skew(r)) + col, reg[i]);
+    st16(lds + (KC ? r * C::RS_KC + (((c & 7) ^ C::kc_swz(r)) * C::VE) : r * C::RS_KM + C::skew(r) + col), reg[i]);
   }
 }
 
@@ -132,7 +153,10 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmArgs g) {
   using F = typename Frag8<T>::type;
   constexpr int SZA = AKC ? C::SZ_KC : C::SZ_KM;
   constexpr int SZB = BKC ? C::SZ_KC : C::SZ_KM;
-  __shared__ __attribute__((aligned(16))) T lds[SZA + SZB];
+  // the bf16 LDS-staged epilogue reuses the array as a [128][BN + 8] output tile (34.8 KB, more than the
+  // two unpadded 16-KB operand tiles)
+  constexpr int SZE = (sizeof(T) == 2 && BT == 128) ? BM * (BN + 8) : 0;
+  __shared__ __attribute__((aligned(16))) T lds[SZA + SZB > SZE ? SZA + SZB : SZE];
   T* As = lds;
   T* Bs = lds + SZA;
 
@@ -159,6 +183,7 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmArgs g) {
     for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   u32x4 ra[C::CHUNKS], rb[C::CHUNKS];
+  const int kcs = C::kc_swz(lane & 15);     // the K-contiguous fragment rows' chunk swizzle
   const int nk = (kend - kbeg + C::KT - 1) / C::KT;
   load_tile<T, AKC, BT>(ra, A, g.lda, m0, kbeg, g.M, kend, tid);
   load_tile<T, BKC, BT>(rb, B, g.ldb, n0, kbeg, g.N, kend, tid);
@@ -179,13 +204,13 @@ __global__ void __launch_bounds__(NT) gemm_kernel(GemmArgs g) {
 #pragma unroll
       for (int i = 0; i < NI; ++i) {
         const int r = wm * WT + i * 16;
-        if (AKC) a[i] = ld_row8(As + (r + (lane & 15)) * C::RS_KC + kk);
+        if (AKC) a[i] = ld_kc8(As + (r + (lane & 15)) * C::RS_KC, kk, kcs);
         else     a[i] = ld_col8(As + C::skew(kk), C::RS_KM, kk, r, lane);
       }
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
         const int c = wn * WT + j * 16;
-        if (BKC) b[j] = ld_row8(Bs + (c + (lane & 15)) * C::RS_KC + kk);
+        if (BKC) b[j] = ld_kc8(Bs + (c + (lane & 15)) * C::RS_KC, kk, kcs);
         else     b[j] = ld_col8(Bs + C::skew(kk), C::RS_KM, kk, c, lane);
       }
 #pragma unroll
