@@ -52,6 +52,30 @@ __global__ void __launch_bounds__(512) ubench_kernel(int iters, uint32_t seed, l
       r0 = (uint32_t)q0; r1 = (uint32_t)q1; r2 = (uint32_t)q2; r3 = (uint32_t)q3;
     }
     if constexpr (OP == 8) BODY8("v_mul_u32_u24");
+    if constexpr (OP == 10) {   // v_fmac_f32, 64 per iteration: the loop branch amortised 8x further
+#pragma unroll
+      for (int u = 0; u < 8; ++u) BODY8("v_fmac_f32");
+    }
+    if constexpr (OP == 11) {   // v_exp_f32, 64 per iteration
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        asm volatile("v_exp_f32 %0, %0\n\tv_exp_f32 %1, %1\n\tv_exp_f32 %2, %2\n\tv_exp_f32 %3, %3\n\t"
+                     "v_exp_f32 %4, %4\n\tv_exp_f32 %5, %5\n\tv_exp_f32 %6, %6\n\tv_exp_f32 %7, %7"
+                     : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+v"(r4), "+v"(r5), "+v"(r6), "+v"(r7));
+    }
+    if constexpr (OP == 12) {   // v_mad_u64_u32, 64 per iteration (4 chains x 2 per BODY)
+      uint64_t q0 = r0, q1 = r1, q2 = r2, q3 = r3;
+      uint64_t c0, c1, c2, c3;
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        asm volatile("v_mad_u64_u32 %0, %4, %8, %9, %0\n\tv_mad_u64_u32 %1, %5, %8, %9, %1\n\t"
+                     "v_mad_u64_u32 %2, %6, %8, %9, %2\n\tv_mad_u64_u32 %3, %7, %8, %9, %3\n\t"
+                     "v_mad_u64_u32 %0, %4, %8, %9, %0\n\tv_mad_u64_u32 %1, %5, %8, %9, %1\n\t"
+                     "v_mad_u64_u32 %2, %6, %8, %9, %2\n\tv_mad_u64_u32 %3, %7, %8, %9, %3"
+                     : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3), "=&s"(c0), "=&s"(c1), "=&s"(c2), "=&s"(c3)
+                     : "v"(a), "v"(b));
+      r0 = (uint32_t)q0; r1 = (uint32_t)q1; r2 = (uint32_t)q2; r3 = (uint32_t)q3;
+    }
     if constexpr (OP == 9) {   // v_rcp_f32 (1 source)
       asm volatile("v_rcp_f32 %0, %0\n\tv_rcp_f32 %1, %1\n\tv_rcp_f32 %2, %2\n\tv_rcp_f32 %3, %3\n\t"
                    "v_rcp_f32 %4, %4\n\tv_rcp_f32 %5, %5\n\tv_rcp_f32 %6, %6\n\tv_rcp_f32 %7, %7"
@@ -80,6 +104,9 @@ extern "C" int ubench(int op, int blocks, int threads, int iters, long long* cyc
     case 7: hipLaunchKernelGGL(ubench_kernel<7>, g, t, 0, 0, iters, 12345u, cyc, sink); break;
     case 8: hipLaunchKernelGGL(ubench_kernel<8>, g, t, 0, 0, iters, 12345u, cyc, sink); break;
     case 9: hipLaunchKernelGGL(ubench_kernel<9>, g, t, 0, 0, iters, 12345u, cyc, sink); break;
+    case 10: hipLaunchKernelGGL(ubench_kernel<10>, g, t, 0, 0, iters, 12345u, cyc, sink); break;
+    case 11: hipLaunchKernelGGL(ubench_kernel<11>, g, t, 0, 0, iters, 12345u, cyc, sink); break;
+    case 12: hipLaunchKernelGGL(ubench_kernel<12>, g, t, 0, 0, iters, 12345u, cyc, sink); break;
     default: return -1;
   }
   return (int)hipGetLastError();

@@ -8,7 +8,8 @@ from pathlib import Path
 import torch
 
 OPS = ["v_add_u32", "v_mul_lo_u32", "v_mul_hi_u32", "v_fma_f32", "v_xor_b32", "v_mad_u64_u32", "v_exp_f32",
-       "v_pk_fma_f32", "v_mul_u32_u24", "v_rcp_f32"]
+       "v_pk_fma_f32", "v_mul_u32_u24", "v_rcp_f32", "v_fma_f32 x64", "v_exp_f32 x64", "v_mad_u64 x64"]
+PER_ITER = [8] * 10 + [64, 64, 64]      # instructions per loop iteration (the x64 forms amortise the branch)
 
 
 def main():
@@ -26,8 +27,8 @@ def main():
             torch.cuda.synchronize()
             c = cyc.view(-1, 2)[:, 0].double().sort().values
             rt = cyc.view(-1, 2)[:, 1].double().sort().values
-            ns = float(rt[len(rt) // 2]) * 10.0 / (iters * 8)       # wall ns per instruction of one wave
-            print(f"{name:16s} waves/SIMD {threads // 256}: {float(c[len(c) // 2]) / (iters * 8):6.2f} cyc/inst "
+            ns = float(rt[len(rt) // 2]) * 10.0 / (iters * PER_ITER[op])       # wall ns per instruction of one wave
+            print(f"{name:16s} waves/SIMD {threads // 256}: {float(c[len(c) // 2]) / (iters * PER_ITER[op]):6.2f} cyc/inst "
                   f"(s_memtime)  {ns:6.3f} ns/inst per wave  SIMD rate {threads // 256 / ns:6.3f} inst/ns",
                   flush=True)
 
