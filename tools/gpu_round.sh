@@ -22,6 +22,7 @@ for s in "${@:2}"; do
     gemm) step gemm timeout -k 10 300 python -u tools/gemm_bench.py > $O/${TAG}_gemm.log 2>&1 || exit 1 ;;
     bench) step bench timeout -k 10 580 python -u bench.py > $O/${TAG}_bench.json 2> $O/${TAG}_bench.err || exit 1 ;;
     prof) (cd /tmp && export TMPDIR=/tmp && step prof timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$O/${TAG}_prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 4 --warmup 2 --no-cpu-baseline > $GRAFT_REPO_ROOT/$O/${TAG}_prof.log 2>&1) || exit 1 ;;
+    profnp) (cd /tmp && export TMPDIR=/tmp && step profnp timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$O/${TAG}_profnp -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 6 --warmup 2 --no-cpu-baseline --no-probe > $GRAFT_REPO_ROOT/$O/${TAG}_profnp.log 2>&1) || exit 1 ;;
     c5) step c5 timeout -k 10 600 python -u bench.py --batch 512 --eps-sweep 0.1,1,3,5,10 --feawei 2048 --steps 4 --warmup 2 --no-cpu-baseline > $O/${TAG}_c5.json 2> $O/${TAG}_c5.err || exit 1 ;;
     priconcat) step priconcat timeout -k 10 300 python -u bench.py --variant priconcat --no-cpu-baseline > $O/${TAG}_priconcat.json 2> $O/${TAG}_priconcat.err || exit 1 ;;
     b512) step b512 timeout -k 10 300 python -u bench.py --batch 512 --no-cpu-baseline > $O/${TAG}_b512.json 2> $O/${TAG}_b512.err || exit 1 ;;
