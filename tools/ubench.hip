@@ -63,6 +63,33 @@ __global__ void __launch_bounds__(512) ubench_kernel(int iters, uint32_t seed, l
                      "v_exp_f32 %4, %4\n\tv_exp_f32 %5, %5\n\tv_exp_f32 %6, %6\n\tv_exp_f32 %7, %7"
                      : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+v"(r4), "+v"(r5), "+v"(r6), "+v"(r7));
     }
+    if constexpr (OP == 13) {   // v_pk_fma_f32, 64 per iteration
+      uint64_t q0 = r0, q1 = r1, q2 = r2, q3 = r3;
+      const uint64_t ab = ((uint64_t)b << 32) | a;
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        asm volatile("v_pk_fma_f32 %0, %4, %4, %0\n\tv_pk_fma_f32 %1, %4, %4, %1\n\t"
+                     "v_pk_fma_f32 %2, %4, %4, %2\n\tv_pk_fma_f32 %3, %4, %4, %3\n\t"
+                     "v_pk_fma_f32 %0, %4, %4, %0\n\tv_pk_fma_f32 %1, %4, %4, %1\n\t"
+                     "v_pk_fma_f32 %2, %4, %4, %2\n\tv_pk_fma_f32 %3, %4, %4, %3"
+                     : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3) : "v"(ab));
+      r0 = (uint32_t)q0; r1 = (uint32_t)q1; r2 = (uint32_t)q2; r3 = (uint32_t)q3;
+    }
+    if constexpr (OP == 14) {   // v_cvt_pk_bf16_f32, 64 per iteration
+#pragma unroll
+      for (int u = 0; u < 8; ++u) BODY8("v_cvt_pk_bf16_f32");
+    }
+    if constexpr (OP == 15) {   // v_accvgpr_read_b32, 64 per iteration (8 AGPRs written once)
+      asm volatile("v_accvgpr_write_b32 a0, %0\n\tv_accvgpr_write_b32 a1, %0\n\tv_accvgpr_write_b32 a2, %0\n\t"
+                   "v_accvgpr_write_b32 a3, %0\n\tv_accvgpr_write_b32 a4, %0\n\tv_accvgpr_write_b32 a5, %0\n\t"
+                   "v_accvgpr_write_b32 a6, %0\n\tv_accvgpr_write_b32 a7, %0\n\ts_nop 2" ::"v"(a) : "a0", "a1", "a2", "a3", "a4", "a5", "a6", "a7");
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        asm volatile("v_accvgpr_read_b32 %0, a0\n\tv_accvgpr_read_b32 %1, a1\n\tv_accvgpr_read_b32 %2, a2\n\t"
+                     "v_accvgpr_read_b32 %3, a3\n\tv_accvgpr_read_b32 %4, a4\n\tv_accvgpr_read_b32 %5, a5\n\t"
+                     "v_accvgpr_read_b32 %6, a6\n\tv_accvgpr_read_b32 %7, a7"
+                     : "=v"(r0), "=v"(r1), "=v"(r2), "=v"(r3), "=v"(r4), "=v"(r5), "=v"(r6), "=v"(r7));
+    }
     if constexpr (OP == 12) {   // v_mad_u64_u32, 64 per iteration (4 chains x 2 per BODY)
       uint64_t q0 = r0, q1 = r1, q2 = r2, q3 = r3;
       uint64_t c0, c1, c2, c3;
@@ -107,6 +134,9 @@ extern "C" int ubench(int op, int blocks, int threads, int iters, long long* cyc
     case 10: hipLaunchKernelGGL(ubench_kernel<10>, g, t, 0, 0, iters, 12345u, cyc, sink); break;
     case 11: hipLaunchKernelGGL(ubench_kernel<11>, g, t, 0, 0, iters, 12345u, cyc, sink); break;
     case 12: hipLaunchKernelGGL(ubench_kernel<12>, g, t, 0, 0, iters, 12345u, cyc, sink); break;
+    case 13: hipLaunchKernelGGL(ubench_kernel<13>, g, t, 0, 0, iters, 12345u, cyc, sink); break;
+    case 14: hipLaunchKernelGGL(ubench_kernel<14>, g, t, 0, 0, iters, 12345u, cyc, sink); break;
+    case 15: hipLaunchKernelGGL(ubench_kernel<15>, g, t, 0, 0, iters, 12345u, cyc, sink); break;
     default: return -1;
   }
   return (int)hipGetLastError();

@@ -8,8 +8,9 @@ from pathlib import Path
 import torch
 
 OPS = ["v_add_u32", "v_mul_lo_u32", "v_mul_hi_u32", "v_fma_f32", "v_xor_b32", "v_mad_u64_u32", "v_exp_f32",
-       "v_pk_fma_f32", "v_mul_u32_u24", "v_rcp_f32", "v_fma_f32 x64", "v_exp_f32 x64", "v_mad_u64 x64"]
-PER_ITER = [8] * 10 + [64, 64, 64]      # instructions per loop iteration (the x64 forms amortise the branch)
+       "v_pk_fma_f32", "v_mul_u32_u24", "v_rcp_f32", "v_fma_f32 x64", "v_exp_f32 x64", "v_mad_u64 x64",
+       "v_pk_fma_f32 x64", "v_cvt_pk_bf16 x64", "v_accvgpr_rd x64"]
+PER_ITER = [8] * 10 + [64] * 6      # instructions per loop iteration (the x64 forms amortise the branch)
 
 
 def main():
