@@ -630,10 +630,24 @@ def main():
             gbps = gt["bytes"] / (gt["us"] * 1e-6) / 1e9
             e = {"avg_us": round(gt["us"], 2), "alg_bytes_per_launch": int(gt["bytes"]), "achieved": round(gbps, 1),
                  "peak": PEAK_HBM, "unit": "GB/s", "frac": round(gbps / PEAK_HBM, 4), "what": KERNEL_GROUPS[t],
-                 "timing": "hipGraph replay of back-to-back launches at the step's shapes (kernel + one boundary)"}
+                 "timing": "hipGraph replay of back-to-back launches at the step's shapes (kernel + one boundary)",
+                 "graph_replay": {"avg_us": round(gt["us"], 2), "alg_bytes_per_launch": int(gt["bytes"]),
+                                  "achieved": round(gbps, 1)}}
             if t in ks:
                 e["launches_per_step"] = round(ks[t]["launches"] / probed_steps, 2)
                 e["in_step_event_us"] = round(ks[t]["avg_ms"] * 1e3, 2)   # includes the host's launch gap
+                ib = ks[t].get("bytes_per_launch")
+                if ib and ks[t]["avg_ms"] > 0:
+                    ig = ib / (ks[t]["avg_ms"] * 1e-3) / 1e9
+                    e["in_step"] = {"avg_us": round(ks[t]["avg_ms"] * 1e3, 2), "alg_bytes_per_launch": int(ib),
+                                    "achieved": round(ig, 1)}
+                    # kernels of >= 40 us: the step's own events (its real mix of forms and buffers; the host's
+                    # launch gap is small against them) are the primary figure; back-to-back graph replays of
+                    # one long streaming kernel ran 20-40 % slower than the same kernel in the step
+                    if ks[t]["avg_ms"] * 1e3 >= 40.0:
+                        e.update(avg_us=round(ks[t]["avg_ms"] * 1e3, 2), alg_bytes_per_launch=int(ib),
+                                 achieved=round(ig, 1), frac=round(ig / PEAK_HBM, 4),
+                                 timing="the step's own HIP events on the launch stream (>= 40 us per launch)")
             p = load_profile_json(PMC_FILE, t)
             if p:
                 e.update(traffic=p.get("hbm_bytes_per_launch"), pmc_round=p.get("round"))
