@@ -29,7 +29,7 @@ P_DROP = 0.1
 LOGIT_REL, LOGIT_COS = 2e-3, 0.99999
 LOGIT_REL_PRICONCAT, LOGIT_COS_PRICONCAT = 1.5e-2, 0.99995
 # epsilon 0.1 / 10 (the sweep's ends): logits rel 8.1e-5 / 1.2e-3, worst gradient cos 0.99378 / 0.99488
-GRAD_COS_WORST, GRAD_COS_MEDIAN = 0.99, 0.999
+GRAD_COS_WORST, GRAD_COS_MEDIAN = 0.99, 0.998     # medians measured 0.99908 (B = 512) .. 0.99996
 
 
 def _cos(a, b):
