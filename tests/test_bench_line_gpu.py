@@ -39,4 +39,5 @@ def test_bench_line_contract():
     assert set(hk) == {"fusion_fwd", "fusion_bwd", "cross_entropy", "ln_fwd768", "adam"}
     for t, e in hk.items():
         assert e["unit"] == "GB/s" and e["peak"] == 8000.0 and 0 < e["frac"] < 1, (t, e)
-        assert abs(e["alg_bytes_per_launch"] / (e["avg_us"] * 1e-6) / 1e9 - e["achieved"]) / e["achieved"] < 0.01, t
+        calc = e["alg_bytes_per_launch"] / (e["avg_us"] * 1e-6) / 1e9     # the line rounds GB/s to 0.1
+        assert abs(calc - e["achieved"]) <= max(0.01 * e["achieved"], 0.06), (t, calc, e["achieved"])
