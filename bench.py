@@ -42,7 +42,7 @@ HID, L, C, A = 768, 256, 64, 32
 F_PER_SAMPLE = 46.03e9            # forward GEMM+attention FLOPs per sample, contract W
 PEAK_BF16 = 2500.0                # TFLOP/s dense bf16 MFMA (MI355X_MICROARCH.md)
 METRIC = "samples/sec at batch 256, 64ch×256 EEG + 32-d action, 1/2/4/8 GPUs"
-PMC_FILE = "pmc_r6z.json"          # profiles/: tools/pmc_table.py output (HBM bytes, MFMA busy per group)
+PMC_FILE = "pmc_r6f.json"          # profiles/: tools/pmc_table.py output (HBM bytes, MFMA busy per group)
 # probed kernel groups (HIP events around each launch on the launch stream, engine.probe)
 KERNEL_GROUPS = {
     "ffn1_fwd": "BertIntermediate GEMM + bias + GELU, pass 1 (no save), 65536x3072x768",
