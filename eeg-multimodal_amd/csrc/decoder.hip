@@ -107,7 +107,10 @@ template <typename TV>
 __global__ void __launch_bounds__(64 * XW) xrow_dot_mfma_kernel(const bf16* __restrict__ mem, const TV* __restrict__ vec,
                                                             const float* __restrict__ kbias, int S,
                                                             float* __restrict__ out) {
-  constexpr int LDV = E + 8;
+  // row stride E + 16 (98 bank quads = 2 mod 16): the 16-lane groups of the ds_read_b128 fragment reads
+  // (rows li, chunk g) land on 16 distinct bank quads; E + 8 (1 mod 16) put rows 11 / 12 and 12 / 13 of
+  // a group on one quad (2-way conflicts, 0.44 of the kernel's LDS cycles in r6x_pmc_table.md)
+  constexpr int LDV = E + 16;
   __shared__ __attribute__((aligned(16))) bf16 vt[2][16 * LDV];
   const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, li = lane & 15;
   // 4 consecutive elements per thread and every load of the loop issued before the first LDS store (one
